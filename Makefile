@@ -1,0 +1,33 @@
+# Top-level build: the gfx950 HIP library (the product), the C++ host-API
+# test programs, and the test-only oracle (oracle/Makefile).
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-pass-failed
+INC      := -Iinclude
+
+LIB      := raikv_amd/libkvh.so
+SRCS     := raikv_amd/csrc/kvh.hip
+HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp include/kvh.h include/raikv_amd/key_hash.hpp
+
+CPP_TESTS := tests/cpp/hash_test_gpu
+
+all: $(LIB) oracle cpptests
+
+$(LIB): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(INC) -shared -o $@ $(SRCS)
+
+oracle:
+	$(MAKE) -C oracle
+
+cpptests: $(CPP_TESTS)
+
+tests/cpp/hash_test_gpu: tests/cpp/hash_test_gpu.cpp $(LIB) include/raikv_amd/key_hash.hpp include/kvh.h
+	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
+
+clean:
+	rm -f $(LIB) $(CPP_TESTS)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle cpptests clean

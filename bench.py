@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident 128-bit Meow key-hash throughput on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4]
+
+A "step" is one pass of the hot path (one kvh_meow128_* launch) over one
+batch of synthetic keys already resident in HBM.  Default workload is
+BASELINE.json configs[1] (C1: 100M fixed 16-byte keys per GPU).  For N>1
+(torch.distributed.run, one rank per GPU) every rank hashes its own batch:
+keys are independent, there is no data-path collective ("scaling": "weak");
+a CPU gloo group only carries the barrier and the max-over-ranks time.
+
+The JSON line carries
+  roofline     : algorithmic bytes/launch / avg kernel time (HIP events on
+                 the launch stream) against 8 TB/s HBM; `traffic` from the
+                 committed rocprofv3 PMC summary for this workload, if any;
+  cpu_baseline : the reference CPU path (oracle/_ref: the unmodified
+                 src/key_hash.c kv_hash_meow128) on this box's host cores,
+                 rank 0 at N=1 only, bounded sample; falls back to the
+                 clean-room oracle port if the reference build is absent.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "128-bit key hashes/sec device-resident, 16–64B keys; GB/s vs HBM peak"
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
+
+CONFIGS = {
+    "c1": dict(workload="C1: 100M fixed 16-byte keys resident in HBM, one lane per key, bit-exact vs reference",
+               n=100_000_000, key_len=16, arity=1, var=False),
+    "c2": dict(workload="C2: 100M variable-length keys 8-256B (zipf theta .99 lengths), packed buffer + u64 offsets",
+               n=100_000_000, key_len=0, arity=1, var=True),
+    "c3": dict(workload="C3: cuckoo arity=4 multi-seed, 4 hashes per key over 50M 32B keys",
+               n=50_000_000, key_len=32, arity=4, var=False),
+    "c4": dict(workload="C4: 32-byte keys, 125M per GPU (1B over 8 GPUs), sharded by index range",
+               n=125_000_000, key_len=32, arity=1, var=False),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg, seed, seconds: float):
+    """Reference kv_hash_meow128 on host threads over a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_ref, load_oracle  # test infrastructure: the checker only
+    import ctypes as C
+    threads = max(1, min(16, os.cpu_count() or 1))
+    L = cfg["key_len"] or 16
+    n = 8_000_000
+    rng = np.random.default_rng(42)
+    keys = rng.integers(0, 256, n * L, dtype=np.uint8)
+    out = np.zeros(2 * n, dtype=np.uint64)
+    ref = load_ref()
+    if ref is not None:
+        kind = "reference"
+        run = lambda: ref.ref_bench_fixed(keys.ctypes.data, L, n, C.c_uint64(seed[0]), C.c_uint64(seed[1]),
+                                          out.ctypes.data, threads)
+    else:  # clean-room port (single thread, scalar C)
+        kind = "port"
+        threads = 1
+        orc = load_oracle()
+
+        def run():
+            t = time.perf_counter()
+            orc.orc_batch_fixed(keys.ctypes.data, L, n, C.c_uint64(seed[0]), C.c_uint64(seed[1]),
+                                out.ctypes.data, 0)
+            return time.perf_counter() - t
+    total_t, total_n = 0.0, 0
+    while total_t < seconds:
+        total_t += float(run())
+        total_n += n
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    return {"value": total_n / total_t, "unit": "hash/s", "cores": threads, "kind": kind,
+            "sample": f"{total_n} packed {L}-byte keys ({n} distinct, {total_n // n} passes) x "
+                      f"kv_hash_meow128 (src/key_hash.c), {threads} threads on {model}, {total_t:.1f} s"}
+
+
+def load_traffic(config_name: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    try:
+        d = json.load(open(p))
+        e = d.get(config_name)
+        if e:
+            return float(e["hbm_bytes_per_launch"]), e.get("source")
+    except Exception:
+        pass
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
+    ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time the PCIe-inclusive host pipeline")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane only: barrier + max time
+    torch.cuda.set_device(local)
+    import raikv_amd as kvh
+    from raikv_amd.workload import STATIC_SEED, C3_SEEDS, zipf_lengths, offsets_from_lengths
+
+    cfg = dict(CONFIGS[args.config])
+    if args.keys:
+        cfg["n"] = args.keys
+    n, L, arity = cfg["n"], cfg["key_len"], cfg["arity"]
+    seed = STATIC_SEED
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(1000 + rank)
+
+    # ---- synthetic keys resident in HBM (each rank its own shard)
+    if cfg["var"]:
+        lens = zipf_lengths(n, 8, 256, seed=3 + rank)
+        offs_np = offsets_from_lengths(lens)
+        key_bytes = int(offs_np[-1])
+        keys = torch.randint(0, 256, (key_bytes,), dtype=torch.uint8, device="cuda", generator=gen)
+        offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
+        del lens
+        alg_bytes = key_bytes + 8 * (n + 1) + 16 * n
+        run = lambda out: kvh.meow128_var(keys, offs, seed, out=out)
+    else:
+        key_bytes = n * L
+        keys = torch.randint(0, 256, (key_bytes,), dtype=torch.uint8, device="cuda", generator=gen)
+        alg_bytes = key_bytes + 16 * n * arity
+        if arity == 1:
+            run = lambda out: kvh.meow128_fixed(keys, L, seed, out=out)
+        else:
+            run = lambda out: kvh.meow128_multiseed(keys, L, list(C3_SEEDS[:arity]), out=out)
+    out = torch.empty((n, arity, 2) if arity > 1 else (n, 2), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        run(out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        run(out)
+        b.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    wall_t = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    wall = float(wall_t.item())
+
+    hashes = n * arity * args.steps * world
+    value = hashes / wall
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic, tsrc = load_traffic(args.config)
+    res = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "hash/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded uniform random key bytes generated on device; zipf lengths for C2)",
+        "config": {"workload": cfg["workload"], "config": args.config, "keys_per_gpu": n,
+                   "key_len": L if L else "zipf 8-256", "hashes_per_key": arity,
+                   "seed": ["0x%016x" % seed[0], "0x%016x" % seed[1]],
+                   "parallelism": f"shard x{world} (index ranges, no collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic,
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
+                     "traffic_source": tsrc},
+        "hashes_per_s_per_gpu": n * arity / (kern_ms * 1e-3),
+    }
+    if args.e2e and rank == 0:
+        res["e2e_pcie"] = e2e(kvh, cfg, seed)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            res["cpu_baseline"] = cpu_baseline(cfg, seed, args.cpu_seconds)
+        except Exception as e:  # report, never hide
+            res["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+def e2e(kvh, cfg, seed):
+    """Pinned host keys -> H2D -> kernel -> D2H -> pinned host hashes."""
+    import torch
+    L = cfg["key_len"] or 16
+    n = 50_000_000
+    hk = torch.randint(0, 256, (n * L,), dtype=torch.uint8).pin_memory()
+    ho = torch.empty((n, 2), dtype=torch.int64).pin_memory()
+    kvh.meow128_fixed_host(hk.numpy(), L, seed, out=ho.numpy().view(np.uint64))
+    t = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        kvh.meow128_fixed_host(hk.numpy(), L, seed, out=ho.numpy().view(np.uint64))
+    dt = (time.perf_counter() - t) / reps
+    return {"hash_per_s": n / dt, "GB_per_s_h2d_plus_d2h": n * (L + 16) / dt / 1e9, "keys": n, "key_len": L,
+            "note": "pinned host buffers, chunked 3-stream H2D/kernel/D2H pipeline (kvh_meow128_fixed_host)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+/*
+ * kvh.h -- C-ABI of the MI355X (gfx950) batched key-hash engine: raikv's
+ * 128-bit Meow-derived AES-round key hash (kv_hash_meow128 and family) as
+ * hand-written HIP kernels.
+ *
+ * Plain C: no HIP, torch or C++ types in any signature.  `stream` is a
+ * hipStream_t passed as void* (NULL = the null stream).  Device entry points
+ * are asynchronous on `stream`; caller owns every buffer; nothing is
+ * allocated in a hot call.
+ *
+ * Semantics follow the reference (/root/reference):
+ *   - (h1,h2) are "the seed and the hash result" (include/raikv/key_hash.h:41)
+ *   - batch outputs interleave (h1,h2) per key exactly like the reference's
+ *     x[] arrays of the x2/x4/x8 variants (key_hash.c:1657-2020)
+ *   - KVH_FIXUP applies KeyFragment::hash's epilogue to h1
+ *     (include/raikv/hash_entry.h:84-85): clear bit 63, 0/1 -> 2.
+ *
+ * Error convention (new: the reference has no error path, key_hash.h
+ * functions are void): 0 on success, negative on failure; HIP runtime
+ * errors are returned as KVH_EHIP_BASE - hipError_t.
+ */
+#ifndef KVH_H
+#define KVH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KVH_OK          0
+#define KVH_EINVAL    (-22)
+#define KVH_ENOMEM    (-12)
+#define KVH_ENODEV    (-19)
+#define KVH_EHIP_BASE (-1000)
+
+/* flags */
+#define KVH_FIXUP     0x1u  /* KeyFragment::hash epilogue on h1 (hash_entry.h:84-85) */
+
+#define KVH_MAX_ARITY 8
+
+/* ---------------------------------------------------------------------
+ * Batched device entry points (the hot path).  keys/offsets/out are device
+ * pointers (hipMalloc'd or host-registered).  Output layout is
+ * out[(i*arity + a)*2 + 0] = h1, [.. + 1] = h2.
+ * ------------------------------------------------------------------- */
+
+/* n keys of key_len bytes packed at stride key_len.  Replaces n calls of
+ * kv_hash_meow128(p + i*key_len, key_len, &h1, &h2) with h1,h2 = seed1,seed2
+ * (reference key_hash.c:1413-1429, key_hash.h:61) and generalises
+ * kv_hash_meow128_{2,4,8}_same_length (key_hash.c:1657, :1846, :1946). */
+int kvh_meow128_fixed(const void *keys, uint32_t key_len, size_t n,
+                      uint64_t seed1, uint64_t seed2, uint64_t *out,
+                      uint32_t flags, void *stream);
+
+/* n variable-length keys, key i = keys[offsets[i] .. offsets[i+1]) with
+ * 64-bit offsets (n+1 entries, non-decreasing).  Generalises
+ * kv_hash_meow128_{2,4}_diff_length (key_hash.c:1685, :1740). */
+int kvh_meow128_var(const void *keys, const uint64_t *offsets, size_t n,
+                    uint64_t seed1, uint64_t seed2, uint64_t *out,
+                    uint32_t flags, void *stream);
+
+/* Each key hashed under `arity` seeds (seeds = HOST array of 2*arity
+ * words, seed k = (seeds[2k], seeds[2k+1])).  With arity 4 this is the
+ * reference's kv_hash_meow128_4_same_length_4_seed with one key in all four
+ * slots (key_hash.c:1891-1937); it feeds cuckoo slotting (config C3). */
+int kvh_meow128_multiseed(const void *keys, uint32_t key_len, size_t n,
+                          const uint64_t *seeds, uint32_t arity,
+                          uint64_t *out, uint32_t flags, void *stream);
+
+/* One entry point for all of the above (SURVEY.md §8 b): offsets == NULL
+ * selects fixed length `fixed_len`; arity > 1 requires offsets == NULL. */
+int kvh_meow128_batch(const void *keys, const uint64_t *offsets,
+                      uint32_t fixed_len, size_t n, const uint64_t *seeds,
+                      uint32_t arity, uint64_t *out, uint32_t flags,
+                      void *stream);
+
+/* Device-resident batch through the straight-line (unfolded) restatement
+ * with per-key seeds (seeds = DEVICE array, 2 words per key); this is the
+ * kernel behind the host drop-ins below and the x2/x4/x8 variants. */
+int kvh_meow128_var_seeded(const void *keys, const uint64_t *offsets,
+                           size_t n, const uint64_t *seeds, uint64_t *out,
+                           uint32_t flags, void *stream);
+
+/* ---------------------------------------------------------------------
+ * Host-buffer pipeline: keys and out in (pageable or pinned) host memory;
+ * chunked, double-buffered H2D -> kernel -> D2H through pinned staging on
+ * the current device.  Synchronous.  This is the PCIe-inclusive path
+ * (keys arrive from a socket / shm segment, hashes feed the cuckoo probe).
+ * ------------------------------------------------------------------- */
+int kvh_meow128_fixed_host(const void *keys, uint32_t key_len, size_t n,
+                           uint64_t seed1, uint64_t seed2, uint64_t *out,
+                           uint32_t flags);
+
+/* ---------------------------------------------------------------------
+ * Drop-ins for include/raikv/key_hash.h (host pointers, synchronous).  They
+ * execute on the current GPU through kvh_meow128_var_seeded; results are
+ * bit-identical to the reference.  Return 0 or a negative error.
+ * ------------------------------------------------------------------- */
+/* key_hash.h:61 kv_hash_meow128 */
+int kvh_hash_meow128(const void *p, size_t sz, uint64_t *h1, uint64_t *h2);
+/* key_hash.h:60 kv_hash_meow64 (returns h1; errors via kvh_last_error) */
+uint64_t kvh_hash_meow64(const void *p, size_t sz, uint64_t seed);
+/* key_hash.h:104-105 */
+int kvh_hash_meow128_2_same_length(const void *p, const void *p2, size_t sz,
+                                   uint64_t *x4);
+/* key_hash.h:106 */
+int kvh_hash_meow128_4_same_length_a(const void **p, size_t sz, uint64_t *x);
+/* key_hash.h:107 */
+int kvh_hash_meow128_8_same_length_a(const void **p, size_t sz, uint64_t *x);
+/* key_hash.h:108-110 */
+int kvh_hash_meow128_4_same_length(const void *p, const void *p2,
+                                   const void *p3, const void *p4, size_t sz,
+                                   uint64_t *x);
+/* key_hash.h:112-114 */
+int kvh_hash_meow128_4_same_length_4_seed(const void *p, const void *p2,
+                                          const void *p3, const void *p4,
+                                          size_t sz, uint64_t *x);
+/* key_hash.h:115-119 */
+int kvh_hash_meow128_8_same_length(const void *p, const void *p2,
+                                   const void *p3, const void *p4,
+                                   const void *p5, const void *p6,
+                                   const void *p7, const void *p8, size_t sz,
+                                   uint64_t *x);
+/* key_hash.h:120-121 */
+int kvh_hash_meow128_2_diff_length(const void *p, size_t sz, const void *p2,
+                                   size_t sz2, uint64_t *x);
+/* key_hash.h:122-124 */
+int kvh_hash_meow128_4_diff_length(const void *p, size_t sz, const void *p2,
+                                   size_t sz2, const void *p3, size_t sz3,
+                                   const void *p4, size_t sz4, uint64_t *x);
+
+/* key_hash.h:85-92 meow_vec_t / kv_hash_meow128_vec */
+typedef struct {
+  const void *p;
+  size_t      sz;
+} kvh_meow_vec_t;
+int kvh_hash_meow128_vec(const kvh_meow_vec_t *vec, size_t vec_sz,
+                         uint64_t *h1, uint64_t *h2);
+
+/* key_hash.h:67-83, :93-99 streaming hash; same layout as meow_ctx_t /
+ * meow_block_t.  total_update_sz must be known at init (the Mixer uses it). */
+typedef struct {
+  uint64_t ctx[8];
+} kvh_meow_ctx_t __attribute__((__aligned__(64)));
+typedef struct {
+  uint8_t block[64];
+  size_t  off, total_update_sz;
+} kvh_meow_block_t __attribute__((__aligned__(64)));
+
+int kvh_meow128_init(kvh_meow_ctx_t *m, kvh_meow_block_t *b, uint64_t k1,
+                     uint64_t k2, size_t total_update_sz);
+int kvh_meow128_update(kvh_meow_ctx_t *m, kvh_meow_block_t *b, const void *p,
+                       size_t sz);
+int kvh_meow128_final(kvh_meow_ctx_t *m, kvh_meow_block_t *b, uint64_t *k1,
+                      uint64_t *k2);
+/* key_hash.c:1570-1579 kv_meow_test: streaming == one-shot */
+int kvh_meow_test(const void *p, size_t sz, uint64_t *k1, uint64_t *k2);
+
+/* ---------------------------------------------------------------------
+ * Key fragments (include/raikv/hash_entry.h:28-36, key_ctx.cpp:1737-1783).
+ * kvh_key_frag_t is layout-identical to kv_key_frag_t (u16 keylen + bytes).
+ * ------------------------------------------------------------------- */
+typedef struct {
+  uint16_t keylen;
+  char     buf[4]; /* keylen bytes follow in place, like kv_key_frag_s */
+} kvh_key_frag_t;
+
+/* KeyFragment::hash with a HashSeed (shm_ht.h:338-341, hash_entry.h:80-86):
+ * seed in (seed[0], seed[1]) -> fixed-up (k, k2).  kv_hash_key_frag
+ * (key_ctx.cpp:1774-1783) is this with the db-0 seed of the table. */
+int kvh_hash_key_frag(const uint64_t seed[2], const kvh_key_frag_t *frag,
+                      uint64_t *k, uint64_t *k2);
+/* Batch form for a ctest-style pipeline (test/ctest.c:76-104): n fragments
+ * (host pointers) hashed with one seed, fixed-up, into out[2n]. */
+int kvh_hash_key_frags(const uint64_t seed[2], const kvh_key_frag_t *const *frags,
+                       size_t n, uint64_t *out);
+
+/* ---------------------------------------------------------------------
+ * Runtime / diagnostics
+ * ------------------------------------------------------------------- */
+int         kvh_last_error(void);
+const char *kvh_strerror(int err);
+/* engine version string */
+const char *kvh_version(void);
+/* synchronise the current device (host wall-clock timing helpers) */
+int         kvh_device_synchronize(void);
+/* expert tuning knobs (bench/ablation): 0 = tables-per-LDS (2 or 4),
+ * 1 = workgroups per CU multiplier, 2 = force generic kernel (0/1).
+ * Returns the previous value or KVH_EINVAL. */
+int         kvh_set_tuning(int knob, int value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KVH_H */

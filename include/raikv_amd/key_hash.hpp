@@ -1,0 +1,127 @@
+// raikv_amd/key_hash.hpp -- C++ host mirror of raikv's key-fragment hashing
+// API over the C-ABI in kvh.h.  Same names and argument meaning as the
+// reference (/root/reference/include/raikv/hash_entry.h:56-112,
+// key_buf.h:14-110, shm_ht.h:333-351) so existing call sites port by
+// changing the namespace; every hash executes on the GPU.
+//
+// Error behaviour: the reference functions are void and total; here a
+// device/runtime failure throws kvh::Error (the product has no CPU path to
+// fall back to).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+#include <stdexcept>
+#include <string>
+#include <vector>
+#include "../kvh.h"
+
+namespace kvh {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(const char* what, int rc)
+      : std::runtime_error(std::string(what) + ": " + kvh_strerror(rc)), code(rc) {}
+};
+
+inline void check(int rc, const char* what) {
+  if (rc != 0) throw Error(what, rc);
+}
+
+// hash_entry.h:46-50
+static const uint64_t ZOMBIE64 = (uint64_t)0x80000000 << 32, DROPPED_HASH = 1;
+static const size_t KEY_FRAG_SIZE = 6;
+
+// hash_entry.h:28-36 kv_key_frag_t: u16 keylen + bytes (layout-identical)
+struct KeyFragment {
+  uint16_t keylen;
+  union {
+    char buf[4];
+    struct { uint16_t b1, b2; } x;
+  } u;
+
+  // KeyFragment::hash (hash_entry.h:80-86): Meow128 with (seed, seed2) in,
+  // hash out, then h1 &= ~ZOMBIE64, h1 <= 1 -> 2.
+  void hash(uint64_t& seed, uint64_t& seed2) const {
+    const uint64_t s[2] = {seed, seed2};
+    check(kvh_hash_key_frag(s, reinterpret_cast<const kvh_key_frag_t*>(this), &seed, &seed2),
+          "KeyFragment::hash");
+  }
+  // hash_entry.h:87-96: two keys, one seed in seed[0..1], out seed[0..3]
+  static void hash2(KeyFragment& kb, KeyFragment& kb2, uint64_t* seed) {
+    const kvh_key_frag_t* f[2] = {reinterpret_cast<const kvh_key_frag_t*>(&kb),
+                                  reinterpret_cast<const kvh_key_frag_t*>(&kb2)};
+    const uint64_t s[2] = {seed[0], seed[1]};
+    check(kvh_hash_key_frags(s, f, 2, seed), "KeyFragment::hash2");
+  }
+  // hash_entry.h:97-111: four keys
+  static void hash4(KeyFragment& kb, KeyFragment& kb2, KeyFragment& kb3, KeyFragment& kb4,
+                    uint64_t* seed) {
+    const kvh_key_frag_t* f[4] = {
+        reinterpret_cast<const kvh_key_frag_t*>(&kb), reinterpret_cast<const kvh_key_frag_t*>(&kb2),
+        reinterpret_cast<const kvh_key_frag_t*>(&kb3), reinterpret_cast<const kvh_key_frag_t*>(&kb4)};
+    const uint64_t s[2] = {seed[0], seed[1]};
+    check(kvh_hash_key_frags(s, f, 4, seed), "KeyFragment::hash4");
+  }
+};
+
+// key_buf.h:14-60 KeyBufT<N>: a KeyFragment with room for N-2 key bytes
+template <uint16_t KEY_SIZE>
+struct KeyBufT : public KeyFragment {
+  static const uint16_t MAX_BUF_SIZE = KEY_SIZE - 2;
+  char morebuf[KEY_SIZE - KEY_FRAG_SIZE];
+
+  KeyBufT() { this->keylen = 0; }
+  KeyBufT(const char* s) { this->set_string(s); }
+  // includes the trailing NUL, like the reference (key_buf.h:29-31)
+  void set_string(const char* s) { this->copy(s, ::strnlen(s, MAX_BUF_SIZE) + 1); }
+  template <class T> void set(T arg) { this->copy((const void*)&arg, sizeof(T)); }
+  uint16_t copy(const void* p, size_t len) {
+    if (len > MAX_BUF_SIZE) len = MAX_BUF_SIZE;
+    ::memcpy(this->u.buf, p, len);
+    this->keylen = (uint16_t)len;
+    return (uint16_t)len;
+  }
+  void zero(void) { ::memset((void*)this, 0, sizeof(*this)); }
+};
+typedef KeyBufT<128> KeyBuf;
+
+// shm_ht.h:333-351 HashSeed
+struct HashSeed {
+  uint64_t hash1, hash2;
+  void get(uint64_t& h1, uint64_t& h2) const { h1 = this->hash1; h2 = this->hash2; }
+  void hash(KeyFragment& kb, uint64_t& h1, uint64_t& h2) const {
+    h1 = this->hash1; h2 = this->hash2;
+    kb.hash(h1, h2);
+  }
+  void hash(KeyFragment& kb, KeyFragment& kb2, uint64_t* h) const {
+    h[0] = this->hash1; h[1] = this->hash2;
+    KeyFragment::hash2(kb, kb2, h);
+  }
+  void hash(KeyFragment& kb, KeyFragment& kb2, KeyFragment& kb3, KeyFragment& kb4, uint64_t* h) const {
+    h[0] = this->hash1; h[1] = this->hash2;
+    KeyFragment::hash4(kb, kb2, kb3, kb4, h);
+  }
+};
+
+// ---- batched device API (the hot path), C++ shape over kvh.h
+// Fixed-length keys packed at stride key_len, device pointers, async on stream.
+inline void hash_fixed(const void* keys, uint32_t key_len, size_t n, const HashSeed& hs, uint64_t* out,
+                       bool fixup = true, void* stream = nullptr) {
+  check(kvh_meow128_fixed(keys, key_len, n, hs.hash1, hs.hash2, out, fixup ? KVH_FIXUP : 0u, stream),
+        "kvh::hash_fixed");
+}
+inline void hash_var(const void* keys, const uint64_t* offsets, size_t n, const HashSeed& hs, uint64_t* out,
+                     bool fixup = true, void* stream = nullptr) {
+  check(kvh_meow128_var(keys, offsets, n, hs.hash1, hs.hash2, out, fixup ? KVH_FIXUP : 0u, stream),
+        "kvh::hash_var");
+}
+inline void hash_multiseed(const void* keys, uint32_t key_len, size_t n, const std::vector<HashSeed>& seeds,
+                           uint64_t* out, bool fixup = false, void* stream = nullptr) {
+  std::vector<uint64_t> s;
+  for (const HashSeed& h : seeds) { s.push_back(h.hash1); s.push_back(h.hash2); }
+  check(kvh_meow128_multiseed(keys, key_len, n, s.data(), (uint32_t)seeds.size(), out,
+                              fixup ? KVH_FIXUP : 0u, stream),
+        "kvh::hash_multiseed");
+}
+
+}  // namespace kvh

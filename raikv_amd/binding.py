@@ -1,0 +1,241 @@
+"""ctypes binding of libkvh.so (include/kvh.h) + small Python mirrors of
+raikv's key-fragment API (hash_entry.h:56-112, shm_ht.h:333-351).
+
+Device buffers are torch tensors on a ROCm device; the kernels run on the
+caller's current torch stream (or an explicit `stream`).  torch is imported
+before libkvh.so is loaded so that one HIP runtime serves both.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+
+try:  # torch first: one HIP runtime per process
+    import torch
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+KVH_FIXUP = 0x1
+KVH_MAX_ARITY = 8
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+lib_path = os.path.join(_HERE, "libkvh.so")
+
+U64 = C.c_uint64
+U32 = C.c_uint32
+SZ = C.c_size_t
+P = C.c_void_p
+I = C.c_int
+
+
+class KvhError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(lib_path):
+        raise ImportError(
+            f"raikv_amd: HIP library {lib_path} is missing; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` or `make`")
+    lib = C.CDLL(lib_path)
+    sig = {
+        "kvh_meow128_fixed": (I, [P, U32, SZ, U64, U64, P, U32, P]),
+        "kvh_meow128_var": (I, [P, P, SZ, U64, U64, P, U32, P]),
+        "kvh_meow128_multiseed": (I, [P, U32, SZ, P, U32, P, U32, P]),
+        "kvh_meow128_batch": (I, [P, P, U32, SZ, P, U32, P, U32, P]),
+        "kvh_meow128_var_seeded": (I, [P, P, SZ, P, P, U32, P]),
+        "kvh_meow128_fixed_host": (I, [P, U32, SZ, U64, U64, P, U32]),
+        "kvh_hash_meow128": (I, [P, SZ, C.POINTER(U64), C.POINTER(U64)]),
+        "kvh_hash_meow64": (U64, [P, SZ, U64]),
+        "kvh_hash_meow128_2_same_length": (I, [P, P, SZ, P]),
+        "kvh_hash_meow128_2_diff_length": (I, [P, SZ, P, SZ, P]),
+        "kvh_hash_meow128_4_same_length": (I, [P, P, P, P, SZ, P]),
+        "kvh_hash_meow128_4_same_length_a": (I, [P, SZ, P]),
+        "kvh_hash_meow128_4_same_length_4_seed": (I, [P, P, P, P, SZ, P]),
+        "kvh_hash_meow128_4_diff_length": (I, [P, SZ, P, SZ, P, SZ, P, SZ, P]),
+        "kvh_hash_meow128_8_same_length": (I, [P, P, P, P, P, P, P, P, SZ, P]),
+        "kvh_hash_meow128_8_same_length_a": (I, [P, SZ, P]),
+        "kvh_hash_meow128_vec": (I, [P, SZ, C.POINTER(U64), C.POINTER(U64)]),
+        "kvh_meow128_init": (I, [P, P, U64, U64, SZ]),
+        "kvh_meow128_update": (I, [P, P, P, SZ]),
+        "kvh_meow128_final": (I, [P, P, C.POINTER(U64), C.POINTER(U64)]),
+        "kvh_meow_test": (I, [P, SZ, C.POINTER(U64), C.POINTER(U64)]),
+        "kvh_hash_key_frag": (I, [P, P, C.POINTER(U64), C.POINTER(U64)]),
+        "kvh_hash_key_frags": (I, [P, P, SZ, P]),
+        "kvh_last_error": (I, []),
+        "kvh_strerror": (C.c_char_p, [I]),
+        "kvh_version": (C.c_char_p, []),
+        "kvh_device_synchronize": (I, []),
+        "kvh_set_tuning": (I, [I, I]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = "kvh") -> None:
+    if rc != 0:
+        msg = lib.kvh_strerror(rc)
+        raise KvhError(f"{what} failed: {rc} ({msg.decode() if msg else '?'})")
+
+
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is not None:
+        return int(getattr(stream, "cuda_stream", stream))
+    if torch is not None and torch.cuda.is_available():
+        return int(torch.cuda.current_stream().cuda_stream)
+    return None
+
+
+def _dev_ptr(t) -> int:
+    if not t.is_cuda:
+        raise KvhError("expected a device tensor")
+    if not t.is_contiguous():
+        raise KvhError("expected a contiguous tensor")
+    return int(t.data_ptr())
+
+
+def _new_out(shape, like):
+    return torch.empty(shape, dtype=torch.int64, device=like.device)
+
+
+# --------------------------------------------------------------- batches
+def meow128_fixed(keys, key_len: int, seed: Tuple[int, int], out=None, fixup: bool = False,
+                  stream=None, n: Optional[int] = None):
+    """keys: uint8 device tensor of n*key_len bytes -> int64 [n, 2] (h1, h2 bits)."""
+    if n is None:
+        n = keys.numel() // key_len if key_len else 0
+    if out is None:
+        out = _new_out((n, 2), keys)
+    check(lib.kvh_meow128_fixed(_dev_ptr(keys) if keys.numel() else None, key_len, n,
+                                U64(seed[0] & (2**64 - 1)), U64(seed[1] & (2**64 - 1)),
+                                _dev_ptr(out) if n else None, KVH_FIXUP if fixup else 0,
+                                _stream_ptr(stream)), "kvh_meow128_fixed")
+    return out
+
+
+def meow128_var(keys, offsets, seed: Tuple[int, int], out=None, fixup: bool = False, stream=None):
+    """keys: uint8 device tensor; offsets: int64 device tensor [n+1] -> int64 [n, 2]."""
+    n = offsets.numel() - 1
+    if out is None:
+        out = _new_out((n, 2), offsets)
+    check(lib.kvh_meow128_var(_dev_ptr(keys) if keys.numel() else _dev_ptr(offsets),
+                              _dev_ptr(offsets), n, U64(seed[0] & (2**64 - 1)),
+                              U64(seed[1] & (2**64 - 1)), _dev_ptr(out) if n else None,
+                              KVH_FIXUP if fixup else 0, _stream_ptr(stream)), "kvh_meow128_var")
+    return out
+
+
+def meow128_multiseed(keys, key_len: int, seeds: Sequence[Tuple[int, int]], out=None,
+                      fixup: bool = False, stream=None):
+    """Each key hashed under every seed -> int64 [n, arity, 2]."""
+    n = keys.numel() // key_len
+    a = len(seeds)
+    sv = (U64 * (2 * a))(*[int(x) & (2**64 - 1) for s in seeds for x in s])
+    if out is None:
+        out = _new_out((n, a, 2), keys)
+    check(lib.kvh_meow128_multiseed(_dev_ptr(keys), key_len, n, sv, a, _dev_ptr(out),
+                                    KVH_FIXUP if fixup else 0, _stream_ptr(stream)),
+          "kvh_meow128_multiseed")
+    return out
+
+
+def meow128_var_seeded(keys, offsets, seeds, out=None, fixup: bool = False, stream=None):
+    """Per-key seeds (int64 device tensor [n, 2]) through the straight-line kernel."""
+    n = offsets.numel() - 1
+    if out is None:
+        out = _new_out((n, 2), offsets)
+    check(lib.kvh_meow128_var_seeded(_dev_ptr(keys), _dev_ptr(offsets), n, _dev_ptr(seeds),
+                                     _dev_ptr(out), KVH_FIXUP if fixup else 0,
+                                     _stream_ptr(stream)), "kvh_meow128_var_seeded")
+    return out
+
+
+def meow128_fixed_host(keys: np.ndarray, key_len: int, seed: Tuple[int, int],
+                       out: Optional[np.ndarray] = None, fixup: bool = False) -> np.ndarray:
+    """Host keys -> host hashes through the chunked H2D/kernel/D2H pipeline."""
+    n = keys.size // key_len
+    if out is None:
+        out = np.empty((n, 2), dtype=np.uint64)
+    check(lib.kvh_meow128_fixed_host(keys.ctypes.data, key_len, n, U64(seed[0]), U64(seed[1]),
+                                     out.ctypes.data, KVH_FIXUP if fixup else 0),
+          "kvh_meow128_fixed_host")
+    return out
+
+
+# ------------------------------------------------------------- drop-ins
+def kv_hash_meow128(data: bytes, h1: int, h2: int) -> Tuple[int, int]:
+    """key_hash.h:61 semantics: (h1, h2) are the seed in and the hash out."""
+    a, b = U64(h1 & (2**64 - 1)), U64(h2 & (2**64 - 1))
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    check(lib.kvh_hash_meow128(buf, len(data), C.byref(a), C.byref(b)), "kvh_hash_meow128")
+    return a.value, b.value
+
+
+def kv_hash_meow64(data: bytes, seed: int) -> int:
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    return int(lib.kvh_hash_meow64(buf, len(data), U64(seed & (2**64 - 1))))
+
+
+class HashSeed:
+    """shm_ht.h:333-351 HashSeed: a per-db 128-bit seed."""
+
+    def __init__(self, hash1: int, hash2: int):
+        self.hash1, self.hash2 = hash1 & (2**64 - 1), hash2 & (2**64 - 1)
+
+    def hash(self, kb: "KeyFragment") -> Tuple[int, int]:
+        return kb.hash(self.hash1, self.hash2)
+
+    def hash_batch(self, frags: Iterable["KeyFragment"]) -> np.ndarray:
+        frags = list(frags)
+        return KeyFragment.hash_many(frags, self.hash1, self.hash2)
+
+
+class KeyFragment:
+    """hash_entry.h:56-112 KeyFragment: u16 keylen + bytes."""
+
+    def __init__(self, data: bytes):
+        if len(data) > 0xFFFF:
+            raise ValueError("keylen is a u16")
+        self.data = bytes(data)
+
+    @classmethod
+    def from_string(cls, s: str) -> "KeyFragment":
+        """KeyBufT::set_string / kv_set_key_frag_string: includes the NUL."""
+        return cls(s.encode() + b"\0")
+
+    def _raw(self):
+        raw = C.create_string_buffer(2 + len(self.data) + 4)
+        C.memmove(raw, len(self.data).to_bytes(2, "little") + self.data, 2 + len(self.data))
+        return raw
+
+    def hash(self, seed: int, seed2: int) -> Tuple[int, int]:
+        """KeyFragment::hash: Meow128 then the ZOMBIE/reserved fixup on h1."""
+        sv = (U64 * 2)(seed & (2**64 - 1), seed2 & (2**64 - 1))
+        k, k2 = U64(), U64()
+        check(lib.kvh_hash_key_frag(sv, self._raw(), C.byref(k), C.byref(k2)), "kvh_hash_key_frag")
+        return k.value, k2.value
+
+    @staticmethod
+    def hash_many(frags: Sequence["KeyFragment"], seed: int, seed2: int) -> np.ndarray:
+        sv = (U64 * 2)(seed & (2**64 - 1), seed2 & (2**64 - 1))
+        raws = [f._raw() for f in frags]
+        arr = (P * max(1, len(raws)))(*[C.cast(r, P) for r in raws])
+        out = np.empty((len(frags), 2), dtype=np.uint64)
+        check(lib.kvh_hash_key_frags(sv, arr, len(frags), out.ctypes.data), "kvh_hash_key_frags")
+        return out
+
+
+def as_u64(t) -> np.ndarray:
+    """int64 device/host tensor -> numpy uint64 view."""
+    if torch is not None and isinstance(t, torch.Tensor):
+        t = t.detach().cpu().numpy()
+    return np.ascontiguousarray(t).view(np.uint64)

@@ -1,0 +1,766 @@
+// kvh.hip -- gfx950 kernels and the C-ABI (include/kvh.h) of the batched
+// Meow128 key-hash engine.  See DESIGN.md for the data layout in HBM, the
+// kernels' rooflines and the folding argument; meow_dev.hpp for the round.
+//
+// Kernels
+//   k_fixed<L,NT,A16>     fixed length L in {8,16,..,64}, one seed, constants
+//                         folded at compile time into SGPRs (configs C1, C4)
+//   k_fixed_ms<L,NT,A16>  same, `arity` seeds per key (config C3)
+//   k_generic<VAR,NT>     any length: fixed stride or u64 offsets (config C2)
+//   k_seeded              straight-line restatement, per-key seeds, constant
+//                         memory tables (drop-ins, x2/x4/x8 variants)
+//   k_stream_*            streaming init/update/final state transitions
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <mutex>
+#include <vector>
+#include <algorithm>
+#include "meow_dev.hpp"
+#include "../../include/kvh.h"
+
+using namespace kvh;
+
+#ifndef KVH_VERSION
+#define KVH_VERSION "raikv_amd-kvh 0.1 (gfx950)"
+#endif
+
+namespace {
+
+constexpr int kBlock = 1024;          // threads per workgroup (16 waves)
+constexpr int kLT = 64;               // full per-length constant records (L < 64)
+constexpr int kNF = 256;              // F-only records for 64 <= L < 64 + kNF
+
+// ------------------------------------------------------------ helpers
+template <int L, bool A16>
+__device__ __forceinline__ void load_fixed(const uint8_t* __restrict__ p, Blk* D) {
+  constexpr int NC = Plan<L>::NC;
+  if constexpr (A16 && (L % 16) == 0) {
+#pragma unroll
+    for (int j = 0; j < NC; j++) {
+      const uint4 v = *(const uint4*)(p + 16 * j);
+      D[j].w[0] = v.x; D[j].w[1] = v.y; D[j].w[2] = v.z; D[j].w[3] = v.w;
+    }
+  } else {
+    // L % 8 == 0 and 8-byte aligned rows
+#pragma unroll
+    for (int j = 0; j < L / 8; j++) {
+      const uint2 v = *(const uint2*)(p + 8 * j);
+      D[j / 2].w[(j & 1) * 2 + 0] = v.x;
+      D[j / 2].w[(j & 1) * 2 + 1] = v.y;
+    }
+    if constexpr ((L % 16) == 8) { D[NC - 1].w[2] = 0; D[NC - 1].w[3] = 0; }
+  }
+}
+
+__device__ __forceinline__ void store_h(uint64_t* __restrict__ out, uint64_t idx, Blk h, bool fix) {
+  if (fix) h = fixup(h);
+  uint4 v; v.x = h.w[0]; v.y = h.w[1]; v.z = h.w[2]; v.w = h.w[3];
+  *(uint4*)(out + 2 * idx) = v;
+}
+
+// ------------------------------------------------------------ kernels
+template <int L, int NT, bool A16>
+__global__ void __launch_bounds__(kBlock)
+k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
+        uint64_t* __restrict__ out, uint32_t flags) {
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Blk D[Plan<L>::NC];
+  load_fixed<L, A16>(keys + i * L, D);
+  for (;;) {
+    const uint64_t nx = i + stride;
+    Blk E[Plan<L>::NC];
+    const bool more = nx < n;
+    if (more) load_fixed<L, A16>(keys + nx * L, E);  // prefetch next key
+    const Blk h = meow_ct<L>(D, K, T);
+    store_h(out, i, h, fix);
+    if (!more) break;
+#pragma unroll
+    for (int j = 0; j < Plan<L>::NC; j++) D[j] = E[j];
+    i = nx;
+  }
+}
+
+template <int L, int NT, bool A16>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_ms(const uint8_t* __restrict__ keys, uint64_t n, const uint64_t* __restrict__ seeds_unused,
+           uint64_t* __restrict__ out, uint32_t flags, uint32_t arity,
+           uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2,
+           uint64_t a3, uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5,
+           uint64_t a6, uint64_t b6, uint64_t a7, uint64_t b7) {
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ MeowConst kc[KVH_MAX_ARITY];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  if (threadIdx.x < KVH_MAX_ARITY && threadIdx.x < arity) {
+    const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
+    const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
+    kc[threadIdx.x] = make_const(sa[threadIdx.x], sb[threadIdx.x], (uint64_t)L, T);
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    Blk D[Plan<L>::NC];
+    load_fixed<L, A16>(keys + i * L, D);
+    for (uint32_t a = 0; a < arity; a++) {
+      const MeowConst K = uniform(kc[a]);
+      store_h(out, i * arity + a, meow_ct<L>(D, K, T), fix);
+    }
+  }
+}
+
+// per-lane constants for variable-length batches, from LDS records
+template <class Tab>
+struct LdsK {
+  const MeowConst* full;   // [kLT]
+  const Blk* ftab;         // [kNF][4]
+  uint32_t L;
+  Blk m;
+  const Tab& T;
+  __device__ __forceinline__ LdsK(const MeowConst* f, const Blk* ft, uint32_t len, uint64_t s1,
+                                  uint64_t s2, const Tab& t)
+      : full(f), ftab(ft), L(len), m(mixer(s1, s2, len)), T(t) {}
+  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ Blk M() const { return m; }
+  __device__ __forceinline__ Blk F(int i) const {
+    if (L < (uint32_t)kLT) return full[L].F[i];
+    if (L < (uint32_t)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
+    return aesT(bxor(ramp(i), m), T);
+  }
+  __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
+  __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
+  __device__ __forceinline__ Blk CS2b() const { return full[li()].CS2b; }
+  __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
+};
+
+// Any length.  VAR: key i = keys[offs[i], offs[i+1]) with per-lane length;
+// !VAR: stride = fixed_len, every lane the same length, `arity` seeds.
+template <bool VAR, int NT>
+__global__ void __launch_bounds__(kBlock)
+k_generic(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t fixed_len,
+          uint64_t n, uint64_t* __restrict__ out, uint32_t flags, uint32_t arity,
+          uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2,
+          uint64_t a3, uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5,
+          uint64_t a6, uint64_t b6, uint64_t a7, uint64_t b7) {
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ MeowConst kfull[VAR ? kLT : KVH_MAX_ARITY];
+  __shared__ Blk kf[VAR ? kNF * 4 : 1];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  if constexpr (VAR) {
+    for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + kNF); l += blockDim.x) {
+      if (l < (uint32_t)kLT) {
+        kfull[l] = make_const(a0, b0, l, T);
+      } else {
+        const Blk M = mixer(a0, b0, l);
+#pragma unroll
+        for (int s = 0; s < 4; s++) kf[(l - kLT) * 4 + s] = aesT(bxor(ramp(s), M), T);
+      }
+    }
+  } else {
+    if (threadIdx.x < arity) {
+      const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
+      const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
+      kfull[threadIdx.x] = make_const(sa[threadIdx.x], sb[threadIdx.x], fixed_len, T);
+    }
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if constexpr (VAR) {
+      const uint64_t o0 = offs[i], o1 = offs[i + 1];
+      const uint32_t L = (uint32_t)(o1 - o0);
+      const LdsK<LdsTab<NT>> K(kfull, kf, L, a0, b0, T);
+      store_h(out, i, meow_rt(keys + o0, L, K, T), fix);
+    } else {
+      const uint8_t* p = keys + i * (uint64_t)fixed_len;
+      for (uint32_t a = 0; a < arity; a++) {
+        const MeowConst Kc = uniform(kfull[a]);
+        const RegK K{Kc};
+        store_h(out, i * arity + a, meow_rt(p, fixed_len, K, T), fix);
+      }
+    }
+  }
+}
+
+// straight-line restatement, one thread per key, per-key seeds
+__global__ void __launch_bounds__(256)
+k_seeded(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
+         const uint64_t* __restrict__ seeds, uint64_t* __restrict__ out, uint32_t flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ConstTab T;
+  const uint64_t o0 = offs[i], o1 = offs[i + 1];
+  const Blk h = meow_literal(keys + o0, o1 - o0, seeds[2 * i], seeds[2 * i + 1], T);
+  store_h(out, i, h, (flags & KVH_FIXUP) != 0);
+}
+
+// streaming: state[16 words] in/out; absorb nblk full 64-byte blocks
+__global__ void k_stream_absorb(uint32_t* st, const uint8_t* data, uint64_t nblk) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const ConstTab T;
+  MeowState s;
+  for (int i = 0; i < 4; i++) for (int c = 0; c < 4; c++) s.S[i].w[c] = st[4 * i + c];
+  absorb_blocks(s, data, nblk, T);
+  for (int i = 0; i < 4; i++) for (int c = 0; c < 4; c++) st[4 * i + c] = s.S[i].w[c];
+}
+
+// streaming final: Meow_Loop over the buffered `off` bytes, then finish
+// with the Mixer of (k1, k2, total) (key_hash.c:1541-1568)
+__global__ void k_stream_final(const uint32_t* st, const uint8_t* block, uint64_t off,
+                               uint64_t k1, uint64_t k2, uint64_t total, uint64_t* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const ConstTab T;
+  MeowState s;
+  for (int i = 0; i < 4; i++) for (int c = 0; c < 4; c++) s.S[i].w[c] = st[4 * i + c];
+  if (off > 0) absorb_loop(s, block, off, T);
+  const Blk h = finish(s, mixer(k1, k2, total), T);
+  out[0] = (uint64_t)h.w[0] | ((uint64_t)h.w[1] << 32);
+  out[1] = (uint64_t)h.w[2] | ((uint64_t)h.w[3] << 32);
+}
+
+// ------------------------------------------------------------ host side
+thread_local int t_last_err = 0;
+
+struct DevInfo {
+  int cus = 0;
+};
+std::mutex g_mu;
+std::vector<DevInfo> g_dev;
+int g_tune_nt = 4;        // tables per LDS: 2 or 4
+int g_tune_wgmul = 1;     // workgroups per CU multiplier
+int g_tune_generic = 0;   // force the generic kernel
+
+int set_err(int e) { t_last_err = e; return e; }
+int hip_err(hipError_t e) { return set_err(KVH_EHIP_BASE - (int)e); }
+
+int device_cus(int* cus) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  std::lock_guard<std::mutex> g(g_mu);
+  if ((int)g_dev.size() <= dev) g_dev.resize(dev + 1);
+  if (g_dev[dev].cus == 0) {
+    int c = 0;
+    e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return hip_err(e);
+    g_dev[dev].cus = c > 0 ? c : 1;
+  }
+  *cus = g_dev[dev].cus;
+  return 0;
+}
+
+uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
+  const uint64_t need = (n + kBlock - 1) / kBlock;
+  uint64_t g = (uint64_t)cus * (uint64_t)std::max(1, wg_per_cu * g_tune_wgmul);
+  if (need < g) g = need;
+  return (uint32_t)std::max<uint64_t>(g, 1);
+}
+
+int launch_done() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(e);
+  return set_err(0);
+}
+
+template <int L, int NT>
+int launch_fixed_L(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
+                   uint32_t flags, hipStream_t st, int cus) {
+  const bool a16 = ((uintptr_t)keys & 15) == 0;
+  const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
+  if (a16)
+    hipLaunchKernelGGL((k_fixed<L, NT, true>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+  else
+    hipLaunchKernelGGL((k_fixed<L, NT, false>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+  return launch_done();
+}
+
+template <int L>
+int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
+                    uint32_t flags, hipStream_t st, int cus) {
+  if (g_tune_nt == 2) return launch_fixed_L<L, 2>(keys, n, s1, s2, out, flags, st, cus);
+  return launch_fixed_L<L, 4>(keys, n, s1, s2, out, flags, st, cus);
+}
+
+template <int L>
+int launch_ms_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
+                uint32_t flags, hipStream_t st, int cus) {
+  const bool a16 = ((uintptr_t)keys & 15) == 0;
+  const uint32_t grid = grid_for(n, cus, 1);
+  if (a16)
+    hipLaunchKernelGGL((k_fixed_ms<L, 4, true>), dim3(grid), dim3(kBlock), 0, st, keys, n, nullptr, out,
+                       flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10],
+                       s[11], s[12], s[13], s[14], s[15]);
+  else
+    hipLaunchKernelGGL((k_fixed_ms<L, 4, false>), dim3(grid), dim3(kBlock), 0, st, keys, n, nullptr, out,
+                       flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10],
+                       s[11], s[12], s[13], s[14], s[15]);
+  return launch_done();
+}
+
+int launch_generic(bool var, const uint8_t* keys, const uint64_t* offs, uint32_t fixed_len, uint64_t n,
+                   const uint64_t* s, uint32_t arity, uint64_t* out, uint32_t flags, hipStream_t st,
+                   int cus) {
+  const uint32_t grid = grid_for(n, cus, 1);
+  if (var)
+    hipLaunchKernelGGL((k_generic<true, 4>), dim3(grid), dim3(kBlock), 0, st, keys, offs, fixed_len, n,
+                       out, flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
+                       s[10], s[11], s[12], s[13], s[14], s[15]);
+  else
+    hipLaunchKernelGGL((k_generic<false, 4>), dim3(grid), dim3(kBlock), 0, st, keys, offs, fixed_len, n,
+                       out, flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
+                       s[10], s[11], s[12], s[13], s[14], s[15]);
+  return launch_done();
+}
+
+// Pinned/device staging for the synchronous host drop-ins.
+struct Staging {
+  std::mutex mu;
+  uint8_t* dev = nullptr;
+  size_t cap = 0;
+  int device = -1;
+};
+Staging g_stage;
+
+int stage_reserve(size_t bytes) {  // caller holds g_stage.mu
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  if (g_stage.dev && g_stage.device == dev && g_stage.cap >= bytes) return 0;
+  if (g_stage.dev) {
+    int cur = dev;
+    hipSetDevice(g_stage.device);
+    hipFree(g_stage.dev);
+    hipSetDevice(cur);
+    g_stage.dev = nullptr;
+  }
+  size_t cap = std::max<size_t>(bytes, 1 << 20);
+  e = hipMalloc(&g_stage.dev, cap);
+  if (e != hipSuccess) { g_stage.dev = nullptr; g_stage.cap = 0; return hip_err(e); }
+  g_stage.cap = cap;
+  g_stage.device = dev;
+  return 0;
+}
+
+size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// Hash `n` host keys (pointers + lengths) with per-key seeds on the GPU via
+// k_seeded; out gets 2n words.  Synchronous.
+int seeded_host(const void* const* ptrs, const size_t* lens, size_t n, const uint64_t* seeds,
+                uint64_t* out, uint32_t flags) {
+  if (n == 0) return set_err(0);
+  size_t kbytes = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (lens[i] && !ptrs[i]) return set_err(KVH_EINVAL);
+    kbytes += lens[i];
+  }
+  std::vector<uint8_t> host(al16(kbytes) + al16(8 * (n + 1)) + al16(16 * n));
+  std::vector<uint64_t> offs(n + 1);
+  size_t o = 0;
+  for (size_t i = 0; i < n; i++) {
+    offs[i] = o;
+    if (lens[i]) memcpy(host.data() + o, ptrs[i], lens[i]);
+    o += lens[i];
+  }
+  offs[n] = o;
+  const size_t off_offs = al16(kbytes), off_seeds = off_offs + al16(8 * (n + 1)),
+               off_out = off_seeds + al16(16 * n);
+  memcpy(host.data() + off_offs, offs.data(), 8 * (n + 1));
+  memcpy(host.data() + off_seeds, seeds, 16 * n);
+  std::lock_guard<std::mutex> g(g_stage.mu);
+  int rc = stage_reserve(off_out + 16 * n);
+  if (rc) return rc;
+  uint8_t* d = g_stage.dev;
+  hipError_t e = hipMemcpy(d, host.data(), off_out, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_err(e);
+  const uint32_t grid = (uint32_t)((n + 255) / 256);
+  hipLaunchKernelGGL(k_seeded, dim3(grid), dim3(256), 0, 0, d, (const uint64_t*)(d + off_offs), (uint64_t)n,
+                     (const uint64_t*)(d + off_seeds), (uint64_t*)(d + off_out), flags);
+  rc = launch_done();
+  if (rc) return rc;
+  e = hipMemcpy(out, d + off_out, 16 * n, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_err(e);
+  return set_err(0);
+}
+
+int same_len_host(const void* const* ptrs, size_t cnt, size_t sz, const uint64_t* seed_pairs,
+                  bool per_key_seed, uint64_t* x) {
+  std::vector<size_t> lens(cnt, sz);
+  std::vector<uint64_t> seeds(2 * cnt);
+  for (size_t i = 0; i < cnt; i++) {
+    seeds[2 * i] = per_key_seed ? seed_pairs[2 * i] : seed_pairs[0];
+    seeds[2 * i + 1] = per_key_seed ? seed_pairs[2 * i + 1] : seed_pairs[1];
+  }
+  return seeded_host(ptrs, lens.data(), cnt, seeds.data(), x, 0);
+}
+
+}  // namespace
+
+// =============================================================== C-ABI
+extern "C" {
+
+int kvh_meow128_fixed(const void* keys, uint32_t key_len, size_t n, uint64_t seed1, uint64_t seed2,
+                      uint64_t* out, uint32_t flags, void* stream) {
+  if (n == 0) return set_err(0);
+  if (!keys || !out) return set_err(KVH_EINVAL);
+  int cus = 0, rc = device_cus(&cus);
+  if (rc) return rc;
+  const uint8_t* k = (const uint8_t*)keys;
+  hipStream_t st = (hipStream_t)stream;
+  const bool a8 = ((uintptr_t)k & 7) == 0;
+  if (!g_tune_generic && a8) {
+    switch (key_len) {
+      case 8: return launch_fixed_nt<8>(k, n, seed1, seed2, out, flags, st, cus);
+      case 16: return launch_fixed_nt<16>(k, n, seed1, seed2, out, flags, st, cus);
+      case 24: return launch_fixed_nt<24>(k, n, seed1, seed2, out, flags, st, cus);
+      case 32: return launch_fixed_nt<32>(k, n, seed1, seed2, out, flags, st, cus);
+      case 40: return launch_fixed_nt<40>(k, n, seed1, seed2, out, flags, st, cus);
+      case 48: return launch_fixed_nt<48>(k, n, seed1, seed2, out, flags, st, cus);
+      case 56: return launch_fixed_nt<56>(k, n, seed1, seed2, out, flags, st, cus);
+      case 64: return launch_fixed_nt<64>(k, n, seed1, seed2, out, flags, st, cus);
+      default: break;
+    }
+  }
+  uint64_t s[16] = {seed1, seed2};
+  return launch_generic(false, k, nullptr, key_len, n, s, 1, out, flags, st, cus);
+}
+
+int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_t seed1, uint64_t seed2,
+                    uint64_t* out, uint32_t flags, void* stream) {
+  if (n == 0) return set_err(0);
+  if (!keys || !offsets || !out) return set_err(KVH_EINVAL);
+  int cus = 0, rc = device_cus(&cus);
+  if (rc) return rc;
+  uint64_t s[16] = {seed1, seed2};
+  return launch_generic(true, (const uint8_t*)keys, offsets, 0, n, s, 1, out, flags, (hipStream_t)stream,
+                        cus);
+}
+
+int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const uint64_t* seeds,
+                          uint32_t arity, uint64_t* out, uint32_t flags, void* stream) {
+  if (n == 0) return set_err(0);
+  if (!keys || !out || !seeds || arity < 1 || arity > KVH_MAX_ARITY) return set_err(KVH_EINVAL);
+  if (arity == 1) return kvh_meow128_fixed(keys, key_len, n, seeds[0], seeds[1], out, flags, stream);
+  int cus = 0, rc = device_cus(&cus);
+  if (rc) return rc;
+  uint64_t s[16] = {0};
+  for (uint32_t a = 0; a < arity; a++) { s[2 * a] = seeds[2 * a]; s[2 * a + 1] = seeds[2 * a + 1]; }
+  const uint8_t* k = (const uint8_t*)keys;
+  hipStream_t st = (hipStream_t)stream;
+  const bool a8 = ((uintptr_t)k & 7) == 0;
+  if (!g_tune_generic && a8) {
+    switch (key_len) {
+      case 16: return launch_ms_L<16>(k, n, s, arity, out, flags, st, cus);
+      case 32: return launch_ms_L<32>(k, n, s, arity, out, flags, st, cus);
+      case 64: return launch_ms_L<64>(k, n, s, arity, out, flags, st, cus);
+      default: break;
+    }
+  }
+  return launch_generic(false, k, nullptr, key_len, n, s, arity, out, flags, st, cus);
+}
+
+int kvh_meow128_batch(const void* keys, const uint64_t* offsets, uint32_t fixed_len, size_t n,
+                      const uint64_t* seeds, uint32_t arity, uint64_t* out, uint32_t flags, void* stream) {
+  if (!seeds) return set_err(KVH_EINVAL);
+  if (offsets) {
+    if (arity != 1) return set_err(KVH_EINVAL);
+    return kvh_meow128_var(keys, offsets, n, seeds[0], seeds[1], out, flags, stream);
+  }
+  return kvh_meow128_multiseed(keys, fixed_len, n, seeds, arity, out, flags, stream);
+}
+
+int kvh_meow128_var_seeded(const void* keys, const uint64_t* offsets, size_t n, const uint64_t* seeds,
+                           uint64_t* out, uint32_t flags, void* stream) {
+  if (n == 0) return set_err(0);
+  if (!keys || !offsets || !seeds || !out) return set_err(KVH_EINVAL);
+  const uint32_t grid = (uint32_t)((n + 255) / 256);
+  hipLaunchKernelGGL(k_seeded, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)keys, offsets,
+                     (uint64_t)n, seeds, out, flags);
+  return launch_done();
+}
+
+int kvh_meow128_fixed_host(const void* keys, uint32_t key_len, size_t n, uint64_t seed1, uint64_t seed2,
+                           uint64_t* out, uint32_t flags) {
+  if (n == 0) return set_err(0);
+  if (!keys || !out || key_len == 0) return set_err(KVH_EINVAL);
+  // Chunked pipeline: NS streams, each with its own device key/out buffers.
+  // Host buffers are used directly when pinned (hipHostMalloc / registered);
+  // pageable memory goes through pinned bounce buffers.
+  constexpr int NS = 3;
+  const size_t chunk = std::max<size_t>(1, (size_t)(64u << 20) / key_len);  // ~64 MiB of keys per chunk
+  hipPointerAttribute_t ak, ao;
+  bool pin_k = hipPointerGetAttributes(&ak, keys) == hipSuccess && ak.type == hipMemoryTypeHost;
+  bool pin_o = hipPointerGetAttributes(&ao, out) == hipSuccess && ao.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  hipStream_t st[NS];
+  uint8_t* dk[NS] = {};
+  uint64_t* dout[NS] = {};
+  uint8_t* hk[NS] = {};
+  uint64_t* ho[NS] = {};
+  size_t pend_lo[NS], pend_cnt[NS];
+  int rc = 0;
+  hipError_t e = hipSuccess;
+  for (int s = 0; s < NS; s++) {
+    st[s] = nullptr; pend_cnt[s] = 0; pend_lo[s] = 0;
+    if ((e = hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking)) != hipSuccess) break;
+    if ((e = hipMalloc(&dk[s], chunk * key_len)) != hipSuccess) break;
+    if ((e = hipMalloc(&dout[s], chunk * 16)) != hipSuccess) break;
+    if (!pin_k && (e = hipHostMalloc(&hk[s], chunk * key_len, 0)) != hipSuccess) break;
+    if (!pin_o && (e = hipHostMalloc(&ho[s], chunk * 16, 0)) != hipSuccess) break;
+  }
+  if (e != hipSuccess) rc = hip_err(e);
+  auto drain = [&](int s) -> int {
+    if (!pend_cnt[s]) return 0;
+    hipError_t x = hipStreamSynchronize(st[s]);
+    if (x != hipSuccess) return hip_err(x);
+    if (!pin_o) memcpy(out + 2 * pend_lo[s], ho[s], pend_cnt[s] * 16);
+    pend_cnt[s] = 0;
+    return 0;
+  };
+  size_t idx = 0;
+  for (size_t lo = 0; !rc && lo < n; lo += chunk, idx++) {
+    const int s = (int)(idx % NS);
+    if ((rc = drain(s))) break;
+    const size_t cnt = std::min(chunk, n - lo);
+    const uint8_t* src = (const uint8_t*)keys + lo * key_len;
+    if (!pin_k) { memcpy(hk[s], src, cnt * key_len); src = hk[s]; }
+    if ((e = hipMemcpyAsync(dk[s], src, cnt * key_len, hipMemcpyHostToDevice, st[s])) != hipSuccess) {
+      rc = hip_err(e); break;
+    }
+    if ((rc = kvh_meow128_fixed(dk[s], key_len, cnt, seed1, seed2, dout[s], flags, st[s]))) break;
+    uint64_t* dst = pin_o ? out + 2 * lo : ho[s];
+    if ((e = hipMemcpyAsync(dst, dout[s], cnt * 16, hipMemcpyDeviceToHost, st[s])) != hipSuccess) {
+      rc = hip_err(e); break;
+    }
+    pend_lo[s] = lo; pend_cnt[s] = cnt;
+  }
+  for (int s = 0; s < NS; s++) {
+    int r2 = st[s] ? drain(s) : 0;
+    if (!rc) rc = r2;
+    if (st[s]) hipStreamDestroy(st[s]);
+    if (dk[s]) hipFree(dk[s]);
+    if (dout[s]) hipFree(dout[s]);
+    if (hk[s]) hipHostFree(hk[s]);
+    if (ho[s]) hipHostFree(ho[s]);
+  }
+  return rc ? rc : set_err(0);
+}
+
+int kvh_hash_meow128(const void* p, size_t sz, uint64_t* h1, uint64_t* h2) {
+  if (!h1 || !h2) return set_err(KVH_EINVAL);
+  uint64_t s[2] = {*h1, *h2}, o[2];
+  int rc = seeded_host(&p, &sz, 1, s, o, 0);
+  if (rc) return rc;
+  *h1 = o[0]; *h2 = o[1];
+  return 0;
+}
+
+uint64_t kvh_hash_meow64(const void* p, size_t sz, uint64_t seed) {
+  uint64_t h1 = seed, h2 = seed;
+  kvh_hash_meow128(p, sz, &h1, &h2);
+  return h1;
+}
+
+int kvh_hash_meow128_2_same_length(const void* p, const void* p2, size_t sz, uint64_t* x) {
+  const void* ps[2] = {p, p2};
+  return same_len_host(ps, 2, sz, x, false, x);
+}
+int kvh_hash_meow128_4_same_length(const void* p, const void* p2, const void* p3, const void* p4, size_t sz,
+                                   uint64_t* x) {
+  const void* ps[4] = {p, p2, p3, p4};
+  return same_len_host(ps, 4, sz, x, false, x);
+}
+int kvh_hash_meow128_4_same_length_a(const void** p, size_t sz, uint64_t* x) {
+  return same_len_host(p, 4, sz, x, false, x);
+}
+int kvh_hash_meow128_4_same_length_4_seed(const void* p, const void* p2, const void* p3, const void* p4,
+                                          size_t sz, uint64_t* x) {
+  const void* ps[4] = {p, p2, p3, p4};
+  return same_len_host(ps, 4, sz, x, true, x);
+}
+int kvh_hash_meow128_8_same_length(const void* p, const void* p2, const void* p3, const void* p4,
+                                   const void* p5, const void* p6, const void* p7, const void* p8, size_t sz,
+                                   uint64_t* x) {
+  const void* ps[8] = {p, p2, p3, p4, p5, p6, p7, p8};
+  return same_len_host(ps, 8, sz, x, false, x);
+}
+int kvh_hash_meow128_8_same_length_a(const void** p, size_t sz, uint64_t* x) {
+  return same_len_host(p, 8, sz, x, false, x);
+}
+int kvh_hash_meow128_2_diff_length(const void* p, size_t sz, const void* p2, size_t sz2, uint64_t* x) {
+  const void* ps[2] = {p, p2};
+  size_t ls[2] = {sz, sz2};
+  uint64_t seeds[4] = {x[0], x[1], x[0], x[1]};
+  return seeded_host(ps, ls, 2, seeds, x, 0);
+}
+int kvh_hash_meow128_4_diff_length(const void* p, size_t sz, const void* p2, size_t sz2, const void* p3,
+                                   size_t sz3, const void* p4, size_t sz4, uint64_t* x) {
+  const void* ps[4] = {p, p2, p3, p4};
+  size_t ls[4] = {sz, sz2, sz3, sz4};
+  uint64_t seeds[8] = {x[0], x[1], x[0], x[1], x[0], x[1], x[0], x[1]};
+  return seeded_host(ps, ls, 4, seeds, x, 0);
+}
+
+int kvh_hash_meow128_vec(const kvh_meow_vec_t* vec, size_t vec_sz, uint64_t* h1, uint64_t* h2) {
+  if (!h1 || !h2 || (vec_sz && !vec)) return set_err(KVH_EINVAL);
+  size_t total = 0;
+  for (size_t i = 0; i < vec_sz; i++) total += vec[i].sz;
+  std::vector<uint8_t> cat(total ? total : 1);
+  size_t o = 0;
+  for (size_t i = 0; i < vec_sz; i++) {
+    if (vec[i].sz) memcpy(cat.data() + o, vec[i].p, vec[i].sz);
+    o += vec[i].sz;
+  }
+  return kvh_hash_meow128(cat.data(), total, h1, h2);
+}
+
+// Streaming: the 16-word Meow state lives in m->ctx (layout S0..S3 as
+// little-endian 128-bit lanes, same as the reference's Meow_Save_Ctx).
+static int stream_absorb_dev(kvh_meow_ctx_t* m, const uint8_t* data, size_t nblk) {
+  std::lock_guard<std::mutex> g(g_stage.mu);
+  int rc = stage_reserve(64 + nblk * 64);
+  if (rc) return rc;
+  uint8_t* d = g_stage.dev;
+  hipError_t e = hipMemcpy(d, m->ctx, 64, hipMemcpyHostToDevice);
+  if (e == hipSuccess && nblk) e = hipMemcpy(d + 64, data, nblk * 64, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_err(e);
+  hipLaunchKernelGGL(k_stream_absorb, dim3(1), dim3(64), 0, 0, (uint32_t*)d, (const uint8_t*)(d + 64),
+                     (uint64_t)nblk);
+  if ((rc = launch_done())) return rc;
+  e = hipMemcpy(m->ctx, d, 64, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? 0 : hip_err(e);
+}
+
+int kvh_meow128_init(kvh_meow_ctx_t* m, kvh_meow_block_t* b, uint64_t k1, uint64_t k2, size_t total) {
+  if (!m || !b) return set_err(KVH_EINVAL);
+  // Declare_Meow + Xor_Meow (key_hash.c:1509-1521): byte ramps ^ Mixer
+  const uint64_t lo = k1 - total, hi = k2 + total + 1;
+  for (int i = 0; i < 4; i++) {
+    uint8_t r[16];
+    for (int j = 0; j < 16; j++) r[j] = (uint8_t)(16 * i + j);
+    uint64_t w0, w1;
+    memcpy(&w0, r, 8); memcpy(&w1, r + 8, 8);
+    m->ctx[2 * i] = w0 ^ lo;
+    m->ctx[2 * i + 1] = w1 ^ hi;
+  }
+  b->off = 0;
+  b->total_update_sz = total;
+  return set_err(0);
+}
+
+int kvh_meow128_update(kvh_meow_ctx_t* m, kvh_meow_block_t* b, const void* p, size_t sz) {
+  if (!m || !b || (sz && !p)) return set_err(KVH_EINVAL);
+  const uint8_t* src = (const uint8_t*)p;
+  size_t len = sz;
+  int rc = 0;
+  if (b->off > 0) {
+    size_t fill = 64 - b->off;
+    if (fill > len) fill = len;
+    memcpy(&b->block[b->off], src, fill);
+    b->off += fill; len -= fill; src += fill;
+    if (b->off == 64) {
+      if ((rc = stream_absorb_dev(m, b->block, 1))) return rc;
+      b->off = 0;
+    }
+  }
+  if (len > 0) {
+    b->off = len & 63;
+    if (len > b->off && (rc = stream_absorb_dev(m, src, (len - b->off) / 64))) return rc;
+    memcpy(b->block, &src[len - b->off], b->off);
+  }
+  return set_err(0);
+}
+
+int kvh_meow128_final(kvh_meow_ctx_t* m, kvh_meow_block_t* b, uint64_t* k1, uint64_t* k2) {
+  if (!m || !b || !k1 || !k2) return set_err(KVH_EINVAL);
+  std::lock_guard<std::mutex> g(g_stage.mu);
+  int rc = stage_reserve(64 + 64 + 16);
+  if (rc) return rc;
+  uint8_t* d = g_stage.dev;
+  hipError_t e = hipMemcpy(d, m->ctx, 64, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d + 64, b->block, 64, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_err(e);
+  hipLaunchKernelGGL(k_stream_final, dim3(1), dim3(64), 0, 0, (const uint32_t*)d, (const uint8_t*)(d + 64),
+                     (uint64_t)b->off, *k1, *k2, (uint64_t)b->total_update_sz, (uint64_t*)(d + 128));
+  if ((rc = launch_done())) return rc;
+  uint64_t o[2];
+  e = hipMemcpy(o, d + 128, 16, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_err(e);
+  *k1 = o[0]; *k2 = o[1];
+  return set_err(0);
+}
+
+int kvh_meow_test(const void* p, size_t sz, uint64_t* k1, uint64_t* k2) {
+  kvh_meow_ctx_t m;
+  kvh_meow_block_t b;
+  int rc = kvh_meow128_init(&m, &b, *k1, *k2, sz);
+  if (!rc) rc = kvh_meow128_update(&m, &b, p, sz);
+  if (!rc) rc = kvh_meow128_final(&m, &b, k1, k2);
+  return rc;
+}
+
+int kvh_hash_key_frag(const uint64_t seed[2], const kvh_key_frag_t* frag, uint64_t* k, uint64_t* k2) {
+  if (!seed || !frag || !k || !k2) return set_err(KVH_EINVAL);
+  const void* p = frag->buf;
+  size_t len = frag->keylen;
+  uint64_t o[2];
+  int rc = seeded_host(&p, &len, 1, seed, o, KVH_FIXUP);
+  if (rc) return rc;
+  *k = o[0]; *k2 = o[1];
+  return 0;
+}
+
+int kvh_hash_key_frags(const uint64_t seed[2], const kvh_key_frag_t* const* frags, size_t n, uint64_t* out) {
+  if (!seed || (n && (!frags || !out))) return set_err(KVH_EINVAL);
+  std::vector<const void*> ps(n);
+  std::vector<size_t> ls(n);
+  std::vector<uint64_t> seeds(2 * n);
+  for (size_t i = 0; i < n; i++) {
+    ps[i] = frags[i]->buf; ls[i] = frags[i]->keylen;
+    seeds[2 * i] = seed[0]; seeds[2 * i + 1] = seed[1];
+  }
+  return seeded_host(ps.data(), ls.data(), n, seeds.data(), out, KVH_FIXUP);
+}
+
+int kvh_last_error(void) { return t_last_err; }
+
+const char* kvh_strerror(int err) {
+  if (err == 0) return "ok";
+  if (err == KVH_EINVAL) return "invalid argument";
+  if (err == KVH_ENOMEM) return "out of memory";
+  if (err == KVH_ENODEV) return "no device";
+  if (err <= KVH_EHIP_BASE) return hipGetErrorString((hipError_t)(KVH_EHIP_BASE - err));
+  return "unknown error";
+}
+
+const char* kvh_version(void) { return KVH_VERSION; }
+
+int kvh_device_synchronize(void) {
+  hipError_t e = hipDeviceSynchronize();
+  return e == hipSuccess ? set_err(0) : hip_err(e);
+}
+
+int kvh_set_tuning(int knob, int value) {
+  int prev;
+  switch (knob) {
+    case 0: if (value != 2 && value != 4) return KVH_EINVAL; prev = g_tune_nt; g_tune_nt = value; return prev;
+    case 1: if (value < 1 || value > 8) return KVH_EINVAL; prev = g_tune_wgmul; g_tune_wgmul = value; return prev;
+    case 2: prev = g_tune_generic; g_tune_generic = value ? 1 : 0; return prev;
+    default: return KVH_EINVAL;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,413 @@
+// meow_dev.hpp -- CDNA4 (gfx950) device building blocks for raikv's 128-bit
+// Meow-derived key hash (reference: /root/reference/src/key_hash.c:1070-1429).
+//
+// Design:
+//  * one lane per key; the AESDEC round is lowered to integer ALU + LDS
+//    T-table lookups (no AES instruction on the GPU, no MFMA: this is not a
+//    contraction);
+//  * the inverse-cipher T-tables live in LDS replicated 32x so that lane l
+//    always reads copy (l & 31): every ds_read_b32 lane group hits 32
+//    distinct banks, i.e. random lookups are bank-conflict free;
+//  * the LDS byte address of a lookup is built by ONE v_perm_b32 from the
+//    state word and a per-lane "lane word":
+//        addr = (t>>1)<<16 | x<<8 | (t&1)<<7 | (lane&31)<<2
+//    (t = table 0..3, x = state byte);
+//  * data-independent work is folded per (seed, length): the first AESDEC
+//    of a state that still holds init^Mixer is T(init^Mixer) ^ K, states
+//    that never see data are constants, and an AESDEC whose *state* input is
+//    a constant is a single XOR.  16-byte keys need 5 table rounds instead
+//    of 11.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "aes_tables.hpp"
+
+namespace kvh {
+
+__constant__ TdTable c_td0 = kTd0;
+
+struct Blk { uint32_t w[4]; };
+
+__device__ __forceinline__ Blk bxor(const Blk& a, const Blk& b) {
+  Blk r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.w[i] = a.w[i] ^ b.w[i];
+  return r;
+}
+__device__ __forceinline__ Blk bzero() { Blk r; r.w[0] = r.w[1] = r.w[2] = r.w[3] = 0; return r; }
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) {
+  return r == 0 ? x : ((x << r) | (x >> (32 - r)));
+}
+// gfx950 v_bitop3_b32 with truth table 0x96 = a ^ b ^ c in one VALU op
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// ---------------------------------------------------------------- tables
+// LDS-resident, bank-replicated tables.  NT = 4: Td0..Td3 (128 KiB);
+// NT = 2: Td0, Td1 (64 KiB), Td2/Td3 lookups reuse them rotated by 16.
+template <int NT>
+struct LdsTab {
+  static constexpr int kWords = NT * 8192;
+  const uint32_t* lds;
+  uint32_t lw[NT];
+
+  __device__ __forceinline__ explicit LdsTab(const uint32_t* p) : lds(p) {
+    const uint32_t lane = (threadIdx.x & 31u) << 2;
+#pragma unroll
+    for (int t = 0; t < NT; t++)
+      lw[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | lane;
+  }
+  __device__ __forceinline__ uint32_t ld(uint32_t byteaddr) const {
+    return *(const uint32_t*)((const char*)lds + byteaddr);
+  }
+  // perm selector: byte0 <- lane word byte0, byte1 <- state byte k,
+  // byte2 <- lane word byte2, byte3 <- lane word byte3 (= 0)
+  template <int K> static constexpr uint32_t sel() { return 0x03020000u | ((4u + K) << 8); }
+
+  // Td0[a.b0] ^ Td1[b.b1] ^ Td2[c.b2] ^ Td3[d.b3] ^ k  (v_bitop3 0x96 = 3-way XOR)
+  __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
+    if constexpr (NT == 4) {
+      const uint32_t t0 = ld(__builtin_amdgcn_perm(a, lw[0], sel<0>()));
+      const uint32_t t1 = ld(__builtin_amdgcn_perm(b, lw[1], sel<1>()));
+      const uint32_t t2 = ld(__builtin_amdgcn_perm(c, lw[2], sel<2>()));
+      const uint32_t t3 = ld(__builtin_amdgcn_perm(d, lw[3], sel<3>()));
+      return xor3(xor3(t0, t1, k), t2, t3);
+    } else {
+      const uint32_t t0 = ld(__builtin_amdgcn_perm(a, lw[0], sel<0>()));
+      const uint32_t t1 = ld(__builtin_amdgcn_perm(b, lw[1], sel<1>()));
+      const uint32_t t2 = ld(__builtin_amdgcn_perm(c, lw[0], sel<2>()));
+      const uint32_t t3 = ld(__builtin_amdgcn_perm(d, lw[1], sel<3>()));
+      return xor3(t0, t1, k) ^ rotl32(t2 ^ t3, 16);
+    }
+  }
+};
+
+// fill the replicated tables; dword index i = addr >> 2 decodes to
+// copy = i & 31, table = ((i>>14)&1)*2 + ((i>>5)&1), x = (i>>6) & 255
+template <int NT>
+__device__ __forceinline__ void fill_tables(uint32_t* lds) {
+  for (uint32_t i = threadIdx.x; i < (uint32_t)LdsTab<NT>::kWords; i += blockDim.x) {
+    const uint32_t t = (((i >> 14) & 1u) << 1) | ((i >> 5) & 1u);
+    const uint32_t x = (i >> 6) & 255u;
+    lds[i] = rotl32(c_td0.v[x], 8 * (int)t);
+  }
+}
+
+// Table access through the constant segment (tiny batches / drop-ins:
+// no per-workgroup LDS fill).
+struct ConstTab {
+  __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
+    return c_td0.v[a & 255] ^ rotl32(c_td0.v[(b >> 8) & 255], 8) ^
+           rotl32(c_td0.v[(c >> 16) & 255], 16) ^ rotl32(c_td0.v[d >> 24], 24) ^ k;
+  }
+};
+
+// Intel AESDEC(s, k) = InvMixColumns(InvSubBytes(InvShiftRows(s))) ^ k.
+// Output column c takes row r from input column (c - r) & 3.
+template <class Tab>
+__device__ __forceinline__ Blk aesdec(const Blk& s, const Blk& k, const Tab& T) {
+  Blk o;
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    o.w[c] = T.col(s.w[c], s.w[(c + 3) & 3], s.w[(c + 2) & 3], s.w[(c + 1) & 3], k.w[c]);
+  return o;
+}
+// the keyless half: T(s) = AESDEC(s, 0)
+template <class Tab>
+__device__ __forceinline__ Blk aesT(const Blk& s, const Tab& T) {
+  Blk o;
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    o.w[c] = T.col(s.w[c], s.w[(c + 3) & 3], s.w[(c + 2) & 3], s.w[(c + 1) & 3], 0u);
+  return o;
+}
+
+// ------------------------------------------------------- Meow constants
+// Meow state init ramps (key_hash.c:1106-1113): state i = bytes 16i..16i+15
+__device__ __forceinline__ Blk ramp(int i) {
+  Blk r;
+#pragma unroll
+  for (int c = 0; c < 4; c++) r.w[c] = 0x03020100u + 0x04040404u * (uint32_t)c + 0x10101010u * (uint32_t)i;
+  return r;
+}
+// Mixer = _mm_set_epi64x(seed2 + sz + 1, seed1 - sz)   (key_hash.c:1418)
+__device__ __forceinline__ Blk mixer(uint64_t s1, uint64_t s2, uint64_t sz) {
+  const uint64_t lo = s1 - sz, hi = s2 + sz + 1;
+  Blk m;
+  m.w[0] = (uint32_t)lo; m.w[1] = (uint32_t)(lo >> 32);
+  m.w[2] = (uint32_t)hi; m.w[3] = (uint32_t)(hi >> 32);
+  return m;
+}
+
+// Everything about a hash that depends only on (seed, length):
+//   F[i]  = T(ramp_i ^ M)           first absorb into state i = F[i] ^ K, then 1 round
+//   G[i]  = F[i] ^ M                state i after Mix_Meow when it never saw data
+//   TG2   = T(G2)                   Compress2 S2 <- AESDEC(G2, S3) = TG2 ^ S3
+//   CS2b  = AESDEC(AESDEC(G2,G3),M) Compress2 result for S2 when S2,S3 untouched
+//   TCS0a = T(AESDEC(G0, G1))       Compress S0 <- AESDEC(const, S2) = TCS0a ^ S2
+struct MeowConst {
+  Blk M, F[4], G[4], TG2, CS2b, TCS0a;
+};
+
+template <class Tab>
+__device__ __forceinline__ MeowConst make_const(uint64_t s1, uint64_t s2, uint64_t len, const Tab& T) {
+  MeowConst K;
+  K.M = mixer(s1, s2, len);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    K.F[i] = aesT(bxor(ramp(i), K.M), T);
+    K.G[i] = bxor(K.F[i], K.M);
+  }
+  K.TG2 = aesT(K.G[2], T);
+  K.CS2b = aesdec(bxor(K.TG2, K.G[3]), K.M, T);
+  K.TCS0a = aesT(bxor(aesT(K.G[0], T), K.G[1]), T);
+  return K;
+}
+
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ Blk rfl(const Blk& b) {
+  Blk r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.w[i] = rfl(b.w[i]);
+  return r;
+}
+// move wave-uniform constants to SGPRs
+__device__ __forceinline__ MeowConst uniform(const MeowConst& k) {
+  MeowConst r;
+  r.M = rfl(k.M);
+#pragma unroll
+  for (int i = 0; i < 4; i++) { r.F[i] = rfl(k.F[i]); r.G[i] = rfl(k.G[i]); }
+  r.TG2 = rfl(k.TG2); r.CS2b = rfl(k.CS2b); r.TCS0a = rfl(k.TCS0a);
+  return r;
+}
+
+// ------------------------------------------------- compile-time length
+// Key of compile-time length L given as NC = ceil(L/16) chunks, chunk j =
+// bytes [16j, 16j+16) zero padded past L.  Follows Meow_Loop/Meow_Loop_Trail
+// (key_hash.c:1200-1226), Mix_Meow (:1155-1160), Compress_Meow2/_Meow
+// (:1167-1176) as used by kv_hash_meow128 (:1413-1429).
+template <int L>
+struct Plan {
+  static constexpr int NB = L / 64;           // full 64-byte blocks
+  static constexpr int C = (L % 64) & 48;     // trail full-chunk bytes
+  static constexpr int T = L & 15;            // partial tail bytes -> S3
+  static constexpr int NC = (L + 15) / 16;
+  static constexpr bool T0 = NB > 0 || C >= 16;
+  static constexpr bool T1 = NB > 0 || C >= 32;
+  static constexpr bool T2 = NB > 0 || C >= 48;
+  static constexpr bool T3 = NB > 0 || T != 0;
+};
+
+template <int L, class Tab>
+__device__ __forceinline__ Blk meow_ct(const Blk* D, const MeowConst& K, const Tab& T) {
+  using P = Plan<L>;
+  Blk S0, S1, S2, S3;
+  // absorb full blocks; the first AESDEC on a state is folded
+#pragma unroll
+  for (int b = 0; b < P::NB; b++) {
+    const Blk& k0 = D[4 * b + 0]; const Blk& k1 = D[4 * b + 1];
+    const Blk& k2 = D[4 * b + 2]; const Blk& k3 = D[4 * b + 3];
+    if (b == 0) {
+      S0 = aesdec(bxor(K.F[0], k0), k0, T); S1 = aesdec(bxor(K.F[1], k1), k1, T);
+      S2 = aesdec(bxor(K.F[2], k2), k2, T); S3 = aesdec(bxor(K.F[3], k3), k3, T);
+    } else {
+      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+    }
+  }
+  constexpr bool first = P::NB == 0;
+  constexpr int base = 4 * P::NB;
+  if constexpr (P::T != 0) {
+    const Blk& k = D[base + P::C / 16];
+    S3 = first ? aesdec(bxor(K.F[3], k), k, T) : aesdec(aesdec(S3, k, T), k, T);
+  }
+  if constexpr (P::C >= 48) {
+    const Blk& k = D[base + 2];
+    S2 = first ? aesdec(bxor(K.F[2], k), k, T) : aesdec(aesdec(S2, k, T), k, T);
+  }
+  if constexpr (P::C >= 32) {
+    const Blk& k = D[base + 1];
+    S1 = first ? aesdec(bxor(K.F[1], k), k, T) : aesdec(aesdec(S1, k, T), k, T);
+  }
+  if constexpr (P::C >= 16) {
+    const Blk& k = D[base + 0];
+    S0 = first ? aesdec(bxor(K.F[0], k), k, T) : aesdec(aesdec(S0, k, T), k, T);
+  }
+  // Mix_Meow
+  if constexpr (P::T3) S3 = aesdec(S3, K.M, T); else S3 = K.G[3];
+  if constexpr (P::T2) S2 = aesdec(S2, K.M, T); else S2 = K.G[2];
+  if constexpr (P::T1) S1 = aesdec(S1, K.M, T); else S1 = K.G[1];
+  if constexpr (P::T0) S0 = aesdec(S0, K.M, T); else S0 = K.G[0];
+  // Compress_Meow2: S2 = AESDEC(S2,S3); S0 = AESDEC(S0,S1); S2 = AESDEC(S2,M)
+  Blk S2b;
+  if constexpr (P::T2) S2b = aesdec(aesdec(S2, S3, T), K.M, T);
+  else if constexpr (P::T3) S2b = aesdec(bxor(K.TG2, S3), K.M, T);
+  else S2b = K.CS2b;
+  // Compress_Meow: S0 = AESDEC(S0, S2); S0 = AESDEC(S0, M)
+  Blk S0b;
+  if constexpr (P::T0) S0b = aesdec(aesdec(S0, S1, T), S2b, T);
+  else S0b = bxor(K.TCS0a, S2b);
+  return aesdec(S0b, K.M, T);
+}
+
+// ---------------------------------------------------- runtime lengths
+// bytes [p, p+n), 0 <= n <= 16, zero padded; reads only the dwords that
+// intersect [p, p+n), so it never touches memory past the key's last byte's
+// dword (no fault at the end of an allocation).
+__device__ __forceinline__ Blk load_bytes(const uint8_t* p, uint32_t n) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t nd = (sh + n + 3) >> 2;
+  uint32_t d[5];
+#pragma unroll
+  for (uint32_t j = 0; j < 5; j++) d[j] = j < nd ? q[j] : 0u;
+  Blk r;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(d[c + 1], d[c], sh);
+    const int keep = (int)n - 4 * c;
+    const uint32_t m = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+    r.w[c] = v & m;
+  }
+  return r;
+}
+
+// Source of per-length constants for the runtime path.
+struct ConstRef {
+  const MeowConst* k;
+};
+
+// Runtime-length Meow over key bytes at p (global memory).  Branches are
+// wave-uniform when every lane has the same length (generic fixed-length
+// kernel) and lane-divergent (masked) for variable-length batches.
+template <class Tab, class KGet>
+__device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet& K, const Tab& T) {
+  const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
+  Blk S0, S1, S2, S3;
+  if (nb > 0) {
+    Blk k0 = load_bytes(p, 16), k1 = load_bytes(p + 16, 16), k2 = load_bytes(p + 32, 16),
+        k3 = load_bytes(p + 48, 16);
+    S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
+    S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
+    for (uint32_t b = 1; b < nb; b++) {
+      const uint8_t* q = p + 64 * b;
+      k0 = load_bytes(q, 16); k1 = load_bytes(q + 16, 16);
+      k2 = load_bytes(q + 32, 16); k3 = load_bytes(q + 48, 16);
+      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+    }
+  }
+  const bool first = nb == 0;
+  const uint8_t* q = p + 64 * nb;
+  // trail (key_hash.c:1200-1210); a state's first absorb is folded
+  if (t) {
+    const Blk k = load_bytes(q + C, t);
+    S3 = first ? aesdec(bxor(K.F(3), k), k, T) : aesdec(aesdec(S3, k, T), k, T);
+  }
+  if (C >= 48) {
+    const Blk k = load_bytes(q + 32, 16);
+    S2 = first ? aesdec(bxor(K.F(2), k), k, T) : aesdec(aesdec(S2, k, T), k, T);
+  }
+  if (C >= 32) {
+    const Blk k = load_bytes(q + 16, 16);
+    S1 = first ? aesdec(bxor(K.F(1), k), k, T) : aesdec(aesdec(S1, k, T), k, T);
+  }
+  if (C >= 16) {
+    const Blk k = load_bytes(q, 16);
+    S0 = first ? aesdec(bxor(K.F(0), k), k, T) : aesdec(aesdec(S0, k, T), k, T);
+  }
+  const bool T0 = !first || C >= 16, T1 = !first || C >= 32, T2 = !first || C >= 48,
+             T3 = !first || t != 0;
+  const Blk M = K.M();
+  S3 = T3 ? aesdec(S3, M, T) : K.G(3);
+  S2 = T2 ? aesdec(S2, M, T) : K.G(2);
+  S1 = T1 ? aesdec(S1, M, T) : K.G(1);
+  S0 = T0 ? aesdec(S0, M, T) : K.G(0);
+  Blk S2b;
+  if (T2) S2b = aesdec(aesdec(S2, S3, T), M, T);
+  else if (T3) S2b = aesdec(bxor(K.TG2(), S3), M, T);
+  else S2b = K.CS2b();
+  Blk S0b;
+  if (T0) S0b = aesdec(aesdec(S0, S1, T), S2b, T);
+  else S0b = bxor(K.TCS0a(), S2b);
+  return aesdec(S0b, M, T);
+}
+
+// constants held in registers (uniform length)
+struct RegK {
+  const MeowConst& k;
+  __device__ __forceinline__ Blk M() const { return k.M; }
+  __device__ __forceinline__ Blk F(int i) const { return k.F[i]; }
+  __device__ __forceinline__ Blk G(int i) const { return k.G[i]; }
+  __device__ __forceinline__ Blk TG2() const { return k.TG2; }
+  __device__ __forceinline__ Blk CS2b() const { return k.CS2b; }
+  __device__ __forceinline__ Blk TCS0a() const { return k.TCS0a; }
+};
+
+// ------------------------------------------- literal restatement (small)
+// Straight-line kv_hash_meow128 with no folding: used by the tiny-batch /
+// drop-in kernel, and as an independent second device path in tests.
+template <class Tab>
+__device__ __forceinline__ Blk absorb2(const Blk& s, const Blk& k, const Tab& T) {
+  return aesdec(aesdec(s, k, T), k, T);
+}
+
+struct MeowState { Blk S[4]; };
+
+template <class Tab>
+__device__ __forceinline__ void absorb_blocks(MeowState& st, const uint8_t* p, uint64_t nblk, const Tab& T) {
+  for (uint64_t b = 0; b < nblk; b++, p += 64) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) st.S[i] = absorb2(st.S[i], load_bytes(p + 16 * i, 16), T);
+  }
+}
+
+// Meow_Loop with `sz` selecting the trail (key_hash.c:1212-1226)
+template <class Tab>
+__device__ __forceinline__ void absorb_loop(MeowState& st, const uint8_t* p, uint64_t sz, const Tab& T) {
+  const uint64_t nblk = sz >> 6;
+  absorb_blocks(st, p, nblk, T);
+  p += 64 * nblk;
+  const uint32_t t = (uint32_t)sz & 15, C = (uint32_t)sz & 48;
+  if (t) st.S[3] = absorb2(st.S[3], load_bytes(p + C, t), T);
+  if (C >= 48) st.S[2] = absorb2(st.S[2], load_bytes(p + 32, 16), T);
+  if (C >= 32) st.S[1] = absorb2(st.S[1], load_bytes(p + 16, 16), T);
+  if (C >= 16) st.S[0] = absorb2(st.S[0], load_bytes(p, 16), T);
+}
+
+template <class Tab>
+__device__ __forceinline__ Blk finish(MeowState& st, const Blk& M, const Tab& T) {
+  st.S[3] = aesdec(st.S[3], M, T); st.S[2] = aesdec(st.S[2], M, T);
+  st.S[1] = aesdec(st.S[1], M, T); st.S[0] = aesdec(st.S[0], M, T);
+  st.S[2] = aesdec(st.S[2], st.S[3], T);
+  st.S[0] = aesdec(st.S[0], st.S[1], T);
+  st.S[2] = aesdec(st.S[2], M, T);
+  st.S[0] = aesdec(st.S[0], st.S[2], T);
+  return aesdec(st.S[0], M, T);
+}
+
+__device__ __forceinline__ void state_init(MeowState& st, const Blk& M) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) st.S[i] = bxor(ramp(i), M);
+}
+
+template <class Tab>
+__device__ __forceinline__ Blk meow_literal(const uint8_t* p, uint64_t sz, uint64_t s1, uint64_t s2, const Tab& T) {
+  MeowState st;
+  const Blk M = mixer(s1, s2, sz);
+  state_init(st, M);
+  absorb_loop(st, p, sz, T);
+  return finish(st, M, T);
+}
+
+// KeyFragment::hash epilogue (include/raikv/hash_entry.h:84-85):
+// clear the ZOMBIE bit 63 of h1; 0 and 1 are reserved -> 2
+__device__ __forceinline__ Blk fixup(Blk h) {
+  h.w[1] &= 0x7fffffffu;
+  if (h.w[1] == 0 && h.w[0] <= 1u) h.w[0] = 2u;
+  return h;
+}
+
+}  // namespace kvh

@@ -1,0 +1,281 @@
+"""GPU parity: every device path through the C-ABI vs the oracle and the
+reference's golden vectors.  Bit-exact (integer/byte work).
+
+Run on an MI355X:  python -m pytest tests -m gpu -x -q
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle_lib import (GOLDEN, ROOT, golden, load_oracle, orc_fixed, orc_meow, orc_multiseed,  # noqa: E402
+                        orc_var)
+
+ORC = load_oracle()
+VEC = json.load(open(os.path.join(GOLDEN, "reference_vectors.json")))
+STATIC = (0xA8E0BCC94D1855F5, 0xAD3BEC1E8DE4A1A3)
+
+
+@pytest.fixture(scope="module")
+def kvh():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
+    import raikv_amd
+    return raikv_amd
+
+
+def dev(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def dev_u64(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
+
+
+def u64(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("L", [8, 16, 24, 32, 40, 48, 56, 64, 1, 13, 100, 255])
+def test_fixed_golden(kvh, L):
+    g = golden(f"fixed_{L}.npz")
+    out = kvh.meow128_fixed(dev(g["keys"]), L, STATIC)
+    np.testing.assert_array_equal(u64(out), g["out"])
+    # KeyFragment::hash epilogue fused
+    fx = kvh.meow128_fixed(dev(g["keys"]), L, STATIC, fixup=True)
+    np.testing.assert_array_equal(u64(fx), orc_fixed(ORC, g["keys"], L, STATIC, fixup=True))
+
+
+@pytest.mark.parametrize("nt", [4, 2])
+def test_fixed_fast_kernels_both_table_layouts(kvh, nt):
+    prev = kvh.lib.kvh_set_tuning(0, nt)
+    try:
+        for L in (8, 16, 24, 32, 40, 48, 56, 64):
+            g = golden(f"fixed_{L}.npz")
+            np.testing.assert_array_equal(u64(kvh.meow128_fixed(dev(g["keys"]), L, STATIC)), g["out"])
+    finally:
+        kvh.lib.kvh_set_tuning(0, prev)
+
+
+def test_all_lengths_0_300_all_paths(kvh):
+    g = golden("lengths.npz")
+    keys, seeds, out = g["keys"], g["seeds"], g["out"]
+    maxl = keys.shape[0] - 1
+    lens = np.arange(maxl + 1, dtype=np.uint32)
+    offs = np.zeros(maxl + 2, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    flat = np.concatenate([keys[L, :L] for L in range(maxl + 1)])
+    dk, doff = dev(flat), dev_u64(offs)
+    for si in range(seeds.shape[0]):
+        s = (int(seeds[si, 0]), int(seeds[si, 1]))
+        # variable-length kernel, every length in one batch
+        np.testing.assert_array_equal(u64(kvh.meow128_var(dk, doff, s)), out[:, si], err_msg=f"var seed {si}")
+        # straight-line kernel with per-key seeds
+        sd = dev_u64(np.tile(np.array(s, dtype=np.uint64), (maxl + 1, 1)))
+        np.testing.assert_array_equal(u64(kvh.meow128_var_seeded(dk, doff, sd)), out[:, si])
+    # fixed-length entry for every length (fast kernels for L%8==0, generic otherwise),
+    # all four seeds at once through the multi-seed entry
+    sl = [(int(a), int(b)) for a, b in seeds]
+    for L in range(1, maxl + 1):
+        got = u64(kvh.meow128_multiseed(dev(keys[L, :L].copy()), L, sl))
+        np.testing.assert_array_equal(got[0], out[L], err_msg=f"L={L}")
+        got1 = u64(kvh.meow128_fixed(dev(keys[L, :L].copy()), L, sl[3]))
+        np.testing.assert_array_equal(got1[0], out[L, 3], err_msg=f"fixed L={L}")
+
+
+def test_var_zipf_golden(kvh):
+    g = golden("var_zipf.npz")
+    out = kvh.meow128_var(dev(g["keys"]), dev_u64(g["offsets"]), STATIC)
+    np.testing.assert_array_equal(u64(out), g["out"])
+    fx = kvh.meow128_var(dev(g["keys"]), dev_u64(g["offsets"]), STATIC, fixup=True)
+    np.testing.assert_array_equal(u64(fx), orc_var(ORC, g["keys"], g["offsets"], STATIC, fixup=True))
+
+
+def test_multiseed_golden_and_arities(kvh):
+    g = golden("multiseed4_32.npz")
+    seeds = [tuple(int(x) for x in s) for s in g["seeds"].reshape(-1, 2)]
+    np.testing.assert_array_equal(u64(kvh.meow128_multiseed(dev(g["keys"]), 32, seeds)), g["out"])
+    rng = np.random.default_rng(4)
+    for L in (16, 32, 64, 24, 20):
+        kb = rng.integers(0, 256, 3000 * L, dtype=np.uint8)
+        for a in range(1, 9):
+            ss = [(int(rng.integers(0, 2**63)) * 2 + 1, int(rng.integers(0, 2**63))) for _ in range(a)]
+            got = u64(kvh.meow128_multiseed(dev(kb), L, ss))
+            np.testing.assert_array_equal(got.reshape(-1, a, 2), orc_multiseed(ORC, kb, L, ss), err_msg=f"{L} {a}")
+
+
+def test_hash_test_int_keys(kvh):
+    g = golden("hash_test_int16.npz")
+    np.testing.assert_array_equal(u64(kvh.meow128_fixed(dev(g["keys"]), 16, (0, 0))), g["out"])
+
+
+def test_unaligned_bases_and_allocation_end(kvh):
+    rng = np.random.default_rng(5)
+    for L in (16, 32, 13, 8, 64, 3):
+        n = 5000
+        for shift in (1, 3, 4, 8):
+            raw = rng.integers(0, 256, n * L + shift, dtype=np.uint8)
+            t = dev(raw)
+            view = t[shift:]  # device pointer at base + shift
+            got = u64(kvh.meow128_fixed(view, L, STATIC, n=n))
+            np.testing.assert_array_equal(got, orc_fixed(ORC, raw[shift:].copy(), L, STATIC), err_msg=f"{L}+{shift}")
+    # keys ending exactly at the end of a fresh allocation (odd sizes)
+    for L in (1, 7, 13, 31, 33, 255):
+        n = 777
+        kb = rng.integers(0, 256, n * L, dtype=np.uint8)
+        t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        t.copy_(torch.from_numpy(kb))
+        np.testing.assert_array_equal(u64(kvh.meow128_fixed(t, L, STATIC)), orc_fixed(ORC, kb, L, STATIC))
+
+
+def test_empty_single_and_zero_length(kvh):
+    z = torch.empty(0, dtype=torch.uint8, device="cuda")
+    assert kvh.meow128_fixed(z, 16, STATIC).shape == (0, 2)
+    one = np.frombuffer(b"hello\0", dtype=np.uint8).copy()
+    got = u64(kvh.meow128_var(dev(one), dev_u64(np.array([0, 6], dtype=np.uint64)), STATIC))
+    assert "%016x:%016x" % tuple(int(v) for v in got[0]) == "2aa73a1eeb0b2d45:fd102121185ce157"
+    # all-empty keys through the var kernel
+    offs = np.zeros(1001, dtype=np.uint64)
+    got = u64(kvh.meow128_var(dev(one), dev_u64(offs), (7, 9)))
+    assert np.all(got == np.array(orc_meow(ORC, b"", 7, 9), dtype=np.uint64))
+
+
+def test_drop_ins_against_reference_vectors(kvh):
+    for k in VEC["kat"]:
+        assert "%016x:%016x" % kvh.kv_hash_meow128(bytes.fromhex(k["key_hex"]), *k["seed"]) == k["h"]
+    for m in VEC["meow64"]:
+        assert kvh.kv_hash_meow64(bytes.fromhex(m["key_hex"]), m["seed"]) == m["h"]
+    r = VEC["variants"]["results"]
+    keys = [k.encode() for k in VEC["variants"]["keys"]]
+    s1, s2 = VEC["variants"]["seed"]
+    L = len(keys[0])
+    bufs = [C.create_string_buffer(k, L) for k in keys]
+    lib = kvh.lib
+    x = (C.c_uint64 * 8)(*([s1, s2] * 4))
+    assert lib.kvh_hash_meow128_2_same_length(bufs[0], bufs[1], L, x) == 0
+    assert lib.kvh_hash_meow128_2_same_length(bufs[2], bufs[3], L, C.c_void_p(C.addressof(x) + 32)) == 0
+    assert list(x) == r["2_same"]
+    x = (C.c_uint64 * 8)(*([s1, s2] * 4))
+    assert lib.kvh_hash_meow128_4_diff_length(bufs[0], L, bufs[1], L, bufs[2], L, bufs[3], L, x) == 0
+    assert list(x) == r["4_diff"]
+    x = (C.c_uint64 * 8)(*([s1, s2] * 4))
+    assert lib.kvh_hash_meow128_4_same_length(bufs[0], bufs[1], bufs[2], bufs[3], L, x) == 0
+    assert list(x) == r["4_same"]
+    x = (C.c_uint64 * 16)(*([s1, s2] * 8))
+    pa = (C.c_void_p * 8)(*[C.cast(b, C.c_void_p) for b in bufs + bufs])
+    assert lib.kvh_hash_meow128_8_same_length_a(pa, L, x) == 0
+    assert list(x) == r["8_same"]
+    x = (C.c_uint64 * 8)(*r["4_same_4_seed"]["seeds"])
+    assert lib.kvh_hash_meow128_4_same_length_4_seed(bufs[0], bufs[1], bufs[2], bufs[3], L, x) == 0
+    assert list(x) == r["4_same_4_seed"]["x"]
+    for i, k in enumerate(keys):
+        a, b = C.c_uint64(s1), C.c_uint64(s2)
+        assert lib.kvh_meow_test(bufs[i], L, C.byref(a), C.byref(b)) == 0
+        assert [a.value, b.value] == r["stream"][i]
+    # KeyFragment / HashSeed mirrors with the fixup
+    hs = kvh.HashSeed(*STATIC)
+    kf = kvh.KeyFragment.from_string("hello")
+    assert hs.hash(kf) == (0x2AA73A1EEB0B2D45 & ~(1 << 63), 0xFD102121185CE157)
+    frags = [kvh.KeyFragment(bytes([i]) * i) for i in range(40)]
+    got = hs.hash_batch(frags)
+    for i, f in enumerate(frags):
+        h1, h2 = orc_meow(ORC, f.data, *STATIC)
+        assert int(got[i, 0]) == int(ORC.orc_fixup(h1)) and int(got[i, 1]) == h2
+
+
+def test_streaming_uneven_updates(kvh):
+    lib = kvh.lib
+    data = bytes(range(256)) * 4
+    for total in (0, 1, 15, 16, 63, 64, 65, 127, 128, 300, 1000):
+        m = C.create_string_buffer(64 + 64)
+        b = C.create_string_buffer(128)
+        # 64-byte alignment of the ctx struct is not needed by the GPU path
+        assert lib.kvh_meow128_init(m, b, 11, 22, total) == 0
+        pos = 0
+        for piece in (3, 64, 1, 70, 200, 1000):
+            take = min(piece, total - pos)
+            if take <= 0:
+                break
+            assert lib.kvh_meow128_update(m, b, C.create_string_buffer(data[pos:pos + take], take), take) == 0
+            pos += take
+        h1, h2 = C.c_uint64(11), C.c_uint64(22)
+        assert lib.kvh_meow128_final(m, b, C.byref(h1), C.byref(h2)) == 0
+        assert (h1.value, h2.value) == orc_meow(ORC, data[:total], 11, 22), total
+
+
+def test_host_pipeline_pinned_and_pageable(kvh):
+    rng = np.random.default_rng(6)
+    n, L = 3_000_001, 16
+    kb = rng.integers(0, 256, n * L, dtype=np.uint8)
+    want = u64(kvh.meow128_fixed(dev(kb), L, STATIC))
+    got = kvh.meow128_fixed_host(kb, L, STATIC)
+    np.testing.assert_array_equal(got, want)
+    pk = torch.from_numpy(kb).pin_memory()
+    po = torch.empty((n, 2), dtype=torch.int64).pin_memory()
+    got2 = kvh.meow128_fixed_host(pk.numpy(), L, STATIC, out=po.numpy().view(np.uint64))
+    np.testing.assert_array_equal(got2, want)
+
+
+def test_full_size_c1_properties(kvh):
+    """BASELINE config C1 at full size (100M x 16 B): sampled oracle parity,
+    agreement of three independent kernels, determinism."""
+    n, L = 100_000_000, 16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234)
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    out = kvh.meow128_fixed(keys, L, STATIC)
+    out2 = kvh.meow128_fixed(keys, L, STATIC)
+    assert torch.equal(out, out2)
+    h = u64(out)
+    idx = np.random.default_rng(7).choice(n, 20000, replace=False)
+    idx.sort()
+    kb = keys.view(n, L)[torch.from_numpy(idx).cuda()].cpu().numpy().reshape(-1)
+    np.testing.assert_array_equal(h[idx], orc_fixed(ORC, kb, L, STATIC))
+    # generic (runtime-length) kernel and variable-length kernel on a 10M prefix
+    m = 10_000_000
+    prev = kvh.lib.kvh_set_tuning(2, 1)
+    try:
+        gen = u64(kvh.meow128_fixed(keys[: m * L], L, STATIC))
+    finally:
+        kvh.lib.kvh_set_tuning(2, prev)
+    np.testing.assert_array_equal(gen, h[:m])
+    offs = torch.arange(0, (m + 1) * L, L, dtype=torch.int64, device="cuda")
+    np.testing.assert_array_equal(u64(kvh.meow128_var(keys, offs, STATIC)), h[:m])
+    assert len(np.unique(h[:1_000_000, 0])) > 999_000  # no degenerate collisions
+
+
+def test_var_10m_zipf_vs_literal_kernel(kvh):
+    from raikv_amd.workload import zipf_lengths, offsets_from_lengths
+    m = 10_000_000
+    lens = zipf_lengths(m, 8, 256, seed=11)
+    offs = offsets_from_lengths(lens)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(99)
+    keys = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device="cuda", generator=g)
+    doff = dev_u64(offs)
+    a = kvh.meow128_var(keys, doff, STATIC)
+    sd = dev_u64(np.tile(np.array(STATIC, dtype=np.uint64), (m, 1)))
+    b = kvh.meow128_var_seeded(keys, doff, sd)
+    assert torch.equal(a, b)
+    idx = np.random.default_rng(8).choice(m, 3000, replace=False)
+    kh = keys.cpu().numpy()
+    ha = u64(a)
+    for i in idx:
+        o0, o1 = int(offs[i]), int(offs[i + 1])
+        assert orc_meow(ORC, kh[o0:o1].tobytes(), *STATIC) == (int(ha[i, 0]), int(ha[i, 1]))
+
+
+def test_cpp_hash_test_program(kvh):
+    exe = os.path.join(ROOT, "tests", "cpp", "hash_test_gpu")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "cpptests"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
