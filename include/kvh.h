@@ -187,7 +187,10 @@ const char *kvh_version(void);
 /* synchronise the current device (host wall-clock timing helpers) */
 int         kvh_device_synchronize(void);
 /* expert tuning knobs (bench/ablation): 0 = tables-per-LDS (2 or 4),
- * 1 = workgroups per CU multiplier, 2 = force generic kernel (0/1).
+ * 1 = workgroups per CU multiplier, 2 = force generic kernel (0/1),
+ * 3 = keys per lane per step in the fixed-length kernel (1, 2 or 4),
+ * 5 = ablation mode of the 16/32-byte kernel (0 product, 1 copy-only,
+ *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3).
  * Returns the previous value or KVH_EINVAL. */
 int         kvh_set_tuning(int knob, int value);
 

@@ -33,20 +33,27 @@ constexpr int kLT = 64;               // full per-length constant records (L < 6
 constexpr int kNF = 256;              // F-only records for 64 <= L < 64 + kNF
 
 // ------------------------------------------------------------ helpers
-template <int L, bool A16>
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
+// Key i of a fixed-length batch as NC 16-byte chunks (zero padded past L).
+// NTM: non-temporal (streamed-once) loads.
+template <int L, bool A16, bool NTM = false>
 __device__ __forceinline__ void load_fixed(const uint8_t* __restrict__ p, Blk* D) {
   constexpr int NC = Plan<L>::NC;
   if constexpr (A16 && (L % 16) == 0) {
 #pragma unroll
     for (int j = 0; j < NC; j++) {
-      const uint4 v = *(const uint4*)(p + 16 * j);
+      const v4u* q = (const v4u*)(p + 16 * j);
+      const v4u v = NTM ? __builtin_nontemporal_load(q) : *q;
       D[j].w[0] = v.x; D[j].w[1] = v.y; D[j].w[2] = v.z; D[j].w[3] = v.w;
     }
   } else {
     // L % 8 == 0 and 8-byte aligned rows
 #pragma unroll
     for (int j = 0; j < L / 8; j++) {
-      const uint2 v = *(const uint2*)(p + 8 * j);
+      const v2u* q = (const v2u*)(p + 8 * j);
+      const v2u v = NTM ? __builtin_nontemporal_load(q) : *q;
       D[j / 2].w[(j & 1) * 2 + 0] = v.x;
       D[j / 2].w[(j & 1) * 2 + 1] = v.y;
     }
@@ -54,39 +61,189 @@ __device__ __forceinline__ void load_fixed(const uint8_t* __restrict__ p, Blk* D
   }
 }
 
+template <bool NTM = false>
 __device__ __forceinline__ void store_h(uint64_t* __restrict__ out, uint64_t idx, Blk h, bool fix) {
   if (fix) h = fixup(h);
-  uint4 v; v.x = h.w[0]; v.y = h.w[1]; v.z = h.w[2]; v.w = h.w[3];
-  *(uint4*)(out + 2 * idx) = v;
+  v4u v;
+  v.x = h.w[0]; v.y = h.w[1]; v.z = h.w[2]; v.w = h.w[3];
+  v4u* q = (v4u*)(out + 2 * idx);
+  if constexpr (NTM) __builtin_nontemporal_store(v, q); else *q = v;
 }
 
 // ------------------------------------------------------------ kernels
-template <int L, int NT, bool A16>
+// Wave-chunked streaming: wave w owns chunks of 64*U consecutive keys
+// (chunk c = keys [64U(w + c*W), 64U(w + c*W + 1)), W = waves in the grid);
+// lane l takes keys base + 64u + l, so every load/store instruction moves
+// one contiguous 64*L-byte (64*16-byte) run.  The U loads of a chunk are all
+// issued before the first round (U independent AES chains per lane hide LDS
+// latency; U loads per lane in flight hide HBM latency), loads and stores are
+// non-temporal (each byte is touched once).  Measured on MI355X this access
+// shape streams 6.2 TB/s where a grid-stride loop with a one-step register
+// prefetch tops out near 5.1 TB/s (tools/mem_probe.hip).
+// Indices past the end are clamped to n-1: those lanes recompute key n-1 and
+// store the identical hash to out[n-1] (benign duplicate), which keeps the
+// chunk body one basic block.
+// MODE (ablation builds, kvh_set_tuning(5, m)): 0 = the product path;
+// 1 = copy keys to out without hashing (memory-only); 2 = no key loads (keys
+// synthesised from the index: LDS + stores); 3 = no stores (hashes folded
+// into one value per lane: LDS + loads).
+template <int L, int NT, bool A16, int U, int MODE = 0>
 __global__ void __launch_bounds__(kBlock)
 k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
         uint64_t* __restrict__ out, uint32_t flags) {
+  constexpr int NC = Plan<L>::NC;
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
   fill_tables<NT>(lds);
   __syncthreads();
   const LdsTab<NT> T(lds);
   const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
   const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  Blk D[Plan<L>::NC];
-  load_fixed<L, A16>(keys + i * L, D);
-  for (;;) {
-    const uint64_t nx = i + stride;
-    Blk E[Plan<L>::NC];
-    const bool more = nx < n;
-    if (more) load_fixed<L, A16>(keys + nx * L, E);  // prefetch next key
-    const Blk h = meow_ct<L>(D, K, T);
-    store_h(out, i, h, fix);
-    if (!more) break;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  const uint64_t last = n - 1;
+  Blk acc = bzero();
+  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
+    Blk D[U][NC];
 #pragma unroll
-    for (int j = 0; j < Plan<L>::NC; j++) D[j] = E[j];
-    i = nx;
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+          for (int w = 0; w < 4; w++) D[u][c].w[w] = (uint32_t)j * 2654435761u + (uint32_t)(4 * c + w);
+      } else {
+        load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
+      }
+    }
+    Blk h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if constexpr (MODE == 1) h[u] = D[u][0];
+      else h[u] = meow_ct<L>(D[u], K, T);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      if constexpr (MODE == 3) acc = bxor(acc, h[u]);
+      else store_h<true>(out, j < last ? j : last, h[u], fix);
+    }
+  }
+  if constexpr (MODE == 3) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < n) store_h(out, g, acc, false);
+  }
+}
+
+// ---------------------------------------------------------------------
+// LDS-DMA streaming (the C1/C4 hot path).  One 1024-thread workgroup per CU:
+// NT replicated tables plus, per wave, a ring of R chunk slots in the SAME
+// __shared__ array (one LDS object: no compiler-inserted vmcnt(0) before the
+// ring reads).  A chunk is 64 consecutive keys (64*L contiguous bytes); the
+// wave streams them into its ring with global_load_lds_dwordx4 (no VGPRs,
+// non-temporal), R-1 chunks ahead of the one it hashes, so the HBM latency is
+// covered by DMA in flight instead of by registers.  Each wave waits for its
+// own chunk with a counted `s_waitcnt vmcnt(N)` (N = DMA and store
+// instructions issued after it), reads its key from LDS, hashes, and stores
+// 16 B per key non-temporally.  Only full chunks take this path; the < 64
+// trailing keys are hashed by the last wave with direct loads.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int L, int NT, int R>
+struct DmaCfg {
+  static constexpr int kWaves = kBlock / 64;
+  static constexpr int CH = 64 * L;                 // chunk bytes
+  static constexpr int D = (CH + 1023) / 1024;      // DMA instructions per chunk
+  static constexpr int S = 1;                       // store instructions per chunk
+  static constexpr int kTabBytes = NT * 8192 * 4;
+  static constexpr int kBytes = kTabBytes + kWaves * R * CH;
+  static constexpr bool kFits = kBytes <= 163840 && L % 16 == 0;
+};
+
+template <int L, int NT, int R>
+__device__ __forceinline__ void dma_chunk(const uint8_t* __restrict__ src, uint32_t* slot, uint32_t lane) {
+  using C = DmaCfg<L, NT, R>;
+#pragma unroll
+  for (int q = 0; q < C::D; q++) {
+    __builtin_amdgcn_global_load_lds((const void*)(src + 1024 * q + 16 * lane),
+                                     (void __attribute__((address_space(3)))*)((char*)slot + 1024 * q),
+                                     16, 0, 2 /* nt */);
+  }
+}
+
+// wait until DMA(k) has landed: after it were issued (R-1) chunk DMAs and
+// min(k, R-1) iterations' stores
+template <int L, int NT, int R>
+__device__ __forceinline__ void wait_chunk(uint64_t k) {
+  using C = DmaCfg<L, NT, R>;
+  constexpr int base = (R - 1) * C::D;
+  if (k >= (uint64_t)(R - 1)) { wait_vmcnt<base + (R - 1) * C::S>(); return; }
+  if constexpr (R > 1) if (k == 0) { wait_vmcnt<base>(); return; }
+  if constexpr (R > 2) if (k == 1) { wait_vmcnt<base + C::S>(); return; }
+  if constexpr (R > 3) if (k == 2) { wait_vmcnt<base + 2 * C::S>(); return; }
+  if constexpr (R > 4) if (k == 3) { wait_vmcnt<base + 3 * C::S>(); return; }
+  if constexpr (R > 5) if (k == 4) { wait_vmcnt<base + 4 * C::S>(); return; }
+  if constexpr (R > 6) if (k == 5) { wait_vmcnt<base + 5 * C::S>(); return; }
+  if constexpr (R > 7) if (k == 6) { wait_vmcnt<base + 6 * C::S>(); return; }
+  wait_vmcnt<0>();
+}
+
+template <int L, int NT, int R>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_dma(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
+            uint64_t* __restrict__ out, uint32_t flags) {
+  using C = DmaCfg<L, NT, R>;
+  static_assert(C::kFits, "LDS budget / 16-byte key pieces");
+  constexpr int NC = Plan<L>::NC;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[C::kBytes / 4];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t gw = (uint64_t)blockIdx.x * C::kWaves + wv;
+  const uint64_t NW = (uint64_t)gridDim.x * C::kWaves;
+  const uint64_t nchunks = n / 64;
+  uint32_t* ring = lds + C::kTabBytes / 4 + wv * (R * C::CH / 4);
+  const uint64_t nk = gw < nchunks ? (nchunks - 1 - gw) / NW + 1 : 0;  // wave-uniform
+  if (nk) {
+    const uint64_t lastc = nchunks - 1;
+    auto src_of = [&](uint64_t k) {
+      const uint64_t c = gw + k * NW;
+      return keys + (c < lastc ? c : lastc) * (uint64_t)C::CH;
+    };
+#pragma unroll
+    for (int k = 0; k < R - 1; k++) dma_chunk<L, NT, R>(src_of(k), ring + k * (C::CH / 4), lane);
+    for (uint64_t k = 0; k < nk; k++) {
+      const uint64_t kn = k + R - 1;
+      dma_chunk<L, NT, R>(src_of(kn), ring + (kn % R) * (C::CH / 4), lane);
+      wait_chunk<L, NT, R>(k);
+      const uint32_t* slot = ring + (k % R) * (C::CH / 4);
+      Blk D[NC];
+#pragma unroll
+      for (int j = 0; j < NC; j++) {
+        const v4u v = *(const v4u*)((const char*)slot + lane * L + 16 * j);
+        D[j].w[0] = v.x; D[j].w[1] = v.y; D[j].w[2] = v.z; D[j].w[3] = v.w;
+      }
+      const Blk h = meow_ct<L>(D, K, T);
+      store_h<true>(out, (gw + k * NW) * 64 + lane, h, fix);
+    }
+    wait_vmcnt<0>();  // drain the trailing dummy DMAs before the wave exits
+  }
+  // keys past the last full chunk
+  if (gw == NW - 1) {
+    const uint64_t j = nchunks * 64 + lane;
+    if (j < n) {
+      Blk D[NC];
+      load_fixed<L, true>(keys + j * L, D);
+      store_h(out, j, meow_ct<L>(D, K, T), fix);
+    }
   }
 }
 
@@ -196,6 +353,127 @@ k_generic(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, u
   }
 }
 
+// ---------------------------------------------------------------------
+// Variable-length batches (config C2).  One lane per key, but NOT in input
+// order: each workgroup takes a window of 1024 consecutive keys, counting-
+// sorts them by length in LDS (LDS atomics + one wave-wide scan), and every
+// wave then hashes 64 keys of (nearly) equal length, so the absorb loop trip
+// count and every trail/finalisation branch are (nearly) wave-uniform.  The
+// window's key bytes (~50 KB for C2) stay L2-resident while its waves gather
+// their keys with dword-aligned dwordx4 loads; hashes are scattered back to
+// the keys' original slots.  Per-length constants live in LDS: the full
+// folding record for L < 64 and the first-absorb folds F[i] for
+// 64 <= L < 64 + NF; longer keys fold in-lane.
+template <int NT>
+struct VarCfg {
+  static constexpr int kNF = NT == 4 ? 32 : 256;
+  static constexpr int kTab = NT * 8192 * 4;
+  static constexpr int kFull = kTab;                                 // MeowConst[kLT]
+  static constexpr int kFOff = kFull + kLT * (int)sizeof(MeowConst); // Blk[kNF][4]
+  static constexpr int kCnt = kFOff + kNF * 4 * 16;                  // u32[320] counts / starts
+  static constexpr int kRecO = kCnt + 320 * 4;                       // u64[1024] sorted key start
+  static constexpr int kRecL = kRecO + kBlock * 8;                   // u32[1024] sorted key length
+  static constexpr int kRecI = kRecL + kBlock * 4;                   // u16[1024] sorted -> window slot
+  static constexpr int kBytes = kRecI + kBlock * 2;
+  static_assert(kBytes <= 163840, "LDS budget");
+};
+
+template <class Tab, int NF>
+struct LdsKV {
+  const MeowConst* full;
+  const Blk* ftab;
+  uint32_t L;
+  Blk m;
+  const Tab& T;
+  __device__ __forceinline__ LdsKV(const MeowConst* f, const Blk* ft, uint32_t len, uint64_t s1, uint64_t s2,
+                                   const Tab& t)
+      : full(f), ftab(ft), L(len), m(mixer(s1, s2, len)), T(t) {}
+  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ Blk M() const { return m; }
+  __device__ __forceinline__ Blk F(int i) const {
+    if (L < (uint32_t)kLT) return full[L].F[i];
+    if (L < (uint32_t)(kLT + NF)) return ftab[(L - kLT) * 4 + i];
+    return aesT(bxor(ramp(i), m), T);
+  }
+  __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
+  __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
+  __device__ __forceinline__ Blk CS2b() const { return full[li()].CS2b; }
+  __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
+};
+
+template <int NT>
+__global__ void __launch_bounds__(kBlock)
+k_var(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+      uint64_t* __restrict__ out, uint32_t flags) {
+  using C = VarCfg<NT>;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[C::kBytes / 4];
+  MeowConst* kfull = (MeowConst*)((char*)lds + C::kFull);
+  Blk* kf = (Blk*)((char*)lds + C::kFOff);
+  uint32_t* cnt = (uint32_t*)((char*)lds + C::kCnt);
+  uint64_t* rec_o = (uint64_t*)((char*)lds + C::kRecO);
+  uint32_t* rec_l = (uint32_t*)((char*)lds + C::kRecL);
+  uint16_t* rec_i = (uint16_t*)((char*)lds + C::kRecI);
+  fill_tables<NT>(lds);
+  for (uint32_t b = threadIdx.x; b < 320; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + C::kNF); l += blockDim.x) {
+    if (l < (uint32_t)kLT) {
+      kfull[l] = make_const(s1, s2, l, T);
+    } else {
+      const Blk M = mixer(s1, s2, l);
+#pragma unroll
+      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), M), T);
+    }
+  }
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  const uint64_t wstep = (uint64_t)gridDim.x * kBlock;
+  uint64_t base = (uint64_t)blockIdx.x * kBlock;
+  // offsets of this thread's key in the first window (prefetched one window ahead)
+  uint64_t p0 = 0, p1 = 0;
+  if (base + t < n) { p0 = offs[base + t]; p1 = offs[base + t + 1]; }
+  for (; base < n; base += wstep) {
+    const uint64_t o0 = p0, o1 = p1;
+    const uint64_t nxt = base + wstep + t;
+    if (nxt < n) { p0 = offs[nxt]; p1 = offs[nxt + 1]; }
+    const bool valid = base + t < n;
+    const uint32_t L = (uint32_t)(o1 - o0);
+    const uint32_t bucket = valid ? (L < 255u ? L : 255u) : 300u;  // past-the-end keys sort last
+    atomicAdd(&cnt[bucket], 1u);
+    __syncthreads();
+    if (t < 64) {  // exclusive scan of 320 counts by one wave: 5 per lane
+      uint32_t v[5], sum = 0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) { v[k] = cnt[lane * 5 + k]; sum += v[k]; }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+      }
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int k = 0; k < 5; k++) { cnt[lane * 5 + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+    const uint32_t pos = atomicAdd(&cnt[bucket], 1u);
+    rec_o[pos] = o0;
+    rec_l[pos] = L;
+    rec_i[pos] = (uint16_t)t;
+    __syncthreads();
+    const uint64_t ko = rec_o[t];
+    const uint32_t kl = rec_l[t];
+    const uint64_t j = base + rec_i[t];
+    cnt[t < 320 ? t : 319] = 0;  // ready for the next window (read only before the barrier above)
+    if (j < n) {
+      const LdsKV<LdsTab<NT>, C::kNF> K(kfull, kf, kl, s1, s2, T);
+      store_h(out, j, meow_var(keys + ko, kl, K, T), fix);
+    }
+    __syncthreads();  // rec_* / cnt reuse by the next window
+  }
+}
+
 // straight-line restatement, one thread per key, per-key seeds
 __global__ void __launch_bounds__(256)
 k_seeded(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
@@ -240,9 +518,13 @@ struct DevInfo {
 };
 std::mutex g_mu;
 std::vector<DevInfo> g_dev;
-int g_tune_nt = 4;        // tables per LDS: 2 or 4
+int g_tune_nt = 2;        // tables per LDS: 2 or 4
 int g_tune_wgmul = 1;     // workgroups per CU multiplier
 int g_tune_generic = 0;   // force the generic kernel
+int g_tune_kpl = 2;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8)
+int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
+int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
+int g_tune_var = 0;       // var-length kernel: 0 = unsorted k_generic, 2/4 = windowed sort (NT tables)
 
 int set_err(int e) { t_last_err = e; return e; }
 int hip_err(hipError_t e) { return set_err(KVH_EHIP_BASE - (int)e); }
@@ -276,23 +558,64 @@ int launch_done() {
   return set_err(0);
 }
 
-template <int L, int NT>
-int launch_fixed_L(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
-                   uint32_t flags, hipStream_t st, int cus) {
+template <int L, int NT, int U, int MODE = 0>
+int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,
+             hipStream_t st, int cus) {
   const bool a16 = ((uintptr_t)keys & 15) == 0;
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
   if (a16)
-    hipLaunchKernelGGL((k_fixed<L, NT, true>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+    hipLaunchKernelGGL((k_fixed<L, NT, true, U, MODE>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
   else
-    hipLaunchKernelGGL((k_fixed<L, NT, false>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+    hipLaunchKernelGGL((k_fixed<L, NT, false, U, MODE>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
   return launch_done();
 }
 
+// Default (NT, U) per length from tools/tune.py sweeps; the tuning knobs
+// override them for the benchmark lengths (16, 32) only.
 template <int L>
 int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
                     uint32_t flags, hipStream_t st, int cus) {
-  if (g_tune_nt == 2) return launch_fixed_L<L, 2>(keys, n, s1, s2, out, flags, st, cus);
-  return launch_fixed_L<L, 4>(keys, n, s1, s2, out, flags, st, cus);
+  if constexpr (L == 16 || L == 32) {
+    if (g_tune_ablate) {
+      switch (g_tune_ablate) {
+        case 1: return launch_k<L, 2, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
+        case 2: return launch_k<L, 2, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
+        case 3: return launch_k<L, 2, 4, 3>(keys, n, s1, s2, out, flags, st, cus);
+        default: return set_err(KVH_EINVAL);
+      }
+    }
+    if (g_tune_dma && ((uintptr_t)keys & 15) == 0) {
+      const int dk = g_tune_nt * 10 + g_tune_dma;
+      const uint32_t grid = grid_for(n, cus, 1);
+      switch (dk) {
+#define KVH_DMA(NTv, Rv)                                                                              \
+  case NTv * 10 + Rv:                                                                                 \
+    if constexpr (DmaCfg<L, NTv, Rv>::kFits) {                                                        \
+      hipLaunchKernelGGL((k_fixed_dma<L, NTv, Rv>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, \
+                         flags);                                                                       \
+      return launch_done();                                                                           \
+    }                                                                                                 \
+    break;
+        KVH_DMA(2, 2) KVH_DMA(2, 3) KVH_DMA(2, 4) KVH_DMA(2, 6) KVH_DMA(4, 2)
+#undef KVH_DMA
+        default: break;
+      }
+    }
+    const int key = g_tune_nt * 100 + g_tune_kpl;
+    switch (key) {
+      case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
+      case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
+      case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
+      case 408: return launch_k<L, 4, 8>(keys, n, s1, s2, out, flags, st, cus);
+      case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
+      case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
+      case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
+      case 208: return launch_k<L, 2, 8>(keys, n, s1, s2, out, flags, st, cus);
+      default: return set_err(KVH_EINVAL);
+    }
+  } else {
+    return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
+  }
 }
 
 template <int L>
@@ -444,9 +767,19 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
   if (!keys || !offsets || !out) return set_err(KVH_EINVAL);
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
-  uint64_t s[16] = {seed1, seed2};
-  return launch_generic(true, (const uint8_t*)keys, offsets, 0, n, s, 1, out, flags, (hipStream_t)stream,
-                        cus);
+  if (g_tune_var == 0) {
+    uint64_t s[16] = {seed1, seed2};
+    return launch_generic(true, (const uint8_t*)keys, offsets, 0, n, s, 1, out, flags, (hipStream_t)stream,
+                          cus);
+  }
+  const uint32_t grid = grid_for(n, cus, 1);
+  if (g_tune_var == 4)
+    hipLaunchKernelGGL((k_var<4>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
+                       offsets, (uint64_t)n, seed1, seed2, out, flags);
+  else
+    hipLaunchKernelGGL((k_var<2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
+                       offsets, (uint64_t)n, seed1, seed2, out, flags);
+  return launch_done();
 }
 
 int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const uint64_t* seeds,
@@ -759,6 +1092,12 @@ int kvh_set_tuning(int knob, int value) {
     case 0: if (value != 2 && value != 4) return KVH_EINVAL; prev = g_tune_nt; g_tune_nt = value; return prev;
     case 1: if (value < 1 || value > 8) return KVH_EINVAL; prev = g_tune_wgmul; g_tune_wgmul = value; return prev;
     case 2: prev = g_tune_generic; g_tune_generic = value ? 1 : 0; return prev;
+    case 3: if (value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_kpl; g_tune_kpl = value; return prev;
+    case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
+    case 7: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL;
+            prev = g_tune_var; g_tune_var = value; return prev;
+    case 6: if (value != 0 && value != 2 && value != 3 && value != 4 && value != 6) return KVH_EINVAL;
+            prev = g_tune_dma; g_tune_dma = value; return prev;
     default: return KVH_EINVAL;
   }
 }

@@ -274,6 +274,25 @@ __device__ __forceinline__ Blk load_bytes(const uint8_t* p, uint32_t n) {
   return r;
 }
 
+// 16 bytes at any byte address p whose 16 bytes are all valid: one dwordx4
+// from the enclosing dword-aligned address (every dword of it holds a byte of
+// [p-3, p+16), so it never leaves the key's pages) plus one more dword when p
+// is not dword aligned, funnel-shifted with v_alignbyte.
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ Blk load16_full(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const u32x4_a4 v = *(const u32x4_a4*)q;
+  const uint32_t e = sh ? q[4] : 0u;
+  Blk r;
+  r.w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+  r.w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+  r.w[2] = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+  r.w[3] = __builtin_amdgcn_alignbyte(e, v.w, sh);
+  return r;
+}
+
 // Source of per-length constants for the runtime path.
 struct ConstRef {
   const MeowConst* k;
@@ -287,14 +306,14 @@ __device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet&
   const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
   Blk S0, S1, S2, S3;
   if (nb > 0) {
-    Blk k0 = load_bytes(p, 16), k1 = load_bytes(p + 16, 16), k2 = load_bytes(p + 32, 16),
-        k3 = load_bytes(p + 48, 16);
+    Blk k0 = load16_full(p), k1 = load16_full(p + 16), k2 = load16_full(p + 32),
+        k3 = load16_full(p + 48);
     S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
     S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
     for (uint32_t b = 1; b < nb; b++) {
       const uint8_t* q = p + 64 * b;
-      k0 = load_bytes(q, 16); k1 = load_bytes(q + 16, 16);
-      k2 = load_bytes(q + 32, 16); k3 = load_bytes(q + 48, 16);
+      k0 = load16_full(q); k1 = load16_full(q + 16);
+      k2 = load16_full(q + 32); k3 = load16_full(q + 48);
       S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
       S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
     }
@@ -307,19 +326,70 @@ __device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet&
     S3 = first ? aesdec(bxor(K.F(3), k), k, T) : aesdec(aesdec(S3, k, T), k, T);
   }
   if (C >= 48) {
-    const Blk k = load_bytes(q + 32, 16);
+    const Blk k = load16_full(q + 32);
     S2 = first ? aesdec(bxor(K.F(2), k), k, T) : aesdec(aesdec(S2, k, T), k, T);
   }
   if (C >= 32) {
-    const Blk k = load_bytes(q + 16, 16);
+    const Blk k = load16_full(q + 16);
     S1 = first ? aesdec(bxor(K.F(1), k), k, T) : aesdec(aesdec(S1, k, T), k, T);
   }
   if (C >= 16) {
-    const Blk k = load_bytes(q, 16);
+    const Blk k = load16_full(q);
     S0 = first ? aesdec(bxor(K.F(0), k), k, T) : aesdec(aesdec(S0, k, T), k, T);
   }
   const bool T0 = !first || C >= 16, T1 = !first || C >= 32, T2 = !first || C >= 48,
              T3 = !first || t != 0;
+  const Blk M = K.M();
+  S3 = T3 ? aesdec(S3, M, T) : K.G(3);
+  S2 = T2 ? aesdec(S2, M, T) : K.G(2);
+  S1 = T1 ? aesdec(S1, M, T) : K.G(1);
+  S0 = T0 ? aesdec(S0, M, T) : K.G(0);
+  Blk S2b;
+  if (T2) S2b = aesdec(aesdec(S2, S3, T), M, T);
+  else if (T3) S2b = aesdec(bxor(K.TG2(), S3), M, T);
+  else S2b = K.CS2b();
+  Blk S0b;
+  if (T0) S0b = aesdec(aesdec(S0, S1, T), S2b, T);
+  else S0b = bxor(K.TCS0a(), S2b);
+  return aesdec(S0b, M, T);
+}
+
+// Variable-length Meow with every load issued before the rounds that need
+// it: the trail chunks and block 0 are requested up front, block b+1 while
+// block b is absorbed.  Same dataflow and folding as meow_rt.
+template <class Tab, class KGet>
+__device__ __forceinline__ Blk meow_var(const uint8_t* p, uint32_t L, const KGet& K, const Tab& T) {
+  const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
+  const uint8_t* q = p + 64 * (uint64_t)nb;
+  const Blk z = bzero();
+  // trail chunks (key_hash.c:1200-1210) and the first full block, all in flight together
+  const Blk r3 = t ? load_bytes(q + C, t) : z;
+  const Blk r2 = C >= 48 ? load16_full(q + 32) : z;
+  const Blk r1 = C >= 32 ? load16_full(q + 16) : z;
+  const Blk r0 = C >= 16 ? load16_full(q) : z;
+  Blk S0, S1, S2, S3;
+  if (nb > 0) {
+    Blk k0 = load16_full(p), k1 = load16_full(p + 16), k2 = load16_full(p + 32), k3 = load16_full(p + 48);
+    Blk n0 = z, n1 = z, n2 = z, n3 = z;
+    if (nb > 1) { n0 = load16_full(p + 64); n1 = load16_full(p + 80); n2 = load16_full(p + 96); n3 = load16_full(p + 112); }
+    S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
+    S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
+    for (uint32_t b = 1; b < nb; b++) {
+      k0 = n0; k1 = n1; k2 = n2; k3 = n3;
+      if (b + 1 < nb) {
+        const uint8_t* r = p + 64 * (uint64_t)(b + 1);
+        n0 = load16_full(r); n1 = load16_full(r + 16); n2 = load16_full(r + 32); n3 = load16_full(r + 48);
+      }
+      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+    }
+  }
+  const bool first = nb == 0;
+  if (t) S3 = first ? aesdec(bxor(K.F(3), r3), r3, T) : aesdec(aesdec(S3, r3, T), r3, T);
+  if (C >= 48) S2 = first ? aesdec(bxor(K.F(2), r2), r2, T) : aesdec(aesdec(S2, r2, T), r2, T);
+  if (C >= 32) S1 = first ? aesdec(bxor(K.F(1), r1), r1, T) : aesdec(aesdec(S1, r1, T), r1, T);
+  if (C >= 16) S0 = first ? aesdec(bxor(K.F(0), r0), r0, T) : aesdec(aesdec(S0, r0, T), r0, T);
+  const bool T0 = !first || C >= 16, T1 = !first || C >= 32, T2 = !first || C >= 48, T3 = !first || t != 0;
   const Blk M = K.M();
   S3 = T3 ? aesdec(S3, M, T) : K.G(3);
   S2 = T2 ? aesdec(S2, M, T) : K.G(2);

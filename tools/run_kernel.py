@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Run one workload's kernel a few times (profiling target for rocprofv3)."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import raikv_amd as kvh  # noqa: E402
+from raikv_amd.workload import C3_SEEDS, offsets_from_lengths, zipf_lengths  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c1")
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--n", type=int, default=0)
+ap.add_argument("--nt", type=int, default=0)
+ap.add_argument("--kpl", type=int, default=0)
+a = ap.parse_args()
+if a.nt:
+    kvh.lib.kvh_set_tuning(0, a.nt)
+if a.kpl:
+    kvh.lib.kvh_set_tuning(3, a.kpl)
+torch.cuda.set_device(0)
+g = torch.Generator(device="cuda")
+g.manual_seed(1)
+cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1)}
+n, L, ar = cfg[a.config]
+n = a.n or n
+if L == 0:
+    offs = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=3))
+    keys = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device="cuda", generator=g)
+    doff = torch.from_numpy(offs.view(np.int64)).cuda()
+    f = lambda: kvh.meow128_var(keys, doff, kvh.STATIC_SEED)
+else:
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    if ar == 1:
+        f = lambda: kvh.meow128_fixed(keys, L, kvh.STATIC_SEED)
+    else:
+        f = lambda: kvh.meow128_multiseed(keys, L, list(C3_SEEDS[:ar]))
+for _ in range(a.reps):
+    f()
+torch.cuda.synchronize()
+print("ran", a.config, n, a.reps)
