@@ -118,13 +118,10 @@ def main():
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("gloo")  # control plane only: barrier + max time
+    from raikv_amd import dist as kdist
+    rank, world, local = kdist.env_ranks()
+    kdist.init(world)  # gloo control plane only: barrier + max time
     torch.cuda.set_device(local)
     import raikv_amd as kvh
     from raikv_amd.workload import STATIC_SEED, C3_SEEDS, zipf_lengths, offsets_from_lengths
@@ -162,8 +159,7 @@ def main():
     for _ in range(args.warmup):
         run(out)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    kdist.barrier(world)
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
@@ -172,15 +168,11 @@ def main():
         run(out)
         b.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    kdist.barrier(world)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    wall_t = torch.tensor([wall], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    wall = float(wall_t.item())
+    wall = kdist.reduce_max(wall, world)
 
     hashes = n * arity * args.steps * world
     value = hashes / wall
@@ -217,9 +209,7 @@ def main():
             res["cpu_baseline"] = cpu_baseline(cfg, seed, args.cpu_seconds)
         except Exception as e:  # report, never hide
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    kdist.finalize(world)
     if rank == 0:
         print(json.dumps(res), flush=True)
 

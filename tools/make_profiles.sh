@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round profiling on the GPU box: for each bench config, a rocprofv3
+# kernel-trace summary of the bench command itself, plus FETCH_SIZE and
+# WRITE_SIZE passes (separate runs, as the MI355X guide prescribes).
+# usage: tools/make_profiles.sh <outdir> [configs...]
+set -o pipefail
+OUT=${1:-gpurun_out/profiles}; shift
+CFGS=${@:-c1 c2 c3 c4}
+export TMPDIR=/tmp
+mkdir -p $OUT
+for c in $CFGS; do
+  mkdir -p $OUT/$c
+  B="python3 bench.py --config $c --steps 30 --warmup 30 --no-cpu-baseline"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- $B > $OUT/$c/bench.json 2> $OUT/$c/trace.err || exit 1
+  R="python3 tools/run_kernel.py --config $c --reps 5"
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- $R > $OUT/$c/fetch.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- $R > $OUT/$c/write.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU --output-format csv -d $OUT/$c/sq -o run -- $R > $OUT/$c/sq.log 2>&1 || exit 1
+  python3 tools/pmc_summary.py $OUT/$c/fetch $OUT/$c/write $OUT/$c/sq > $OUT/$c/pmc_summary.json || exit 1
+done
