@@ -136,6 +136,58 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
   }
 }
 
+// Multi-seed (config C3, kv_hash_meow128_4_same_length_4_seed with one key
+// in all slots, key_hash.c:1891-1937): LA = 2, 4 or 8 lanes per key, lane l
+// hashes under seed (l & (LA-1)).  The output slot of (key i, seed a) is
+// i*LA + a, so lane j of a chunk writes slot j: every store is one contiguous
+// 1 KiB run (one lane per key with LA strided 16-byte stores inflated the
+// write traffic 1.3x).  The LA lanes of a key load the same 16-byte pieces
+// (same cache line, one request).  Constants are per lane (VGPRs), computed
+// once in the prologue for the lane's fixed seed.
+template <int L, int NT, bool A16, int U, int LA>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_lanes(const uint8_t* __restrict__ keys, uint64_t n, uint64_t* __restrict__ out, uint32_t flags,
+              uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2, uint64_t a3,
+              uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5, uint64_t a6, uint64_t b6,
+              uint64_t a7, uint64_t b7) {
+  static_assert(LA == 2 || LA == 4 || LA == 8, "lanes per key");
+  constexpr int NC = Plan<L>::NC;
+  constexpr int SH = LA == 2 ? 1 : LA == 4 ? 2 : 3;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const uint32_t sl = threadIdx.x & (LA - 1);
+  const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
+  const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
+  uint64_t s1 = sa[0], s2 = sb[0];
+#pragma unroll
+  for (int q = 1; q < LA; q++)
+    if (sl == (uint32_t)q) { s1 = sa[q]; s2 = sb[q]; }
+  const MeowConst K = make_const(s1, s2, (uint64_t)L, T);
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  const uint64_t ns = n << SH, lastk = n - 1;
+  for (uint64_t b = wave * 64 * U; b < ns; b += step) {
+    Blk D[U][NC];
+    uint64_t slot[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t k = (b + 64 * u + lane) >> SH;
+      k = k < lastk ? k : lastk;
+      slot[u] = (k << SH) | sl;
+      load_fixed<L, A16, true>(keys + k * L, D[u]);
+    }
+    Blk h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
+#pragma unroll
+    for (int u = 0; u < U; u++) store_h<true>(out, slot[u], h[u], fix);
+  }
+}
+
 // ---------------------------------------------------------------------
 // LDS-DMA streaming (the C1/C4 hot path).  One 1024-thread workgroup per CU:
 // NT replicated tables plus, per wave, a ring of R chunk slots in the SAME
@@ -524,6 +576,7 @@ int g_tune_generic = 0;   // force the generic kernel
 int g_tune_kpl = 2;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8)
 int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
 int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
+int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
 int g_tune_var = 0;       // var-length kernel: 0 = unsorted k_generic, 2/4 = windowed sort (NT tables)
 
 int set_err(int e) { t_last_err = e; return e; }
@@ -616,6 +669,24 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
   } else {
     return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
   }
+}
+
+template <int L>
+int launch_lanes_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
+                   uint32_t flags, hipStream_t st, int cus) {
+  const bool a16 = ((uintptr_t)keys & 15) == 0;
+  const uint32_t grid = grid_for(n * arity, cus, 2);
+#define KVH_LANES(A16v, LAv)                                                                            \
+  hipLaunchKernelGGL((k_fixed_lanes<L, 2, A16v, 2, LAv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \
+                     s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13],   \
+                     s[14], s[15])
+  if (a16) {
+    if (arity == 2) KVH_LANES(true, 2); else if (arity == 4) KVH_LANES(true, 4); else KVH_LANES(true, 8);
+  } else {
+    if (arity == 2) KVH_LANES(false, 2); else if (arity == 4) KVH_LANES(false, 4); else KVH_LANES(false, 8);
+  }
+#undef KVH_LANES
+  return launch_done();
 }
 
 template <int L>
@@ -794,6 +865,19 @@ int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const ui
   const uint8_t* k = (const uint8_t*)keys;
   hipStream_t st = (hipStream_t)stream;
   const bool a8 = ((uintptr_t)k & 7) == 0;
+  if (!g_tune_generic && a8 && g_tune_ms_lanes && (arity == 2 || arity == 4 || arity == 8)) {
+    switch (key_len) {
+      case 8: return launch_lanes_L<8>(k, n, s, arity, out, flags, st, cus);
+      case 16: return launch_lanes_L<16>(k, n, s, arity, out, flags, st, cus);
+      case 24: return launch_lanes_L<24>(k, n, s, arity, out, flags, st, cus);
+      case 32: return launch_lanes_L<32>(k, n, s, arity, out, flags, st, cus);
+      case 40: return launch_lanes_L<40>(k, n, s, arity, out, flags, st, cus);
+      case 48: return launch_lanes_L<48>(k, n, s, arity, out, flags, st, cus);
+      case 56: return launch_lanes_L<56>(k, n, s, arity, out, flags, st, cus);
+      case 64: return launch_lanes_L<64>(k, n, s, arity, out, flags, st, cus);
+      default: break;
+    }
+  }
   if (!g_tune_generic && a8) {
     switch (key_len) {
       case 16: return launch_ms_L<16>(k, n, s, arity, out, flags, st, cus);
@@ -1094,6 +1178,7 @@ int kvh_set_tuning(int knob, int value) {
     case 2: prev = g_tune_generic; g_tune_generic = value ? 1 : 0; return prev;
     case 3: if (value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_kpl; g_tune_kpl = value; return prev;
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
+    case 8: prev = g_tune_ms_lanes; g_tune_ms_lanes = value ? 1 : 0; return prev;
     case 7: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL;
             prev = g_tune_var; g_tune_var = value; return prev;
     case 6: if (value != 0 && value != 2 && value != 3 && value != 4 && value != 6) return KVH_EINVAL;
