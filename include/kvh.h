@@ -193,6 +193,8 @@ int         kvh_device_synchronize(void);
  *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3).
  * Returns the previous value or KVH_EINVAL. */
 int         kvh_set_tuning(int knob, int value);
+/* diagnostics: per-wave phase cycle stamps of the last stamped launch */
+int         kvh_debug_stamps(uint64_t *host, size_t count);
 
 #ifdef __cplusplus
 }

@@ -526,6 +526,376 @@ k_var(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint6
   }
 }
 
+// k_var3: windows of KPT*1024 keys per workgroup.
+//  [A] each thread loads the offsets of its KPT window keys (kept in VGPRs)
+//      and counts them into 256 length buckets (LDS atomics);
+//  [B] one wave scans the counts; threads scatter records {u64 start,
+//      u32 length, u16 window slot} in length order;
+//  [C] thread t reads its sorted records t, t+1024, ... and hashes them with
+//      the first pieces of the next key already in flight (prefetch_first):
+//      the keys of a wave have (nearly) one length, so trip counts and
+//      trail/finalisation branches are (nearly) uniform;
+//  [D] hashes are staged in LDS by window slot (the record area, free after
+//      [C] has read it) and written back as contiguous 16-byte runs -- a
+//      scattered 16-byte store per key doubled the HBM write traffic.
+template <int NT, int KPT>
+struct Var3Cfg {
+  static constexpr int W = KPT * kBlock;
+  static constexpr int kTab = NT * 8192 * 4;
+  static constexpr int kFull = kTab;                                   // MeowConst[kLT]
+  static constexpr int kCnt = kFull + kLT * (int)sizeof(MeowConst);    // u32[320]
+  static constexpr int kU = kCnt + 320 * 4;                            // union area
+  static constexpr int kRecO = kU;                                     // u64[W]
+  static constexpr int kRecL = kRecO + W * 8;                          // u32[W]
+  static constexpr int kRecI = kRecL + W * 4;                          // u16[W]
+  static constexpr int kRecEnd = kRecI + W * 2;
+  static constexpr int kOutEnd = kU + W * 16;                          // Blk[W] staged hashes
+  static constexpr int kBytes = kRecEnd > kOutEnd ? kRecEnd : kOutEnd;
+  static_assert(kBytes <= 163840, "LDS budget");
+};
+
+template <int NT, int KPT, int MODE = 0>
+__global__ void __launch_bounds__(kBlock)
+k_var3(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+       uint64_t* __restrict__ out, uint32_t flags) {
+  using C = Var3Cfg<NT, KPT>;
+  constexpr uint32_t W = C::W;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[C::kBytes / 4];
+  MeowConst* kfull = (MeowConst*)((char*)lds + C::kFull);
+  uint32_t* cnt = (uint32_t*)((char*)lds + C::kCnt);
+  uint64_t* rec_o = (uint64_t*)((char*)lds + C::kRecO);
+  uint32_t* rec_l = (uint32_t*)((char*)lds + C::kRecL);
+  uint16_t* rec_i = (uint16_t*)((char*)lds + C::kRecI);
+  Blk* hout = (Blk*)((char*)lds + C::kU);
+  fill_tables<NT>(lds);
+  for (uint32_t b = threadIdx.x; b < 320; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) kfull[l] = make_const(s1, s2, l, T);
+  const Blk* nofold = nullptr;
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  for (uint64_t base = (uint64_t)blockIdx.x * W; base < n; base += (uint64_t)gridDim.x * W) {
+    const uint64_t wend = base + W < n ? base + W : n;
+    const uint32_t nw = (uint32_t)(wend - base);
+    // [A]
+    uint64_t o0[KPT], o1[KPT];
+    uint32_t bk[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const uint32_t s = t + k * kBlock;
+      o0[k] = o1[k] = 0;
+      if (s < nw) { o0[k] = offs[base + s]; o1[k] = offs[base + s + 1]; }
+    }
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const uint64_t L = o1[k] - o0[k];
+      bk[k] = (t + k * kBlock < nw) ? (L < 255 ? (uint32_t)L : 255u) : 300u;
+      atomicAdd(&cnt[bk[k]], 1u);
+    }
+    __syncthreads();
+    // [B]
+    if (t < 64) {
+      uint32_t v[5], sum = 0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) { v[k] = cnt[lane * 5 + k]; sum += v[k]; }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+      }
+      uint32_t run = incl - sum;
+#pragma unroll
+      for (int k = 0; k < 5; k++) { cnt[lane * 5 + k] = run; run += v[k]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const uint32_t pos = MODE == 3 ? t + k * kBlock : atomicAdd(&cnt[bk[k]], 1u);
+      rec_o[pos] = o0[k];
+      rec_l[pos] = (uint32_t)(o1[k] - o0[k]);
+      rec_i[pos] = (uint16_t)(t + k * kBlock);
+    }
+    __syncthreads();
+    // [C]
+    uint64_t ko[KPT];
+    uint32_t kl[KPT], ki[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const uint32_t s = t + k * kBlock;
+      ko[k] = rec_o[s]; kl[k] = rec_l[s]; ki[k] = rec_i[s];
+    }
+    for (uint32_t b = t; b < 320; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();  // records consumed: the area now stages hashes
+    Blk pre[4] = {bzero(), bzero(), bzero(), bzero()};
+    if (MODE != 2 && t < nw) prefetch_first(keys + ko[0], kl[0], pre);
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const uint32_t s = t + k * kBlock;
+      Blk npre[4] = {bzero(), bzero(), bzero(), bzero()};
+      if (MODE != 2 && k + 1 < KPT && s + kBlock < nw) prefetch_first(keys + ko[k + 1], kl[k + 1], npre);
+      if (s < nw) {
+        const LdsKV<LdsTab<NT>, 0> K(kfull, nofold, kl[k], s1, s2, T);
+        Blk h;
+        if constexpr (MODE == 1) h = bxor(bxor(pre[0], pre[1]), bxor(pre[2], pre[3]));
+        else if constexpr (MODE == 2) {
+          Blk sy[4];
+          for (int q = 0; q < 4; q++) for (int w = 0; w < 4; w++) sy[q].w[w] = (uint32_t)ko[k] * 2654435761u + q * 4 + w;
+          h = meow_var_pre(keys, kl[k] < 64 ? kl[k] : (kl[k] & 63), sy, K, T);
+        } else h = meow_var_pre(keys + ko[k], kl[k], pre, K, T);
+        if (fix) h = fixup(h);
+        hout[ki[k]] = h;
+      }
+      if (k + 1 < KPT) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) pre[q] = npre[q];
+      }
+    }
+    __syncthreads();
+    // [D]
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+      const uint32_t s = t + k * kBlock;
+      if (s < nw) store_h<true>(out, base + s, hout[s], false);
+    }
+    __syncthreads();  // staging area reuse
+  }
+}
+
+// k_var5: windows of 1024 keys; the window's contiguous key bytes are
+// streamed into an LDS staging buffer by LDS-DMA (coalesced 1 KiB pieces)
+// while the window is counting-sorted by length.  The sorted list is then
+// cut into 16 WORK-BALANCED contiguous ranges, one per wave (work of a key ~
+// its table rounds), and each wave hashes its range 64 lanes at a time:
+// lanes of a step hold (nearly) equal lengths, and no wave idles at the
+// window barrier while another hashes the longest keys.  Key bytes are read
+// from LDS; hashes are staged in LDS in sorted order and written back
+// through the inverse permutation as contiguous 16-byte runs.  (Gathering
+// keys straight from HBM/L2 ran at ~2.4 TB/s; equal-size per-wave slices of
+// the sorted list left 3/4 of the waves idle at the barrier.)  A window
+// whose bytes exceed the staging buffer (~0.2 % for zipf 8-256 B keys)
+// gathers from global memory instead.
+struct VConst {  // MeowConst minus the Mixer (recomputed in-lane)
+  Blk F[4], G[4], TG2, CS2b, TCS0a;
+};
+
+template <class Tab>
+struct LdsKV5 {
+  const VConst* full;
+  uint32_t L;
+  Blk m;
+  const Tab& T;
+  __device__ __forceinline__ LdsKV5(const VConst* f, uint32_t len, uint64_t s1, uint64_t s2, const Tab& t)
+      : full(f), L(len), m(mixer(s1, s2, len)), T(t) {}
+  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ Blk M() const { return m; }
+  __device__ __forceinline__ Blk F(int i) const {
+    if (L < (uint32_t)kLT) return full[L].F[i];
+    return aesT(bxor(ramp(i), m), T);
+  }
+  __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
+  __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
+  __device__ __forceinline__ Blk CS2b() const { return full[li()].CS2b; }
+  __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
+};
+
+template <int NT>
+struct Var5Cfg {
+  static constexpr int kTab = NT * 8192 * 4;
+  static constexpr int kFull = kTab;                                 // VConst[kLT]
+  static constexpr int kCnt = kFull + kLT * (int)sizeof(VConst);     // u32[320] counts -> bucket ends
+  static constexpr int kWpre = kCnt + 320 * 4;                       // u32[321] work prefix per bucket
+  static constexpr int kRecO = kWpre + 324 * 4;                      // u32[1024] offset in window
+  static constexpr int kRecL = kRecO + kBlock * 4;                   // u16[1024]
+  static constexpr int kRecI = kRecL + kBlock * 2;                   // u16[1024] sorted -> slot
+  static constexpr int kInv = kRecI + kBlock * 2;                    // u16[1024] slot -> sorted
+  static constexpr int kHout = kInv + kBlock * 2;                    // Blk[1024] hashes, sorted order
+  static constexpr int kStage = kHout + kBlock * 16;                 // staging buffer
+  static constexpr int S = ((163840 - kStage) / 1024) * 1024;
+  static constexpr int kBytes = kStage + S;
+  static_assert(kHout % 16 == 0 && kStage % 16 == 0, "alignment");
+  static_assert(S >= 32768 && kBytes <= 163840, "LDS budget");
+};
+
+// work estimate of a length bucket: table rounds + load/store overhead
+__device__ __forceinline__ uint32_t bucket_work(uint32_t b) {
+  return b >= 300 ? 0u : 2u * ((b + 15u) >> 4) + 11u;
+}
+
+__device__ uint64_t g_dbg[4096 * 8];  // diagnostic stamps (STAMP builds only)
+
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+template <int NT, bool STAMP = false>
+__global__ void __launch_bounds__(kBlock)
+k_var5(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+       uint64_t* __restrict__ out, uint32_t flags) {
+  using C = Var5Cfg<NT>;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[C::kBytes / 4];
+  VConst* kfull = (VConst*)((char*)lds + C::kFull);
+  uint32_t* cnt = (uint32_t*)((char*)lds + C::kCnt);
+  uint32_t* wpre = (uint32_t*)((char*)lds + C::kWpre);
+  uint32_t* rec_o = (uint32_t*)((char*)lds + C::kRecO);
+  uint16_t* rec_l = (uint16_t*)((char*)lds + C::kRecL);
+  uint16_t* rec_i = (uint16_t*)((char*)lds + C::kRecI);
+  uint16_t* inv = (uint16_t*)((char*)lds + C::kInv);
+  Blk* hout = (Blk*)((char*)lds + C::kHout);
+  uint8_t* stage = (uint8_t*)lds + C::kStage;
+  fill_tables<NT>(lds);
+  for (uint32_t b = threadIdx.x; b < 320; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) {
+    const MeowConst k = make_const(s1, s2, l, T);
+    VConst v;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { v.F[q] = k.F[q]; v.G[q] = k.G[q]; }
+    v.TG2 = k.TG2; v.CS2b = k.CS2b; v.TCS0a = k.TCS0a;
+    kfull[l] = v;
+  }
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  constexpr uint32_t NWV = kBlock / 64;
+  const uint64_t wstep = (uint64_t)gridDim.x * kBlock;
+  uint64_t base = (uint64_t)blockIdx.x * kBlock;
+  uint64_t po0 = 0, po1 = 0, pws = 0, pwe = 0;
+  if (base < n) {
+    const uint64_t wend = base + kBlock < n ? base + kBlock : n;
+    if (base + t < n) { po0 = offs[base + t]; po1 = offs[base + t + 1]; }
+    pws = offs[base]; pwe = offs[wend];
+  }
+  uint64_t acc[6] = {0, 0, 0, 0, 0, 0}, tp = 0;
+  auto mark = [&](int ph) {
+    if constexpr (STAMP) { const uint64_t x = stamp(); if (ph >= 0) acc[ph] += x - tp; tp = x; }
+  };
+  mark(-1);
+  for (; base < n; base += wstep) {
+    const uint64_t wend = base + kBlock < n ? base + kBlock : n;
+    const uint32_t nw = (uint32_t)(wend - base);
+    const uint64_t o0 = po0, o1 = po1, ws = pws, we = pwe;
+    const uint64_t astart = ws & ~(uint64_t)15;
+    const uint64_t span = we - astart;
+    const bool staged = span <= (uint64_t)C::S;
+    if (staged) {  // DMA the window bytes [astart, we) in 1 KiB pieces, wave-strided
+      const uint32_t np = (uint32_t)((span + 1023) >> 10);
+      for (uint32_t pc = wv; pc < np; pc += NWV) {
+        const uint64_t src = astart + (uint64_t)pc * 1024 + 16 * lane;
+        uint8_t* dst = stage + pc * 1024;
+        if (src + 16 <= we) {
+          __builtin_amdgcn_global_load_lds((const void*)(keys + src), (void __attribute__((address_space(3)))*)dst,
+                                           16, 0, 2 /* nt */);
+        } else if (src < we) {  // the piece holding the window's last byte: never read past it
+          const uint32_t* q = (const uint32_t*)(keys + src);
+          uint32_t* d = (uint32_t*)(dst + 16 * lane);
+          for (uint32_t j = 0; j < 4; j++)
+            if (src + 4 * j < we) d[j] = q[j];
+        }
+      }
+    }
+    mark(0);
+    const uint64_t L = o1 - o0;
+    const uint32_t bk = t < nw ? (L < 255 ? (uint32_t)L : 255u) : 300u;
+    atomicAdd(&cnt[bk], 1u);
+    __syncthreads();
+    if (t < 64) {  // bucket starts and work prefix, one wave, 5 buckets per lane
+      uint32_t v[5], sum = 0, wsum = 0;
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        v[k] = cnt[lane * 5 + k];
+        sum += v[k];
+        wsum += v[k] * bucket_work(lane * 5 + k);
+      }
+      uint32_t incl = sum, wincl = wsum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64), wy = __shfl_up(wincl, d, 64);
+        if (lane >= (uint32_t)d) { incl += y; wincl += wy; }
+      }
+      uint32_t run = incl - sum, wrun = wincl - wsum;
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        cnt[lane * 5 + k] = run;
+        wpre[lane * 5 + k] = wrun;
+        run += v[k];
+        wrun += v[k] * bucket_work(lane * 5 + k);
+      }
+      if (lane == 63) wpre[320] = wrun;
+    }
+    __syncthreads();
+    {
+      const uint32_t pos = atomicAdd(&cnt[bk], 1u);  // cnt[b] ends as the end of bucket b
+      rec_o[pos] = (uint32_t)(o0 - astart);
+      rec_l[pos] = (uint16_t)(L < 65535 ? L : 65535);
+      rec_i[pos] = (uint16_t)t;
+      inv[t] = (uint16_t)pos;
+    }
+    mark(1);
+    wait_vmcnt<0>();  // this wave's DMA pieces have landed ...
+    __syncthreads();  // ... and everyone's; records are complete
+    mark(2);
+    {  // prefetch the next window's offsets (lands while this window hashes)
+      const uint64_t nb = base + wstep;
+      if (nb < n) {
+        const uint64_t nwend = nb + kBlock < n ? nb + kBlock : n;
+        if (nb + t < n) { po0 = offs[nb + t]; po1 = offs[nb + t + 1]; }
+        pws = offs[nb]; pwe = offs[nwend];
+      }
+    }
+    // this wave's work-balanced range [lo, hi) of sorted positions
+    const uint32_t TW = wpre[320];
+    auto pos_of = [&](uint32_t x) -> uint32_t {  // first sorted position with work prefix >= x
+      if (x >= TW) return nw;
+      uint32_t lo = 0, hi = 319;                  // largest bucket b with wpre[b] <= x
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (wpre[mid] <= x) lo = mid; else hi = mid - 1;
+      }
+      const uint32_t b = lo, st = b ? cnt[b - 1] : 0u, en = cnt[b];
+      const uint32_t w = bucket_work(b);
+      uint32_t p = st + (w ? (x - wpre[b] + w - 1) / w : 0u);
+      return p < en ? p : en;
+    };
+    const uint32_t lo = pos_of((uint32_t)(((uint64_t)TW * wv) / NWV));
+    const uint32_t hi = wv + 1 == NWV ? nw : pos_of((uint32_t)(((uint64_t)TW * (wv + 1)) / NWV));
+    for (uint32_t p0 = lo; p0 < hi; p0 += 64) {
+      const uint32_t pos = p0 + lane;
+      if (pos < hi) {
+        const uint32_t ko = rec_o[pos], ki = rec_i[pos];
+        uint32_t kl = rec_l[pos];
+        Blk h;
+        if (staged) {
+          const LdsKV5<LdsTab<NT>> K(kfull, kl, s1, s2, T);
+          h = meow_rt<LdsTab<NT>, LdsKV5<LdsTab<NT>>, LdsLd>(stage + ko, kl, K, T);
+        } else {
+          const uint64_t g0 = offs[base + ki];
+          kl = (uint32_t)(offs[base + ki + 1] - g0);
+          const LdsKV5<LdsTab<NT>> K(kfull, kl, s1, s2, T);
+          h = meow_rt(keys + g0, kl, K, T);
+        }
+        if (fix) h = fixup(h);
+        hout[pos] = h;
+      }
+    }
+    mark(3);
+    __syncthreads();
+    mark(4);
+    if (t < nw) store_h<true>(out, base + t, hout[inv[t]], false);
+    for (uint32_t b = t; b < 320; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();  // staging areas reuse
+    mark(5);
+  }
+  if constexpr (STAMP) {
+    const uint32_t gw = blockIdx.x * (kBlock / 64) + wv;
+    if (lane == 0 && gw < 4096)
+      for (int q = 0; q < 6; q++) g_dbg[gw * 8 + q] = acc[q];
+  }
+}
+
 // straight-line restatement, one thread per key, per-key seeds
 __global__ void __launch_bounds__(256)
 k_seeded(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
@@ -577,6 +947,7 @@ int g_tune_kpl = 2;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8)
 int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
 int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
 int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
+int g_tune_var_mode = 0;  // ablation of k_var3: 1 no-hash, 2 no-gather, 3 no-sort
 int g_tune_var = 0;       // var-length kernel: 0 = unsorted k_generic, 2/4 = windowed sort (NT tables)
 
 int set_err(int e) { t_last_err = e; return e; }
@@ -842,6 +1213,34 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
     uint64_t s[16] = {seed1, seed2};
     return launch_generic(true, (const uint8_t*)keys, offsets, 0, n, s, 1, out, flags, (hipStream_t)stream,
                           cus);
+  }
+  if (g_tune_var == 6) {
+    const uint32_t grid = grid_for(n, cus, 1);
+    if (g_tune_var_mode == 1)
+      hipLaunchKernelGGL((k_var5<2, true>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
+                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+    else
+      hipLaunchKernelGGL((k_var5<2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
+                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+    return launch_done();
+  }
+  if (g_tune_var == 3 || g_tune_var == 5) {
+    const uint32_t grid = grid_for((n + 3) / 4, cus, 1);
+    if (g_tune_var_mode) {
+      switch (g_tune_var_mode) {
+        case 1: hipLaunchKernelGGL((k_var3<2, 4, 1>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
+        case 2: hipLaunchKernelGGL((k_var3<2, 4, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
+        default: hipLaunchKernelGGL((k_var3<2, 4, 3>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
+      }
+      return launch_done();
+    }
+    if (g_tune_var == 5)
+      hipLaunchKernelGGL((k_var3<2, 4>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
+                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+    else
+      hipLaunchKernelGGL((k_var3<2, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
+                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+    return launch_done();
   }
   const uint32_t grid = grid_for(n, cus, 1);
   if (g_tune_var == 4)
@@ -1152,6 +1551,13 @@ int kvh_hash_key_frags(const uint64_t seed[2], const kvh_key_frag_t* const* frag
   return seeded_host(ps.data(), ls.data(), n, seeds.data(), out, KVH_FIXUP);
 }
 
+// diagnostics: copy the per-wave phase stamps of the last STAMP launch
+int kvh_debug_stamps(uint64_t* host, size_t count) {
+  if (count > 4096 * 8) count = 4096 * 8;
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg), count * 8, 0, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? set_err(0) : hip_err(e);
+}
+
 int kvh_last_error(void) { return t_last_err; }
 
 const char* kvh_strerror(int err) {
@@ -1178,8 +1584,9 @@ int kvh_set_tuning(int knob, int value) {
     case 2: prev = g_tune_generic; g_tune_generic = value ? 1 : 0; return prev;
     case 3: if (value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_kpl; g_tune_kpl = value; return prev;
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
+    case 9: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_var_mode; g_tune_var_mode = value; return prev;
     case 8: prev = g_tune_ms_lanes; g_tune_ms_lanes = value ? 1 : 0; return prev;
-    case 7: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL;
+    case 7: if (value < 0 || value > 6 || value == 1) return KVH_EINVAL;
             prev = g_tune_var; g_tune_var = value; return prev;
     case 6: if (value != 0 && value != 2 && value != 3 && value != 4 && value != 6) return KVH_EINVAL;
             prev = g_tune_dma; g_tune_dma = value; return prev;

@@ -293,6 +293,36 @@ __device__ __forceinline__ Blk load16_full(const uint8_t* p) {
   return r;
 }
 
+// Key-byte sources for meow_rt: global memory (HBM/L2) or an LDS staging
+// buffer (dword reads only: misaligned LDS b128 reads replay at 64 cycles).
+struct GlobalLd {
+  static __device__ __forceinline__ Blk full(const uint8_t* p) { return load16_full(p); }
+  static __device__ __forceinline__ Blk part(const uint8_t* p, uint32_t n) { return load_bytes(p, n); }
+};
+struct LdsLd {
+  static __device__ __forceinline__ Blk full(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) d[j] = q[j];
+    Blk r;
+#pragma unroll
+    for (int c = 0; c < 4; c++) r.w[c] = __builtin_amdgcn_alignbyte(d[c + 1], d[c], sh);
+    return r;
+  }
+  static __device__ __forceinline__ Blk part(const uint8_t* p, uint32_t n) {
+    Blk r = full(p);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int keep = (int)n - 4 * c;
+      r.w[c] &= keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+    }
+    return r;
+  }
+};
+
 // Source of per-length constants for the runtime path.
 struct ConstRef {
   const MeowConst* k;
@@ -301,19 +331,19 @@ struct ConstRef {
 // Runtime-length Meow over key bytes at p (global memory).  Branches are
 // wave-uniform when every lane has the same length (generic fixed-length
 // kernel) and lane-divergent (masked) for variable-length batches.
-template <class Tab, class KGet>
+template <class Tab, class KGet, class Ld = GlobalLd>
 __device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet& K, const Tab& T) {
   const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
   Blk S0, S1, S2, S3;
   if (nb > 0) {
-    Blk k0 = load16_full(p), k1 = load16_full(p + 16), k2 = load16_full(p + 32),
-        k3 = load16_full(p + 48);
+    Blk k0 = Ld::full(p), k1 = Ld::full(p + 16), k2 = Ld::full(p + 32),
+        k3 = Ld::full(p + 48);
     S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
     S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
     for (uint32_t b = 1; b < nb; b++) {
       const uint8_t* q = p + 64 * b;
-      k0 = load16_full(q); k1 = load16_full(q + 16);
-      k2 = load16_full(q + 32); k3 = load16_full(q + 48);
+      k0 = Ld::full(q); k1 = Ld::full(q + 16);
+      k2 = Ld::full(q + 32); k3 = Ld::full(q + 48);
       S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
       S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
     }
@@ -322,19 +352,19 @@ __device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet&
   const uint8_t* q = p + 64 * nb;
   // trail (key_hash.c:1200-1210); a state's first absorb is folded
   if (t) {
-    const Blk k = load_bytes(q + C, t);
+    const Blk k = Ld::part(q + C, t);
     S3 = first ? aesdec(bxor(K.F(3), k), k, T) : aesdec(aesdec(S3, k, T), k, T);
   }
   if (C >= 48) {
-    const Blk k = load16_full(q + 32);
+    const Blk k = Ld::full(q + 32);
     S2 = first ? aesdec(bxor(K.F(2), k), k, T) : aesdec(aesdec(S2, k, T), k, T);
   }
   if (C >= 32) {
-    const Blk k = load16_full(q + 16);
+    const Blk k = Ld::full(q + 16);
     S1 = first ? aesdec(bxor(K.F(1), k), k, T) : aesdec(aesdec(S1, k, T), k, T);
   }
   if (C >= 16) {
-    const Blk k = load16_full(q);
+    const Blk k = Ld::full(q);
     S0 = first ? aesdec(bxor(K.F(0), k), k, T) : aesdec(aesdec(S0, k, T), k, T);
   }
   const bool T0 = !first || C >= 16, T1 = !first || C >= 32, T2 = !first || C >= 48,
@@ -385,6 +415,71 @@ __device__ __forceinline__ Blk meow_var(const uint8_t* p, uint32_t L, const KGet
     }
   }
   const bool first = nb == 0;
+  if (t) S3 = first ? aesdec(bxor(K.F(3), r3), r3, T) : aesdec(aesdec(S3, r3, T), r3, T);
+  if (C >= 48) S2 = first ? aesdec(bxor(K.F(2), r2), r2, T) : aesdec(aesdec(S2, r2, T), r2, T);
+  if (C >= 32) S1 = first ? aesdec(bxor(K.F(1), r1), r1, T) : aesdec(aesdec(S1, r1, T), r1, T);
+  if (C >= 16) S0 = first ? aesdec(bxor(K.F(0), r0), r0, T) : aesdec(aesdec(S0, r0, T), r0, T);
+  const bool T0 = !first || C >= 16, T1 = !first || C >= 32, T2 = !first || C >= 48, T3 = !first || t != 0;
+  const Blk M = K.M();
+  S3 = T3 ? aesdec(S3, M, T) : K.G(3);
+  S2 = T2 ? aesdec(S2, M, T) : K.G(2);
+  S1 = T1 ? aesdec(S1, M, T) : K.G(1);
+  S0 = T0 ? aesdec(S0, M, T) : K.G(0);
+  Blk S2b;
+  if (T2) S2b = aesdec(aesdec(S2, S3, T), M, T);
+  else if (T3) S2b = aesdec(bxor(K.TG2(), S3), M, T);
+  else S2b = K.CS2b();
+  Blk S0b;
+  if (T0) S0b = aesdec(aesdec(S0, S1, T), S2b, T);
+  else S0b = bxor(K.TCS0a(), S2b);
+  return aesdec(S0b, M, T);
+}
+
+// First four 16-byte pieces a key consumes: block 0 for L >= 64, else the
+// trail (full chunks at p, p+16, p+32 as present, partial tail at p+C).
+// Issued one key ahead by k_var so the gather latency overlaps the rounds of
+// the previous key.
+__device__ __forceinline__ void prefetch_first(const uint8_t* p, uint32_t L, Blk (&pre)[4]) {
+  const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
+  const Blk z = bzero();
+  pre[0] = (nb || C >= 16) ? load16_full(p) : z;
+  pre[1] = (nb || C >= 32) ? load16_full(p + 16) : z;
+  pre[2] = (nb || C >= 48) ? load16_full(p + 32) : z;
+  pre[3] = nb ? load16_full(p + 48) : (t ? load_bytes(p + C, t) : z);
+}
+
+// meow_var with the first four pieces supplied by prefetch_first; later
+// blocks are fetched one block ahead and the trail of a long key together
+// with its block 1.
+template <class Tab, class KGet>
+__device__ __forceinline__ Blk meow_var_pre(const uint8_t* p, uint32_t L, const Blk (&pre)[4], const KGet& K,
+                                            const Tab& T) {
+  const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
+  const bool first = nb == 0;
+  Blk S0, S1, S2, S3, r0, r1, r2, r3;
+  if (first) {
+    r0 = pre[0]; r1 = pre[1]; r2 = pre[2]; r3 = pre[3];
+  } else {
+    const uint8_t* q = p + 64 * (uint64_t)nb;
+    const Blk z = bzero();
+    Blk n0 = z, n1 = z, n2 = z, n3 = z;
+    if (nb > 1) { n0 = load16_full(p + 64); n1 = load16_full(p + 80); n2 = load16_full(p + 96); n3 = load16_full(p + 112); }
+    r3 = t ? load_bytes(q + C, t) : z;
+    r2 = C >= 48 ? load16_full(q + 32) : z;
+    r1 = C >= 32 ? load16_full(q + 16) : z;
+    r0 = C >= 16 ? load16_full(q) : z;
+    S0 = aesdec(bxor(K.F(0), pre[0]), pre[0], T); S1 = aesdec(bxor(K.F(1), pre[1]), pre[1], T);
+    S2 = aesdec(bxor(K.F(2), pre[2]), pre[2], T); S3 = aesdec(bxor(K.F(3), pre[3]), pre[3], T);
+    for (uint32_t b = 1; b < nb; b++) {
+      const Blk k0 = n0, k1 = n1, k2 = n2, k3 = n3;
+      if (b + 1 < nb) {
+        const uint8_t* r = p + 64 * (uint64_t)(b + 1);
+        n0 = load16_full(r); n1 = load16_full(r + 16); n2 = load16_full(r + 32); n3 = load16_full(r + 48);
+      }
+      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+    }
+  }
   if (t) S3 = first ? aesdec(bxor(K.F(3), r3), r3, T) : aesdec(aesdec(S3, r3, T), r3, T);
   if (C >= 48) S2 = first ? aesdec(bxor(K.F(2), r2), r2, T) : aesdec(aesdec(S2, r2, T), r2, T);
   if (C >= 32) S1 = first ? aesdec(bxor(K.F(1), r1), r1, T) : aesdec(aesdec(S1, r1, T), r1, T);

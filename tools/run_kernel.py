@@ -17,11 +17,14 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--n", type=int, default=0)
 ap.add_argument("--nt", type=int, default=0)
 ap.add_argument("--kpl", type=int, default=0)
+ap.add_argument("--var", type=int, default=-1)
 a = ap.parse_args()
 if a.nt:
     kvh.lib.kvh_set_tuning(0, a.nt)
 if a.kpl:
     kvh.lib.kvh_set_tuning(3, a.kpl)
+if a.var >= 0:
+    kvh.lib.kvh_set_tuning(7, a.var)
 torch.cuda.set_device(0)
 g = torch.Generator(device="cuda")
 g.manual_seed(1)

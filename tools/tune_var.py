@@ -9,7 +9,7 @@ from raikv_amd.workload import zipf_lengths, offsets_from_lengths  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=100_000_000)
-ap.add_argument("--variants", default="0,2,4")
+ap.add_argument("--variants", default="0,5,6")
 ap.add_argument("--rounds", type=int, default=3)
 a = ap.parse_args()
 torch.cuda.set_device(0)
