@@ -6,15 +6,21 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-pass-failed
 INC      := -Iinclude
 
 LIB      := raikv_amd/libkvh.so
-SRCS     := raikv_amd/csrc/kvh.hip
-HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp include/kvh.h include/raikv_amd/key_hash.hpp
+SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/ht_pos.hip
+OBJS     := $(SRCS:.hip=.o)
+HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/csrc/kvh_internal.hpp \
+            raikv_amd/csrc/ht_pos.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
 CPP_TESTS := tests/cpp/hash_test_gpu
 
 all: $(LIB) oracle cpptests
 
-$(LIB): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) $(INC) -shared -o $@ $(SRCS)
+# one object per translation unit so `make -j` compiles them in parallel
+raikv_amd/csrc/%.o: raikv_amd/csrc/%.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(INC) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
 
 oracle:
 	$(MAKE) -C oracle
@@ -27,7 +33,7 @@ tests/cpp/hash_test_gpu: tests/cpp/hash_test_gpu.cpp $(LIB) include/raikv_amd/ke
 	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
 
 clean:
-	rm -f $(LIB) $(CPP_TESTS)
+	rm -f $(LIB) $(OBJS) $(CPP_TESTS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle cpptests clean

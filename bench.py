@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "128-bit key hashes/sec device-resident, 16–64B keys; GB/s vs HBM peak"
+METRIC_F1 = "keys/sec -> hash + cuckoo table positions, device-resident (SURVEY.md §8 f1)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 
 CONFIGS = {
@@ -44,7 +45,15 @@ CONFIGS = {
                n=50_000_000, key_len=32, arity=4, var=False),
     "c4": dict(workload="C4: 32-byte keys, 125M per GPU (1B over 8 GPUs), sharded by index range",
                n=125_000_000, key_len=32, arity=1, var=False),
+    # SURVEY.md §8 f1 (next row): the consumer side of the hash
+    "f1": dict(workload="F1: 100M fixed 16-byte keys -> Meow128 + fixup + cuckoo arity-4 table positions "
+                        "(64 GiB map, 4 buckets), hashes and u64 positions stored; one fused kernel",
+               n=100_000_000, key_len=16, arity=1, var=False, positions="fused"),
+    "f1p": dict(workload="F1p: 100M resident fixed-up (h1,h2) -> cuckoo arity-4 table positions "
+                         "(64 GiB map, 4 buckets), u64 positions",
+                n=100_000_000, key_len=16, arity=1, var=False, positions="only"),
 }
+F1_GEOM = dict(map_size=64 << 30, hash_entry_size=64, hash_value_ratio=1.0, cuckoo_buckets=4, cuckoo_arity=4)
 
 
 def log(*a):
@@ -88,6 +97,49 @@ def cpu_baseline(cfg, seed, seconds: float):
     return {"value": total_n / total_t, "unit": "hash/s", "cores": threads, "kind": kind,
             "sample": f"{total_n} packed {L}-byte keys ({n} distinct, {total_n // n} passes) x "
                       f"kv_hash_meow128 (src/key_hash.c), {threads} threads on {model}, {total_t:.1f} s"}
+
+
+def cpu_baseline_positions(cfg, seed, seconds: float, geom):
+    """Reference per-key path for the f1 configs: kv_hash_meow128 + fixup +
+    KeyCtx::set_hash + CuckooAltHash::calc_hash (oracle/ref_cuckoo.cpp,
+    compiled from the reference's ht_init/ht_cuckoo/key_ctx sources) on host
+    threads; f1p times calc_hash alone on precomputed hashes."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_ref_ht, load_oracle, orc_geom, orc_positions  # checker only
+    import ctypes as C
+    threads = max(1, min(16, os.cpu_count() or 1))
+    L, n = cfg["key_len"], 4_000_000
+    rng = np.random.default_rng(42)
+    keys = rng.integers(0, 256, n * L, dtype=np.uint8)
+    hashes = np.zeros(2 * n, dtype=np.uint64)
+    pos = np.zeros(n * geom.per_key, dtype=np.uint64)
+    only = cfg["positions"] == "only"
+    if only:
+        hashes[:] = rng.integers(0, 2 ** 63, 2 * n, dtype=np.uint64)
+    ref = load_ref_ht()
+    if ref is not None:
+        kind = "reference"
+        run = lambda: ref.ref_cuckoo_bench(geom.ht_size, geom.ht_mod_mask, geom.ht_mod_fraction, geom.ht_mod_shift,
+                                           geom.cuckoo_buckets, geom.cuckoo_arity,
+                                           None if only else keys.ctypes.data, L, n, C.c_uint64(seed[0]),
+                                           C.c_uint64(seed[1]), hashes.ctypes.data, pos.ctypes.data, threads)
+    else:  # clean-room port, positions only, single thread
+        kind, threads, only = "port", 1, True
+        orc = load_oracle()
+        og = orc_geom(orc, F1_GEOM["map_size"], 64, 1.0, F1_GEOM["cuckoo_buckets"], F1_GEOM["cuckoo_arity"])
+
+        def run():
+            t = time.perf_counter()
+            orc_positions(orc, og, hashes.reshape(-1, 2))
+            return time.perf_counter() - t
+    total_t, total_n = 0.0, 0
+    while total_t < seconds:
+        total_t += float(run())
+        total_n += n
+    what = "calc_hash on resident hashes" if only else f"kv_hash_meow128({L} B) + fixup + set_hash + calc_hash"
+    return {"value": total_n / total_t, "unit": "key/s", "cores": threads, "kind": kind,
+            "sample": f"{total_n} keys ({n} distinct) x {what}, arity {geom.cuckoo_arity}, "
+                      f"{threads} threads, {total_t:.1f} s"}
 
 
 def load_traffic(config_name: str):
@@ -144,6 +196,19 @@ def main():
         del lens
         alg_bytes = key_bytes + 8 * (n + 1) + 16 * n
         run = lambda out: kvh.meow128_var(keys, offs, seed, out=out)
+    elif cfg.get("positions"):
+        geom = kvh.HtGeom.from_map(**F1_GEOM)
+        pk = geom.per_key
+        keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=gen)
+        hashes = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+        pos = torch.empty((n, pk), dtype=torch.int64, device="cuda")
+        if cfg["positions"] == "fused":
+            alg_bytes = n * L + 16 * n + 8 * pk * n
+            run = lambda out: kvh.meow128_fixed_positions(keys, L, seed, geom, hashes=hashes, out=pos)
+        else:
+            kvh.meow128_fixed(keys, L, seed, out=hashes, fixup=True)
+            alg_bytes = 16 * n + 8 * pk * n
+            run = lambda out: kvh.ht_positions(hashes, geom, out=pos)
     else:
         key_bytes = n * L
         keys = torch.randint(0, 256, (key_bytes,), dtype=torch.uint8, device="cuda", generator=gen)
@@ -152,7 +217,8 @@ def main():
             run = lambda out: kvh.meow128_fixed(keys, L, seed, out=out)
         else:
             run = lambda out: kvh.meow128_multiseed(keys, L, list(C3_SEEDS[:arity]), out=out)
-    out = torch.empty((n, arity, 2) if arity > 1 else (n, 2), dtype=torch.int64, device="cuda")
+    out = None if cfg.get("positions") else \
+        torch.empty((n, arity, 2) if arity > 1 else (n, 2), dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -174,14 +240,14 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     wall = kdist.reduce_max(wall, world)
 
-    hashes = n * arity * args.steps * world
-    value = hashes / wall
+    n_hash = n * arity * args.steps * world  # keys for the f1 configs
+    value = n_hash / wall
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic, tsrc = load_traffic(args.config)
     res = {
-        "metric": METRIC,
+        "metric": METRIC_F1 if cfg.get("positions") else METRIC,
         "value": value,
-        "unit": "hash/s",
+        "unit": "key/s" if cfg.get("positions") else "hash/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -206,7 +272,10 @@ def main():
         res["e2e_pcie"] = e2e(kvh, cfg, seed)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            res["cpu_baseline"] = cpu_baseline(cfg, seed, args.cpu_seconds)
+            if cfg.get("positions"):
+                res["cpu_baseline"] = cpu_baseline_positions(cfg, seed, args.cpu_seconds, geom)
+            else:
+                res["cpu_baseline"] = cpu_baseline(cfg, seed, args.cpu_seconds)
         except Exception as e:  # report, never hide
             res["cpu_baseline"] = {"value": None, "error": repr(e)}
     kdist.finalize(world)

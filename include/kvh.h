@@ -178,6 +178,62 @@ int kvh_hash_key_frags(const uint64_t seed[2], const kvh_key_frag_t *const *frag
                        size_t n, uint64_t *out);
 
 /* ---------------------------------------------------------------------
+ * Table positions: what KeyCtx probes for a key hash.
+ *   home slot  FileHdr::ht_mod, include/raikv/shm_ht.h:181-184
+ *   cuckoo     CuckooAltHash::calc_hash, src/ht_cuckoo.cpp:38-79
+ *              (called with start = ht_mod(h1), ht_cuckoo.cpp:374-398,
+ *              key_ctx.cpp:89-94)
+ * kvh_ht_geom_t carries the FileHdr fields those read (shm_ht.h:143-157);
+ * a maintainer fills it from ht->hdr directly or via kvh_ht_geom_init.
+ * Positions per key: cuckoo_arity when cuckoo_buckets > 1 and arity > 1
+ * (pos[0] = home slot, pos[k] = CuckooAltHash::pos[k]), else 1 (the
+ * linear-probe start slot, key_ctx.cpp:130).  Output layout
+ * pos[i * per_key + k], u64 (u32 with KVH_POS32).  hashes are (h1,h2)
+ * pairs already fixed up as KeyFragment::hash leaves them.
+ * ------------------------------------------------------------------- */
+#define KVH_POS32     0x2u  /* store positions as u32 (ht_size <= 2^32) */
+
+typedef struct {
+  uint64_t ht_size;         /* FileHdr::ht_size          shm_ht.h:143 */
+  uint64_t ht_mod_mask;     /* FileHdr::ht_mod_mask      shm_ht.h:146 */
+  uint64_t ht_mod_fraction; /* FileHdr::ht_mod_fraction  shm_ht.h:147 */
+  uint32_t ht_mod_shift;    /* FileHdr::ht_mod_shift     shm_ht.h:156 */
+  uint16_t cuckoo_buckets;  /* FileHdr::cuckoo_buckets   shm_ht.h:153 */
+  uint8_t  cuckoo_arity;    /* FileHdr::cuckoo_arity     shm_ht.h:157 */
+  uint8_t  pad;
+} kvh_ht_geom_t;
+
+/* HashTab::initialize's geometry (src/ht_init.cpp:117-156) for a map of
+ * map_size bytes: same ht_size / mask / fraction / shift as the reference
+ * (kv_geom_t fields, shm_ht.h:14-21).  Host only. */
+int kvh_ht_geom_init(uint64_t map_size, uint32_t hash_entry_size,
+                     float hash_value_ratio, uint16_t cuckoo_buckets,
+                     uint8_t cuckoo_arity, kvh_ht_geom_t *geom);
+/* positions stored per key for this geometry (0 for NULL) */
+uint32_t kvh_positions_per_key(const kvh_ht_geom_t *geom);
+
+/* n device-resident hash pairs (16-byte aligned) -> positions (16-byte
+ * aligned device buffer).  Replaces, per key, ht_mod(key) and
+ * CuckooAltHash::calc_hash(kctx, key, key2, ht_mod(key)).  KVH_EINVAL for a
+ * geometry whose ht_mod leaves ht[] or whose table is too small to place
+ * per_key non-clashing slots; a slot the rejection loop could not place
+ * within 2^20 steps (unreachable for an accepted geometry) is ~0. */
+int kvh_ht_positions(const uint64_t *hashes, size_t n,
+                     const kvh_ht_geom_t *geom, void *pos, uint32_t flags,
+                     void *stream);
+
+/* Fused: n fixed-length keys -> kv_hash_meow128 with (seed1, seed2) ->
+ * KeyFragment fixup -> positions, one pass (KeyCtx::set_key_hash then the
+ * probe positions, key_ctx.cpp:97-105).  `hashes` (2n u64, may be NULL)
+ * receives the fixed-up hashes.  One kernel for key_len 16/32 with 16-byte
+ * aligned keys and 1/2/4/8 positions per key; other shapes run the hash
+ * kernel then kvh_ht_positions. */
+int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
+                                uint64_t seed1, uint64_t seed2,
+                                const kvh_ht_geom_t *geom, uint64_t *hashes,
+                                void *pos, uint32_t flags, void *stream);
+
+/* ---------------------------------------------------------------------
  * Runtime / diagnostics
  * ------------------------------------------------------------------- */
 int         kvh_last_error(void);

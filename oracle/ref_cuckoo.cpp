@@ -1,0 +1,135 @@
+/*
+ * oracle/ref_cuckoo.cpp -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Driver compiled together with the unmodified reference KV-core sources
+ * (oracle/Makefile) into oracle/_ref/libkvref_ht.so.  It builds a malloc()
+ * HashTab (HashTab::alloc_map, src/ht_init.cpp:252-261) of the requested
+ * geometry and asks the reference's CuckooAltHash::calc_hash
+ * (src/ht_cuckoo.cpp:38-79) for the arity table positions of given
+ * (h1, h2) pairs, exactly as KeyCtx::acquire_cuckoo does
+ * (src/ht_cuckoo.cpp:374-398) after KeyCtx::set_hash (src/key_ctx.cpp:89-94:
+ * start = ht_mod(h1)).  A linear table (cuckoo_buckets <= 1 selects
+ * acquire_linear_probe, src/key_ctx.cpp:130) has only the start slot; so
+ * does arity <= 1.  Used only to produce golden vectors; no reference
+ * source is copied here.
+ */
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+#include <new>
+#include <raikv/shm_ht.h>
+#include <raikv/key_ctx.h>
+#include <raikv/ht_cuckoo.h>
+
+using namespace rai::kv;
+
+extern "C" int ref_cuckoo_positions(uint64_t map_size, uint32_t entry_size, float ratio, uint16_t buckets,
+                                    uint8_t arity, const uint64_t *h, size_t n, uint64_t *pos,
+                                    uint64_t *geom_out) {
+  HashTabGeom g;
+  memset(&g, 0, sizeof(g));
+  g.map_size = map_size;
+  g.max_value_size = 0;
+  g.hash_entry_size = entry_size;
+  g.hash_value_ratio = ratio;
+  g.cuckoo_buckets = buckets;
+  g.cuckoo_arity = arity;
+  HashTab *ht = HashTab::alloc_map(g);
+  if (ht == NULL) return -1;
+  {
+    KeyCtx kctx(*ht, 0);
+    alignas(64) char buf[sizeof(CuckooAltHash) + 3 * 8 * 256];
+    CuckooAltHash *c = new (buf) CuckooAltHash(arity);
+    const bool cuckoo = buckets > 1 && arity > 1;
+    for (size_t i = 0; i < n; i++) {
+      kctx.set_hash(h[2 * i], h[2 * i + 1]);
+      if (!cuckoo) {
+        pos[i] = kctx.start;
+        continue;
+      }
+      c->calc_hash(kctx, kctx.key, kctx.key2, kctx.start);
+      for (uint8_t a = 0; a < arity; a++) pos[i * arity + a] = c->pos[a];
+    }
+  }
+  geom_out[0] = ht->hdr.ht_mod_mask;
+  geom_out[1] = ht->hdr.ht_mod_fraction;
+  geom_out[2] = ht->hdr.ht_mod_shift;
+  geom_out[3] = ht->hdr.ht_size;
+  ::free(ht);
+  return 0;
+}
+
+/* CPU baseline for bench.py's f1/f1p configs: the reference's per-key path
+ * (kv_hash_meow128 + KeyFragment fixup as in KeyCtx::set_key_hash,
+ * key_ctx.cpp:97-105, then CuckooAltHash::calc_hash) on `threads` pthreads.
+ * The table geometry is written into a header-only HashTab (hdr + ctx +
+ * stats regions, zeroed): calc_hash and KeyCtx read only header fields, so
+ * a 64 GiB map's geometry needs no 64 GiB allocation.  keys == NULL times
+ * calc_hash alone on the given hashes (f1p).  Returns elapsed seconds. */
+#include <pthread.h>
+#include <time.h>
+extern "C" void kv_hash_meow128(const void *p, size_t sz, uint64_t *h1, uint64_t *h2);
+
+namespace {
+struct BenchArg {
+  HashTab *ht;
+  const uint8_t *keys;
+  size_t len, lo, hi;
+  uint64_t s1, s2;
+  uint64_t *hashes, *pos;
+};
+
+void *bench_thr(void *vp) {
+  BenchArg *a = (BenchArg *) vp;
+  KeyCtx kctx(*a->ht, 0);
+  const uint8_t ar = a->ht->hdr.cuckoo_arity;
+  alignas(64) char buf[sizeof(CuckooAltHash) + 3 * 8 * 256];
+  CuckooAltHash *c = new (buf) CuckooAltHash(ar);
+  for (size_t i = a->lo; i < a->hi; i++) {
+    uint64_t k, k2;
+    if (a->keys != NULL) {
+      k = a->s1; k2 = a->s2;
+      kv_hash_meow128(a->keys + i * a->len, a->len, &k, &k2);
+      k &= ~((uint64_t) 1 << 63);
+      if (k <= 1) k = 2;
+      a->hashes[2 * i] = k; a->hashes[2 * i + 1] = k2;
+    } else {
+      k = a->hashes[2 * i]; k2 = a->hashes[2 * i + 1];
+    }
+    kctx.set_hash(k, k2);
+    c->calc_hash(kctx, kctx.key, kctx.key2, kctx.start);
+    for (uint8_t j = 0; j < ar; j++) a->pos[i * ar + j] = c->pos[j];
+  }
+  return NULL;
+}
+}  // namespace
+
+extern "C" double ref_cuckoo_bench(uint64_t ht_size, uint64_t mask, uint64_t frac, uint32_t shift,
+                                   uint16_t buckets, uint8_t arity, const uint8_t *keys, size_t len, size_t n,
+                                   uint64_t s1, uint64_t s2, uint64_t *hashes, uint64_t *pos, int threads) {
+  const size_t hdr_bytes = KV_HT_HDR_SIZE + KV_HT_CTX_SIZE + KV_HT_STATS_SIZE;
+  HashTab *ht = (HashTab *) ::aligned_alloc(4096, hdr_bytes);
+  if (ht == NULL || arity < 2 || buckets < 2) return -1.0;
+  ::memset((void *) ht, 0, hdr_bytes);
+  ht->hdr.ht_size = ht_size;
+  ht->hdr.ht_mod_mask = mask;
+  ht->hdr.ht_mod_fraction = frac;
+  ht->hdr.ht_mod_shift = (uint8_t) shift;
+  ht->hdr.cuckoo_buckets = buckets;
+  ht->hdr.cuckoo_arity = arity;
+  ht->hdr.hash_entry_size = 64;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  BenchArg args[256];
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; t++) {
+    args[t] = BenchArg{ht, keys, len, n * t / threads, n * (t + 1) / threads, s1, s2, hashes, pos};
+    pthread_create(&tid[t], NULL, bench_thr, &args[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  ::free(ht);
+  return (double) (t1.tv_sec - t0.tv_sec) + 1e-9 * (double) (t1.tv_nsec - t0.tv_nsec);
+}

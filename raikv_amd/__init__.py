@@ -9,6 +9,10 @@ from __future__ import annotations
 
 from .binding import (  # noqa: F401
     KVH_FIXUP,
+    KVH_POS32,
+    HtGeom,
+    ht_positions,
+    meow128_fixed_positions,
     KvhError,
     lib,
     lib_path,
@@ -27,5 +31,6 @@ from .workload import STATIC_SEED  # noqa: F401
 __all__ = [
     "KVH_FIXUP", "KvhError", "lib", "lib_path", "meow128_fixed", "meow128_var",
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "kv_hash_meow128",
-    "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED",
+    "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
+    "meow128_fixed_positions",
 ]

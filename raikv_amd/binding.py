@@ -19,6 +19,7 @@ except Exception:  # pragma: no cover - torch is part of the image
     torch = None
 
 KVH_FIXUP = 0x1
+KVH_POS32 = 0x2
 KVH_MAX_ARITY = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +34,32 @@ I = C.c_int
 
 class KvhError(RuntimeError):
     pass
+
+
+class HtGeom(C.Structure):
+    """kvh_ht_geom_t: the FileHdr fields ht_mod / calc_hash read
+    (include/raikv/shm_ht.h:143-157)."""
+    _fields_ = [("ht_size", C.c_uint64), ("ht_mod_mask", C.c_uint64), ("ht_mod_fraction", C.c_uint64),
+                ("ht_mod_shift", C.c_uint32), ("cuckoo_buckets", C.c_uint16), ("cuckoo_arity", C.c_uint8),
+                ("pad", C.c_uint8)]
+
+    @classmethod
+    def from_map(cls, map_size: int, hash_entry_size: int = 64, hash_value_ratio: float = 1.0,
+                 cuckoo_buckets: int = 4, cuckoo_arity: int = 2) -> "HtGeom":
+        """HashTab::initialize's geometry (ht_init.cpp:117-156); default
+        cuckoo shape "2+4" as the reference server (arity 2, 4 buckets)."""
+        g = cls()
+        check(lib.kvh_ht_geom_init(map_size, hash_entry_size, hash_value_ratio, cuckoo_buckets, cuckoo_arity,
+                                   C.byref(g)), "kvh_ht_geom_init")
+        return g
+
+    @property
+    def per_key(self) -> int:
+        return int(lib.kvh_positions_per_key(C.byref(self)))
+
+    def ht_mod(self, k: int) -> int:
+        """FileHdr::ht_mod (shm_ht.h:181-184), host side."""
+        return (((k & self.ht_mod_mask) * self.ht_mod_fraction) & (2**64 - 1)) >> self.ht_mod_shift
 
 
 def _load():
@@ -65,6 +92,10 @@ def _load():
         "kvh_meow_test": (I, [P, SZ, C.POINTER(U64), C.POINTER(U64)]),
         "kvh_hash_key_frag": (I, [P, P, C.POINTER(U64), C.POINTER(U64)]),
         "kvh_hash_key_frags": (I, [P, P, SZ, P]),
+        "kvh_ht_geom_init": (I, [U64, U32, C.c_float, C.c_uint16, C.c_uint8, P]),
+        "kvh_positions_per_key": (U32, [P]),
+        "kvh_ht_positions": (I, [P, SZ, P, P, U32, P]),
+        "kvh_meow128_fixed_positions": (I, [P, U32, SZ, U64, U64, P, P, P, U32, P]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
         "kvh_version": (C.c_char_p, []),
@@ -120,6 +151,37 @@ def meow128_fixed(keys, key_len: int, seed: Tuple[int, int], out=None, fixup: bo
                                 _dev_ptr(out) if n else None, KVH_FIXUP if fixup else 0,
                                 _stream_ptr(stream)), "kvh_meow128_fixed")
     return out
+
+
+def ht_positions(hashes, geom: "HtGeom", out=None, pos32: bool = False, stream=None):
+    """hashes: int64 device tensor [n, 2] of fixed-up (h1, h2) -> table
+    positions [n, geom.per_key] (int64, or int32 bit patterns with pos32):
+    ht_mod(h1) and CuckooAltHash::calc_hash (ht_cuckoo.cpp:38-79)."""
+    n = hashes.numel() // 2
+    a = geom.per_key
+    if out is None:
+        out = torch.empty((n, a), dtype=torch.int32 if pos32 else torch.int64, device=hashes.device)
+    check(lib.kvh_ht_positions(_dev_ptr(hashes) if n else None, n, C.byref(geom), _dev_ptr(out) if n else None,
+                               KVH_POS32 if pos32 else 0, _stream_ptr(stream)), "kvh_ht_positions")
+    return out
+
+
+def meow128_fixed_positions(keys, key_len: int, seed: Tuple[int, int], geom: "HtGeom", hashes=None,
+                            keep_hashes: bool = True, out=None, pos32: bool = False, stream=None):
+    """Fused fixed-length hash -> fixup -> table positions.  Returns
+    (hashes [n, 2] or None, positions [n, geom.per_key])."""
+    n = keys.numel() // key_len if key_len else 0
+    a = geom.per_key
+    if hashes is None and keep_hashes:
+        hashes = _new_out((n, 2), keys)
+    if out is None:
+        out = torch.empty((n, a), dtype=torch.int32 if pos32 else torch.int64, device=keys.device)
+    check(lib.kvh_meow128_fixed_positions(_dev_ptr(keys) if n else None, key_len, n, U64(seed[0] & (2**64 - 1)),
+                                          U64(seed[1] & (2**64 - 1)), C.byref(geom),
+                                          _dev_ptr(hashes) if (hashes is not None and n) else None,
+                                          _dev_ptr(out) if n else None, KVH_POS32 if pos32 else 0,
+                                          _stream_ptr(stream)), "kvh_meow128_fixed_positions")
+    return hashes, out
 
 
 def meow128_var(keys, offsets, seed: Tuple[int, int], out=None, fixup: bool = False, stream=None):

@@ -18,9 +18,11 @@
 #include <vector>
 #include <algorithm>
 #include "meow_dev.hpp"
+#include "kvh_internal.hpp"
 #include "../../include/kvh.h"
 
 using namespace kvh;
+using namespace kvh::rt;
 
 #ifndef KVH_VERSION
 #define KVH_VERSION "raikv_amd-kvh 0.1 (gfx950)"
@@ -31,44 +33,6 @@ namespace {
 constexpr int kBlock = 1024;          // threads per workgroup (16 waves)
 constexpr int kLT = 64;               // full per-length constant records (L < 64)
 constexpr int kNF = 256;              // F-only records for 64 <= L < 64 + kNF
-
-// ------------------------------------------------------------ helpers
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-
-// Key i of a fixed-length batch as NC 16-byte chunks (zero padded past L).
-// NTM: non-temporal (streamed-once) loads.
-template <int L, bool A16, bool NTM = false>
-__device__ __forceinline__ void load_fixed(const uint8_t* __restrict__ p, Blk* D) {
-  constexpr int NC = Plan<L>::NC;
-  if constexpr (A16 && (L % 16) == 0) {
-#pragma unroll
-    for (int j = 0; j < NC; j++) {
-      const v4u* q = (const v4u*)(p + 16 * j);
-      const v4u v = NTM ? __builtin_nontemporal_load(q) : *q;
-      D[j].w[0] = v.x; D[j].w[1] = v.y; D[j].w[2] = v.z; D[j].w[3] = v.w;
-    }
-  } else {
-    // L % 8 == 0 and 8-byte aligned rows
-#pragma unroll
-    for (int j = 0; j < L / 8; j++) {
-      const v2u* q = (const v2u*)(p + 8 * j);
-      const v2u v = NTM ? __builtin_nontemporal_load(q) : *q;
-      D[j / 2].w[(j & 1) * 2 + 0] = v.x;
-      D[j / 2].w[(j & 1) * 2 + 1] = v.y;
-    }
-    if constexpr ((L % 16) == 8) { D[NC - 1].w[2] = 0; D[NC - 1].w[3] = 0; }
-  }
-}
-
-template <bool NTM = false>
-__device__ __forceinline__ void store_h(uint64_t* __restrict__ out, uint64_t idx, Blk h, bool fix) {
-  if (fix) h = fixup(h);
-  v4u v;
-  v.x = h.w[0]; v.y = h.w[1]; v.z = h.w[2]; v.w = h.w[3];
-  v4u* q = (v4u*)(out + 2 * idx);
-  if constexpr (NTM) __builtin_nontemporal_store(v, q); else *q = v;
-}
 
 // ------------------------------------------------------------ kernels
 // Wave-chunked streaming: wave w owns chunks of 64*U consecutive keys
@@ -932,7 +896,12 @@ __global__ void k_stream_final(const uint32_t* st, const uint8_t* block, uint64_
   out[1] = (uint64_t)h.w[2] | ((uint64_t)h.w[3] << 32);
 }
 
-// ------------------------------------------------------------ host side
+}  // namespace
+
+// ------------------------------------------------------------ host runtime (kvh_internal.hpp)
+namespace kvh {
+namespace rt {
+
 thread_local int t_last_err = 0;
 
 struct DevInfo {
@@ -940,15 +909,6 @@ struct DevInfo {
 };
 std::mutex g_mu;
 std::vector<DevInfo> g_dev;
-int g_tune_nt = 2;        // tables per LDS: 2 or 4
-int g_tune_wgmul = 1;     // workgroups per CU multiplier
-int g_tune_generic = 0;   // force the generic kernel
-int g_tune_kpl = 2;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8)
-int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
-int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
-int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
-int g_tune_var_mode = 0;  // ablation of k_var3: 1 no-hash, 2 no-gather, 3 no-sort
-int g_tune_var = 0;       // var-length kernel: 0 = unsorted k_generic, 2/4 = windowed sort (NT tables)
 
 int set_err(int e) { t_last_err = e; return e; }
 int hip_err(hipError_t e) { return set_err(KVH_EHIP_BASE - (int)e); }
@@ -969,6 +929,28 @@ int device_cus(int* cus) {
   return 0;
 }
 
+int launch_done() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(e);
+  return set_err(0);
+}
+
+}  // namespace rt
+}  // namespace kvh
+
+namespace {
+
+// ------------------------------------------------------------ host side
+int g_tune_nt = 2;        // tables per LDS: 2 or 4
+int g_tune_wgmul = 1;     // workgroups per CU multiplier
+int g_tune_generic = 0;   // force the generic kernel
+int g_tune_kpl = 2;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8)
+int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
+int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
+int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
+int g_tune_var_mode = 0;  // ablation of k_var3: 1 no-hash, 2 no-gather, 3 no-sort
+int g_tune_var = 0;       // var-length kernel: 0 = unsorted k_generic, 2/4 = windowed sort (NT tables)
+
 uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
   const uint64_t need = (n + kBlock - 1) / kBlock;
   uint64_t g = (uint64_t)cus * (uint64_t)std::max(1, wg_per_cu * g_tune_wgmul);
@@ -976,11 +958,6 @@ uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
   return (uint32_t)std::max<uint64_t>(g, 1);
 }
 
-int launch_done() {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return hip_err(e);
-  return set_err(0);
-}
 
 template <int L, int NT, int U, int MODE = 0>
 int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,

@@ -8,7 +8,12 @@ reference's own functions (kv_hash_meow128 and its batched / streaming /
 vec variants, key_hash.c:1413-2020); the inputs are our own seeded random
 data.  The fixtures are data only (inputs + expected outputs).
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [--only-cuckoo]
+
+The table-position fixtures (cuckoo_*.npz) come from the reference's
+ht_init.cpp + ht_cuckoo.cpp compiled where they lie into
+oracle/_ref/libkvref_ht.so (oracle/ref_cuckoo.cpp drives
+CuckooAltHash::calc_hash).
 """
 from __future__ import annotations
 
@@ -197,5 +202,69 @@ def main():
     print("golden fixtures written to", HERE)
 
 
+# geometries for the table-position fixtures:
+# (name, map_size, hash_entry_size, hash_value_ratio, cuckoo_buckets, cuckoo_arity)
+CUCKOO_GEOMS = [
+    ("kat64m_4x4", 64 << 20, 64, 1.0, 4, 4),        # SURVEY §8c "hello" KAT geometry
+    ("srv64m_2p4", 64 << 20, 64, 0.5, 4, 2),        # server default "2+4" (server.cpp:49)
+    ("tiny600_8x8", (448 << 10) + 64 * 600, 64, 1.0, 8, 8),  # tiny table: heavy rejection
+    ("tiny5000_2x5", (448 << 10) + 64 * 5000, 64, 1.0, 2, 5),
+    ("mid16m_3x1", 16 << 20, 128, 0.75, 1, 3),      # buckets 1 = linear probe (key_ctx.cpp:130)
+    ("mid32m_6x2", 32 << 20, 64, 0.9, 2, 6),
+    ("mid24m_7x3", 24 << 20, 64, 0.6, 3, 7),
+    ("lin64m_1", 64 << 20, 64, 1.0, 1, 1),          # linear table: home slot only
+    ("c2x2_8m", 8 << 20, 64, 1.0, 2, 2),            # smallest cuckoo shape
+    ("ar1b4_8m", 8 << 20, 64, 1.0, 4, 1),           # arity 1: start slot only
+    ("big4g_4x4", 4 << 30, 64, 1.0, 4, 4),          # 2^26-entry table (mask bits > 26)
+]
+
+
+def load_ref_ht():
+    lib = C.CDLL(os.path.join(ROOT, "oracle", "_ref", "libkvref_ht.so"))
+    lib.ref_cuckoo_positions.argtypes = [U64, C.c_uint32, C.c_float, C.c_uint16, C.c_uint8, P, C.c_size_t,
+                                         P, P]
+    return lib
+
+
+def make_cuckoo():
+    """CuckooAltHash::calc_hash positions (ht_cuckoo.cpp:38-79) from the
+    reference's own ht_init.cpp + ht_cuckoo.cpp (oracle/ref_cuckoo.cpp)."""
+    ref = load_ref_ht()
+    lib = load_ref()
+    rng = np.random.default_rng(20261015)
+    # inputs: fixed-up meow hashes of real keys, raw random pairs, and pairs
+    # built to collide (h2 = h1, h2 near h1's slot) so both alt1 branches run
+    n_real, n_rand = 3000, 3000
+    kb = rng.integers(0, 256, size=n_real * 16, dtype=np.uint8)
+    hh = np.zeros(2 * n_real, dtype=np.uint64)
+    lib.ref_batch_fixed(ptr(kb), 16, n_real, U64(STATIC_SEED[0]), U64(STATIC_SEED[1]), ptr(hh))
+    hh = hh.reshape(-1, 2)
+    hh[:, 0] &= np.uint64((1 << 63) - 1)
+    hh[hh[:, 0] <= 1, 0] = 2
+    hello = meow(lib, b"hello\0", *STATIC_SEED)
+    hello = ((hello[0] & ((1 << 63) - 1)) or 2, hello[1])
+    rand = rng.integers(0, 2 ** 64, size=(n_rand, 2), dtype=np.uint64)
+    same = rand[:200].copy(); same[:, 1] = same[:, 0]
+    near = rand[200:400].copy(); near[:, 1] = near[:, 0] + np.uint64(1)
+    edge = np.array([[0, 0], [1, 2], [2 ** 64 - 1, 2 ** 64 - 1], [2 ** 63, 0], [0, 2 ** 63]], dtype=np.uint64)
+    hashes = np.ascontiguousarray(np.concatenate([np.array([hello], dtype=np.uint64), hh, rand, same, near,
+                                                  edge]))
+    for name, ms, es, ratio, buckets, arity in CUCKOO_GEOMS:
+        a = arity if (buckets > 1 and arity > 1) else 1  # linear tables: start slot only
+        pos = np.zeros(len(hashes) * a, dtype=np.uint64)
+        geom = np.zeros(4, dtype=np.uint64)
+        rc = ref.ref_cuckoo_positions(ms, es, ratio, buckets, arity, ptr(hashes), len(hashes), ptr(pos),
+                                      ptr(geom))
+        assert rc == 0, name
+        np.savez_compressed(os.path.join(HERE, f"cuckoo_{name}.npz"), hashes=hashes, pos=pos.reshape(-1, a),
+                            params=np.array([ms, es, buckets, arity], dtype=np.uint64),
+                            ratio=np.array([ratio], dtype=np.float32),
+                            geom=geom,  # ht_mod_mask, ht_mod_fraction, ht_mod_shift, ht_size
+                            keys16=kb, seed=np.array(STATIC_SEED, dtype=np.uint64))  # hashes[1:1+len(kb)//16]
+        print(name, "ht_size", int(geom[3]), "pos[0]", pos[:a])
+
+
 if __name__ == "__main__":
-    main()
+    if "--only-cuckoo" not in sys.argv:
+        main()
+    make_cuckoo()

@@ -82,3 +82,59 @@ def orc_multiseed(lib, keys: np.ndarray, key_len: int, seeds, fixup=False) -> np
 
 def golden(name):
     return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+# ------------------------------------------------------------ table positions (§8 f1)
+class OrcGeom(C.Structure):
+    _fields_ = [("ht_size", U64), ("ht_mod_mask", U64), ("ht_mod_fraction", U64), ("ht_mod_shift", C.c_uint32),
+                ("cuckoo_buckets", C.c_uint16), ("cuckoo_arity", C.c_uint8), ("pad", C.c_uint8)]
+
+
+def _orc_pos_sigs(lib):
+    lib.orc_ht_geom.argtypes = [U64, C.c_uint32, C.c_float, C.c_uint16, C.c_uint8, C.POINTER(OrcGeom)]
+    lib.orc_ht_geom.restype = C.c_int
+    lib.orc_ht_mod.argtypes = [C.POINTER(OrcGeom), U64]
+    lib.orc_ht_mod.restype = U64
+    lib.orc_positions_per_key.argtypes = [C.POINTER(OrcGeom)]
+    lib.orc_positions_per_key.restype = C.c_uint
+    lib.orc_cuckoo_positions.argtypes = [C.POINTER(OrcGeom), P, SZ, P]
+
+
+def orc_geom(lib, map_size, entry_size, ratio, buckets, arity) -> OrcGeom:
+    _orc_pos_sigs(lib)
+    g = OrcGeom()
+    assert lib.orc_ht_geom(map_size, entry_size, ratio, buckets, arity, C.byref(g)) == 0
+    return g
+
+
+def orc_positions(lib, g: OrcGeom, hashes: np.ndarray) -> np.ndarray:
+    _orc_pos_sigs(lib)
+    h = np.ascontiguousarray(hashes, dtype=np.uint64).reshape(-1, 2)
+    a = lib.orc_positions_per_key(C.byref(g))
+    pos = np.zeros((len(h), a), dtype=np.uint64)
+    lib.orc_cuckoo_positions(C.byref(g), h.ctypes.data, len(h), pos.ctypes.data)
+    return pos
+
+
+def cuckoo_fixtures():
+    import glob
+    out = []
+    for f in sorted(glob.glob(os.path.join(GOLDEN, "cuckoo_*.npz"))):
+        d = np.load(f)
+        ms, es, b, a = (int(x) for x in d["params"])
+        out.append(dict(name=os.path.basename(f)[7:-4], map_size=ms, entry_size=es, buckets=b, arity=a,
+                        ratio=float(d["ratio"][0]), geom=d["geom"], hashes=d["hashes"], pos=d["pos"],
+                        keys16=d["keys16"], seed=tuple(int(x) for x in d["seed"])))
+    return out
+
+
+def load_ref_ht():
+    p = os.path.join(ROOT, "oracle", "_ref", "libkvref_ht.so")
+    if not os.path.exists(p):
+        return None
+    lib = C.CDLL(p)
+    lib.ref_cuckoo_positions.argtypes = [U64, C.c_uint32, C.c_float, C.c_uint16, C.c_uint8, P, SZ, P, P]
+    lib.ref_cuckoo_bench.argtypes = [U64, U64, U64, C.c_uint32, C.c_uint16, C.c_uint8, P, SZ, SZ, U64, U64, P, P,
+                                     C.c_int]
+    lib.ref_cuckoo_bench.restype = C.c_double
+    return lib
