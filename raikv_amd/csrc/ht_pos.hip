@@ -31,8 +31,8 @@ namespace {
 constexpr int kPosBlock = 256;  // no LDS: small groups, many waves per CU
 constexpr int kFusedBlock = 1024;
 
-template <int A, bool P32>
-__device__ __forceinline__ void store_pos(void* __restrict__ pos, uint64_t idx, const uint64_t (&q)[A]) {
+template <int A, bool P32, typename W>
+__device__ __forceinline__ void store_pos(void* __restrict__ pos, uint64_t idx, const W (&q)[A]) {
   if constexpr (P32) {
     uint32_t* p = (uint32_t*)pos + idx * A;
     if constexpr (A % 4 == 0) {
@@ -59,42 +59,89 @@ __device__ __forceinline__ void store_pos(void* __restrict__ pos, uint64_t idx, 
 #pragma unroll
       for (int i = 0; i < A; i += 2) {
         v4u v;
-        v.x = (uint32_t)q[i]; v.y = (uint32_t)(q[i] >> 32);
-        v.z = (uint32_t)q[i + 1]; v.w = (uint32_t)(q[i + 1] >> 32);
+        v.x = (uint32_t)q[i]; v.y = (uint32_t)((uint64_t)q[i] >> 32);
+        v.z = (uint32_t)q[i + 1]; v.w = (uint32_t)((uint64_t)q[i + 1] >> 32);
         __builtin_nontemporal_store(v, (v4u*)(p + 2 * i));
       }
     } else {
 #pragma unroll
       for (int i = 0; i < A; i++) {
         v2u v;
-        v.x = (uint32_t)q[i]; v.y = (uint32_t)(q[i] >> 32);
+        v.x = (uint32_t)q[i]; v.y = (uint32_t)((uint64_t)q[i] >> 32);
         __builtin_nontemporal_store(v, (v2u*)(p + 2 * i));
       }
     }
   }
 }
 
-template <int A, bool P32, int U>
+// 32-byte position records (A = 4 u64, or A = 8 u32): one lane per key
+// would store each record as two 16-byte pieces 32 bytes apart, so every
+// store instruction half-fills the lines it touches (the write traffic
+// inflates, as measured for the multi-seed kernel).  Instead lane 2m owns
+// key m and lane 2m+1 key 32+m of the 64-key chunk; adjacent lanes swap one
+// half through a DPP quad permute, after which store 0 writes keys 0..31
+// and store 1 keys 32..63, each one contiguous 1 KiB run.
+template <int A, bool P32>
+constexpr bool kPairRec = A * (P32 ? 4 : 8) == 32;
+
+__device__ __forceinline__ uint64_t chunk_key(uint64_t lane, bool pair) {
+  return pair ? (lane >> 1) + 32 * (lane & 1) : lane;
+}
+
+template <int A, bool P32, typename W>
+__device__ __forceinline__ void store_pos_pair(void* __restrict__ pos, uint64_t base, uint64_t lane, uint64_t last,
+                                               const W (&q)[A]) {
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < A; i++) {
+    if constexpr (P32) {
+      w[i] = (uint32_t)q[i];
+    } else {
+      w[2 * i] = (uint32_t)q[i];
+      w[2 * i + 1] = (uint32_t)((uint64_t)q[i] >> 32);
+    }
+  }
+  const bool even = (lane & 1) == 0;
+  uint32_t y[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t x = even ? w[4 + c] : w[c];
+    y[c] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  }
+  v4u s0, s1;
+  s0.x = even ? w[0] : y[0]; s0.y = even ? w[1] : y[1]; s0.z = even ? w[2] : y[2]; s0.w = even ? w[3] : y[3];
+  s1.x = even ? y[0] : w[4]; s1.y = even ? y[1] : w[5]; s1.z = even ? y[2] : w[6]; s1.w = even ? y[3] : w[7];
+  v4u* p = (v4u*)((uint8_t*)pos + base * 32) + lane;
+  if (base + (lane >> 1) <= last) __builtin_nontemporal_store(s0, p);
+  if (base + 32 + (lane >> 1) <= last) __builtin_nontemporal_store(s1, p + 64);
+}
+
+template <int A, bool P32, typename W, int U>
 __global__ void __launch_bounds__(kPosBlock)
 k_positions(const uint64_t* __restrict__ hashes, uint64_t n, HtGeom g, void* __restrict__ pos) {
+  constexpr bool PAIR = kPairRec<A, P32>;
   const uint64_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
   const uint64_t last = n - 1;
+  const uint64_t kofs = chunk_key(lane, PAIR);
   for (uint64_t b = wave * 64 * U; b < n; b += step) {
     v4u h[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t j = std::min<uint64_t>(b + 64 * u + lane, last);
+      const uint64_t j = std::min<uint64_t>(b + 64 * u + kofs, last);
       h[u] = __builtin_nontemporal_load((const v4u*)(hashes + 2 * j));
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep all U loads in flight before the first use
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t j = std::min<uint64_t>(b + 64 * u + lane, last);
-      uint64_t q[A];
-      cuckoo_positions<A>(g, (uint64_t)h[u].x | ((uint64_t)h[u].y << 32),
-                          (uint64_t)h[u].z | ((uint64_t)h[u].w << 32), q);
-      store_pos<A, P32>(pos, j, q);
+      W q[A];
+      cuckoo_positions<A, W>(g, (uint64_t)h[u].x | ((uint64_t)h[u].y << 32),
+                             (uint64_t)h[u].z | ((uint64_t)h[u].w << 32), q);
+      if constexpr (PAIR)
+        store_pos_pair<A, P32, W>(pos, b + 64 * u, lane, last, q);
+      else
+        store_pos<A, P32, W>(pos, std::min<uint64_t>(b + 64 * u + kofs, last), q);
     }
   }
 }
@@ -102,7 +149,7 @@ k_positions(const uint64_t* __restrict__ hashes, uint64_t n, HtGeom g, void* __r
 // Fused epilogue on k_fixed's body (kvh.hip): the hash is fixed up
 // (KeyFragment::hash, hash_entry.h:84-85) because KeyCtx::set_key_hash
 // feeds the fixed-up h1 to ht_mod (key_ctx.cpp:97-105).
-template <int L, int NT, int A, bool P32, int U>
+template <int L, int NT, int A, bool P32, typename W, int U>
 __global__ void __launch_bounds__(kFusedBlock)
 k_fixed_pos(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2, HtGeom g,
             uint64_t* __restrict__ out, void* __restrict__ pos) {
@@ -117,11 +164,13 @@ k_fixed_pos(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t 
   const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
   const uint64_t last = n - 1;
   const bool keep = out != nullptr;
+  constexpr bool PAIR = kPairRec<A, P32>;
+  const uint64_t kofs = chunk_key(lane, PAIR);
   for (uint64_t b = wave * 64 * U; b < n; b += step) {
     Blk D[U][NC];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t j = std::min<uint64_t>(b + 64 * u + lane, last);
+      const uint64_t j = std::min<uint64_t>(b + 64 * u + kofs, last);
       load_fixed<L, true, true>(keys + j * L, D[u]);
     }
     Blk h[U];
@@ -129,12 +178,15 @@ k_fixed_pos(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t 
     for (int u = 0; u < U; u++) h[u] = fixup(meow_ct<L>(D[u], K, T));
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t j = std::min<uint64_t>(b + 64 * u + lane, last);
+      const uint64_t j = std::min<uint64_t>(b + 64 * u + kofs, last);
       if (keep) store_h<true>(out, j, h[u], false);
-      uint64_t q[A];
-      cuckoo_positions<A>(g, (uint64_t)h[u].w[0] | ((uint64_t)h[u].w[1] << 32),
-                          (uint64_t)h[u].w[2] | ((uint64_t)h[u].w[3] << 32), q);
-      store_pos<A, P32>(pos, j, q);
+      W q[A];
+      cuckoo_positions<A, W>(g, (uint64_t)h[u].w[0] | ((uint64_t)h[u].w[1] << 32),
+                             (uint64_t)h[u].w[2] | ((uint64_t)h[u].w[3] << 32), q);
+      if constexpr (PAIR)
+        store_pos_pair<A, P32, W>(pos, b + 64 * u, lane, last, q);
+      else
+        store_pos<A, P32, W>(pos, j, q);
     }
   }
 }
@@ -149,7 +201,9 @@ uint32_t per_key(const kvh_ht_geom_t* g) {
 // A-1 earlier picks (each excluding a 2*buckets-1 ring window and its
 // 13-bit index class) are non-empty, so the rejection loop terminates.
 int check_geom(const kvh_ht_geom_t* g, bool p32) {
-  if (!g || g->ht_size == 0 || g->ht_mod_shift >= 64 || g->ht_mod_fraction == 0) return KVH_EINVAL;
+  if (!g || g->ht_size == 0 || g->ht_mod_shift >= 64 || g->ht_mod_fraction == 0 ||
+      g->ht_mod_fraction >= (1ull << 32))
+    return KVH_EINVAL;
   const uint64_t top = (g->ht_mod_mask * g->ht_mod_fraction) >> g->ht_mod_shift;
   if (top >= g->ht_size) return KVH_EINVAL;  // ht_mod must stay inside ht[]
   if (p32 && g->ht_size > (1ull << 32)) return KVH_EINVAL;
@@ -167,18 +221,25 @@ HtGeom dev_geom(const kvh_ht_geom_t* g) {
   HtGeom d;
   d.size = g->ht_size;
   d.mask = g->ht_mod_mask;
-  d.frac = g->ht_mod_fraction;
+  d.frac = (uint32_t)g->ht_mod_fraction;
   d.shift = g->ht_mod_shift;
   d.buckets = g->cuckoo_buckets;
   return d;
 }
 
+bool narrow(const HtGeom& g) { return g.mask < (1ull << 32) && g.size < (1ull << 32); }
+
 template <int A, bool P32>
 void launch_positions(const uint64_t* h, uint64_t n, HtGeom g, void* pos, hipStream_t st, int cus) {
-  constexpr int U = 2;
+  constexpr int U = 4;
   const uint64_t need = (n + kPosBlock * U - 1) / (kPosBlock * U);
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)cus * 8));
-  hipLaunchKernelGGL((k_positions<A, P32, U>), dim3((uint32_t)grid), dim3(kPosBlock), 0, st, h, n, g, pos);
+  if (narrow(g))
+    hipLaunchKernelGGL((k_positions<A, P32, uint32_t, U>), dim3((uint32_t)grid), dim3(kPosBlock), 0, st, h, n, g,
+                       pos);
+  else if constexpr (!P32)  // wide tables have no u32 output (check_geom)
+    hipLaunchKernelGGL((k_positions<A, P32, uint64_t, U>), dim3((uint32_t)grid), dim3(kPosBlock), 0, st, h, n, g,
+                       pos);
 }
 
 template <bool P32>
@@ -203,8 +264,12 @@ void launch_fused(const uint8_t* k, uint64_t n, uint64_t s1, uint64_t s2, HtGeom
   constexpr int NT = 2, U = 2;
   const uint64_t need = (n + kFusedBlock - 1) / kFusedBlock;
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)cus * 2));
-  hipLaunchKernelGGL((k_fixed_pos<L, NT, A, P32, U>), dim3((uint32_t)grid), dim3(kFusedBlock), 0, st, k, n, s1,
-                     s2, g, out, pos);
+  if (narrow(g))
+    hipLaunchKernelGGL((k_fixed_pos<L, NT, A, P32, uint32_t, U>), dim3((uint32_t)grid), dim3(kFusedBlock), 0, st, k,
+                       n, s1, s2, g, out, pos);
+  else if constexpr (!P32)
+    hipLaunchKernelGGL((k_fixed_pos<L, NT, A, P32, uint64_t, U>), dim3((uint32_t)grid), dim3(kFusedBlock), 0, st, k,
+                       n, s1, s2, g, out, pos);
 }
 
 template <int L, bool P32>

@@ -117,7 +117,7 @@ def test_huge_table_geometry(kvh):
     # masks beyond 32 bits; geometry from the same restatement the fixtures pin
     rng = np.random.default_rng(21)
     h = rng.integers(0, 2 ** 64, size=(200_000, 2), dtype=np.uint64)
-    for ms in (1 << 41, 3 << 40, 288 << 30):
+    for ms in (1 << 41, 3 << 40, 288 << 30, 255 << 30, 16 << 30):
         g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
         og = orc_geom(ORC, ms, 64, 1.0, 4, 4)
         pos = kvh.ht_positions(dev_u64(h), g)

@@ -9,8 +9,11 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 HOT = ("k_fixed", "k_var", "k_generic", "k_fixed_ms", "k_fixed_dma")
-traffic = {}
-summary = {}
+HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",)}
+tpath = os.path.join(root, "profiles", "pmc_traffic.json")
+spath = os.path.join(dst, "summary.json")
+traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
+summary = json.load(open(spath)) if os.path.exists(spath) else {}
 for c in sorted(os.listdir(src)):
     d = os.path.join(src, c)
     if not os.path.isdir(d):
@@ -21,10 +24,11 @@ for c in sorted(os.listdir(src)):
     if bj:
         shutil.copy(os.path.join(d, "bench.json"), os.path.join(dst, f"{c}_bench_under_rocprof.json"))
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
-    hot = [r for r in stats if any(h in r["Name"] for h in HOT)]
+    hot_names = HOT_BY_CFG.get(c, HOT)
+    hot = [r for r in stats if any(h in r["Name"] for h in hot_names)]
     pmc = json.load(open(os.path.join(d, "pmc_summary.json")))
     for k, v in pmc.items():
-        if any(h in k for h in HOT) and "FETCH_SIZE" in v:
+        if any(h in k for h in hot_names) and "FETCH_SIZE" in v:
             hbm = v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024
             traffic[c] = {"hbm_bytes_per_launch": hbm, "kernel": k,
                           "fetch_size_kb": v["FETCH_SIZE"], "write_size_kb": v["WRITE_SIZE"],
@@ -36,6 +40,6 @@ for c in sorted(os.listdir(src)):
                           "calls": int(hot[0]["Calls"]) if hot else None, "hbm_bytes_per_launch": hbm,
                           "clock_GHz_est": clk,
                           "lds_util": (v["SQ_LDS_IDX_ACTIVE"] / 256 / (v["GRBM_GUI_ACTIVE"] / 8)) if "SQ_LDS_IDX_ACTIVE" in v else None}
-json.dump(traffic, open(os.path.join(root, "profiles", "pmc_traffic.json"), "w"), indent=1)
-json.dump(summary, open(os.path.join(dst, "summary.json"), "w"), indent=1)
+json.dump(traffic, open(tpath, "w"), indent=1)
+json.dump(summary, open(spath, "w"), indent=1)
 print(json.dumps(summary, indent=1))

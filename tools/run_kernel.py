@@ -28,10 +28,21 @@ if a.var >= 0:
 torch.cuda.set_device(0)
 g = torch.Generator(device="cuda")
 g.manual_seed(1)
-cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1)}
+cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1),
+       "f1": (100_000_000, 16, -1), "f1p": (100_000_000, 16, -2)}
 n, L, ar = cfg[a.config]
 n = a.n or n
-if L == 0:
+if ar < 0:  # table positions, geometry as bench.py F1_GEOM
+    geom = kvh.HtGeom.from_map(64 << 30, 64, 1.0, 4, 4)
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    hh = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    pos = torch.empty((n, geom.per_key), dtype=torch.int64, device="cuda")
+    if ar == -1:
+        f = lambda: kvh.meow128_fixed_positions(keys, L, kvh.STATIC_SEED, geom, hashes=hh, out=pos)
+    else:
+        kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=hh, fixup=True)
+        f = lambda: kvh.ht_positions(hh, geom, out=pos)
+elif L == 0:
     offs = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=3))
     keys = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device="cuda", generator=g)
     doff = torch.from_numpy(offs.view(np.int64)).cuda()
