@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "128-bit key hashes/sec device-resident, 16–64B keys; GB/s vs HBM peak"
 METRIC_F1 = "keys/sec -> hash + cuckoo table positions, device-resident (SURVEY.md §8 f1)"
+METRIC_F4 = "CRC32C (kv_crc_c) keys/sec, device-resident (SURVEY.md §8 f4)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 
 CONFIGS = {
@@ -52,6 +53,11 @@ CONFIGS = {
     "f1p": dict(workload="F1p: 100M resident fixed-up (h1,h2) -> cuckoo arity-4 table positions "
                          "(64 GiB map, 4 buckets), u64 positions",
                 n=100_000_000, key_len=16, arity=1, var=False, positions="only"),
+    # batched CRC32C (kv_crc_c) on the C1 / C2 key shapes
+    "f4": dict(workload="F4: 100M fixed 16-byte keys -> kv_crc_c (CRC32C, seed 0), u32 out",
+               n=100_000_000, key_len=16, arity=1, var=False, crc=True),
+    "f4v": dict(workload="F4v: 100M zipf 8-256 B keys (C2 shape) -> kv_crc_c, u32 out",
+                n=100_000_000, key_len=0, arity=1, var=True, crc=True),
 }
 F1_GEOM = dict(map_size=64 << 30, hash_entry_size=64, hash_value_ratio=1.0, cuckoo_buckets=4, cuckoo_arity=4)
 
@@ -142,6 +148,48 @@ def cpu_baseline_positions(cfg, seed, seconds: float, geom):
                       f"{threads} threads, {total_t:.1f} s"}
 
 
+def cpu_baseline_crc(cfg, seconds: float):
+    """Reference kv_crc_c_array (key_hash.c:122-142, SSE4.2 crc32, its own
+    source compiled into oracle/_ref/libkvref.so) on host threads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_ref  # checker only
+    import ctypes as C
+    import threading
+    from raikv_amd.workload import zipf_lengths, offsets_from_lengths
+    ref = load_ref()
+    if ref is None:
+        return {"value": None, "error": "oracle/_ref/libkvref.so not built"}
+    ref.kv_crc_c_array.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n = 2_000_000
+    L = cfg["key_len"]
+    lens = zipf_lengths(n, 8, 256, seed=3) if cfg["var"] else np.full(n, L, np.int64)
+    offs = offsets_from_lengths(lens)
+    keys = np.random.default_rng(1).integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    ptrs = (keys.ctypes.data + offs[:-1].astype(np.uint64)).astype(np.uint64)
+    szs = np.asarray(lens, dtype=np.uint64)
+    seeds = np.zeros(n, dtype=np.uint32)
+    bounds = [n * t // threads for t in range(threads + 1)]
+
+    def part(t):
+        a, b = bounds[t], bounds[t + 1]
+        ref.kv_crc_c_array(ptrs.ctypes.data + 8 * a, szs.ctypes.data + 8 * a, seeds.ctypes.data + 4 * a, b - a)
+
+    total_t, total_n = 0.0, 0
+    while total_t < seconds:
+        ts = [threading.Thread(target=part, args=(t,)) for t in range(threads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        total_t += time.perf_counter() - t0
+        total_n += n
+    return {"value": total_n / total_t, "unit": "key/s", "cores": threads, "kind": "reference",
+            "sample": f"{total_n} keys ({n} distinct, {'zipf 8-256 B' if cfg['var'] else f'{L} B'}) x "
+                      f"kv_crc_c_array, {threads} threads (ctypes releases the GIL), {total_t:.1f} s"}
+
+
 def load_traffic(config_name: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -187,7 +235,21 @@ def main():
     gen.manual_seed(1000 + rank)
 
     # ---- synthetic keys resident in HBM (each rank its own shard)
-    if cfg["var"]:
+    if cfg.get("crc"):
+        crc_out = torch.empty((n,), dtype=torch.int32, device="cuda")
+        if cfg["var"]:
+            lens = zipf_lengths(n, 8, 256, seed=3 + rank)
+            offs_np = offsets_from_lengths(lens)
+            keys = torch.randint(0, 256, (int(offs_np[-1]),), dtype=torch.uint8, device="cuda", generator=gen)
+            offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
+            alg_bytes = int(offs_np[-1]) + 8 * (n + 1) + 4 * n
+            del lens
+            run = lambda out: kvh.crc_c_var(keys, offs, 0, out=crc_out)
+        else:
+            keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=gen)
+            alg_bytes = n * L + 4 * n
+            run = lambda out: kvh.crc_c_fixed(keys, L, 0, out=crc_out)
+    elif cfg["var"]:
         lens = zipf_lengths(n, 8, 256, seed=3 + rank)
         offs_np = offsets_from_lengths(lens)
         key_bytes = int(offs_np[-1])
@@ -217,7 +279,7 @@ def main():
             run = lambda out: kvh.meow128_fixed(keys, L, seed, out=out)
         else:
             run = lambda out: kvh.meow128_multiseed(keys, L, list(C3_SEEDS[:arity]), out=out)
-    out = None if cfg.get("positions") else \
+    out = None if (cfg.get("positions") or cfg.get("crc")) else \
         torch.empty((n, arity, 2) if arity > 1 else (n, 2), dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
 
@@ -245,9 +307,9 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic, tsrc = load_traffic(args.config)
     res = {
-        "metric": METRIC_F1 if cfg.get("positions") else METRIC,
+        "metric": METRIC_F1 if cfg.get("positions") else (METRIC_F4 if cfg.get("crc") else METRIC),
         "value": value,
-        "unit": "key/s" if cfg.get("positions") else "hash/s",
+        "unit": "key/s" if (cfg.get("positions") or cfg.get("crc")) else "hash/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -274,6 +336,8 @@ def main():
         try:
             if cfg.get("positions"):
                 res["cpu_baseline"] = cpu_baseline_positions(cfg, seed, args.cpu_seconds, geom)
+            elif cfg.get("crc"):
+                res["cpu_baseline"] = cpu_baseline_crc(cfg, args.cpu_seconds)
             else:
                 res["cpu_baseline"] = cpu_baseline(cfg, seed, args.cpu_seconds)
         except Exception as e:  # report, never hide

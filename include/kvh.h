@@ -234,6 +234,38 @@ int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
                                 void *pos, uint32_t flags, void *stream);
 
 /* ---------------------------------------------------------------------
+ * CRC32C: raikv's kv_crc_c family (key_hash.c:27-179),
+ * the SSE4.2 crc32 chain from `seed`, no pre/post inversion.
+ * ------------------------------------------------------------------- */
+/* Device batches: out[i] = kv_crc_c(key_i, len_i, seeds ? seeds[i] : seed).
+ * seeds (optional, device) may equal out (kv_crc_c_array's in/out seeds). */
+int kvh_crc_c_fixed(const void *keys, uint32_t key_len, size_t n,
+                    const uint32_t *seeds, uint32_t seed, uint32_t *out,
+                    void *stream);
+int kvh_crc_c_var(const void *keys, const uint64_t *offsets, size_t n,
+                  const uint32_t *seeds, uint32_t seed, uint32_t *out,
+                  void *stream);
+/* Host drop-ins (synchronous, executed on the current GPU). */
+/* key_hash.c:53-63 kv_crc_c (returns the crc; errors via kvh_last_error) */
+uint32_t kvh_crc_c(const void *p, size_t sz, uint32_t seed);
+/* key_hash.c:27-37 kv_hash_uint / kv_hash_uint2 */
+uint32_t kvh_hash_uint(uint32_t i);
+uint32_t kvh_hash_uint2(uint32_t r, uint32_t i);
+/* key_hash.c:65-84, :86-120 */
+int kvh_crc_c_2_diff(const void *p, size_t sz, uint32_t *seed,
+                     const void *p2, size_t sz2, uint32_t *seed2);
+int kvh_crc_c_4_diff(const void *p, size_t sz, uint32_t *seed,
+                     const void *p2, size_t sz2, uint32_t *seed2,
+                     const void *p3, size_t sz3, uint32_t *seed3,
+                     const void *p4, size_t sz4, uint32_t *seed4);
+/* key_hash.c:122-142: seed[i] = kv_crc_c(p[i], psz[i], seed[i]) */
+int kvh_crc_c_array(const void **p, size_t *psz, uint32_t *seed, size_t count);
+/* key_hash.c:168-179: seed[i] = kv_crc_c(p, psz[i], seed[i]) -- prefixes
+ * of ONE buffer p (every entry reads from the same start) */
+int kvh_crc_c_key_array(const void *p, size_t *psz, uint32_t *seed,
+                        size_t count);
+
+/* ---------------------------------------------------------------------
  * Runtime / diagnostics
  * ------------------------------------------------------------------- */
 int         kvh_last_error(void);

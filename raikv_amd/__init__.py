@@ -11,6 +11,9 @@ from .binding import (  # noqa: F401
     KVH_FIXUP,
     KVH_POS32,
     HtGeom,
+    crc_c_fixed,
+    crc_c_var,
+    kv_crc_c,
     ht_positions,
     meow128_fixed_positions,
     KvhError,
@@ -32,5 +35,5 @@ __all__ = [
     "KVH_FIXUP", "KvhError", "lib", "lib_path", "meow128_fixed", "meow128_var",
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
-    "meow128_fixed_positions",
+    "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
 ]

@@ -96,6 +96,15 @@ def _load():
         "kvh_positions_per_key": (U32, [P]),
         "kvh_ht_positions": (I, [P, SZ, P, P, U32, P]),
         "kvh_meow128_fixed_positions": (I, [P, U32, SZ, U64, U64, P, P, P, U32, P]),
+        "kvh_crc_c_fixed": (I, [P, U32, SZ, P, U32, P, P]),
+        "kvh_crc_c_var": (I, [P, P, SZ, P, U32, P, P]),
+        "kvh_crc_c": (U32, [P, SZ, U32]),
+        "kvh_hash_uint": (U32, [U32]),
+        "kvh_hash_uint2": (U32, [U32, U32]),
+        "kvh_crc_c_2_diff": (I, [P, SZ, P, P, SZ, P]),
+        "kvh_crc_c_4_diff": (I, [P, SZ, P, P, SZ, P, P, SZ, P, P, SZ, P]),
+        "kvh_crc_c_array": (I, [P, P, P, SZ]),
+        "kvh_crc_c_key_array": (I, [P, P, P, SZ]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
         "kvh_version": (C.c_char_p, []),
@@ -182,6 +191,39 @@ def meow128_fixed_positions(keys, key_len: int, seed: Tuple[int, int], geom: "Ht
                                           _dev_ptr(out) if n else None, KVH_POS32 if pos32 else 0,
                                           _stream_ptr(stream)), "kvh_meow128_fixed_positions")
     return hashes, out
+
+
+def crc_c_fixed(keys, key_len: int, seed: int = 0, seeds=None, out=None, stream=None):
+    """kv_crc_c over n fixed-length keys (key_hash.c:53-63) -> uint32 bit
+    patterns in an int32 device tensor [n]; seeds: optional int32 [n]."""
+    n = keys.numel() // key_len if key_len else 0
+    if out is None:
+        out = torch.empty((n,), dtype=torch.int32, device=keys.device)
+    check(lib.kvh_crc_c_fixed(_dev_ptr(keys) if keys.numel() else None, key_len, n,
+                              _dev_ptr(seeds) if seeds is not None else None, seed & 0xFFFFFFFF,
+                              _dev_ptr(out) if n else None, _stream_ptr(stream)), "kvh_crc_c_fixed")
+    return out
+
+
+def crc_c_var(keys, offsets, seed: int = 0, seeds=None, out=None, stream=None):
+    """kv_crc_c over n variable-length keys (u64 offsets [n+1])."""
+    n = offsets.numel() - 1
+    if out is None:
+        out = torch.empty((n,), dtype=torch.int32, device=offsets.device)
+    check(lib.kvh_crc_c_var(_dev_ptr(keys) if keys.numel() else _dev_ptr(offsets), _dev_ptr(offsets), n,
+                            _dev_ptr(seeds) if seeds is not None else None, seed & 0xFFFFFFFF,
+                            _dev_ptr(out) if n else None, _stream_ptr(stream)), "kvh_crc_c_var")
+    return out
+
+
+def kv_crc_c(data: bytes, seed: int = 0) -> int:
+    """Drop-in kv_crc_c (executes on the GPU)."""
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    r = lib.kvh_crc_c(buf, len(data), seed & 0xFFFFFFFF)
+    rc = lib.kvh_last_error()
+    if rc:
+        check(rc, "kvh_crc_c")
+    return int(r)
 
 
 def meow128_var(keys, offsets, seed: Tuple[int, int], out=None, fixup: bool = False, stream=None):

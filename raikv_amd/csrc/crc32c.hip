@@ -1,0 +1,303 @@
+// crc32c.hip -- SURVEY.md §8 row f4: batched CRC32C (raikv's kv_crc_c
+// family, src/key_hash.c:27-179) on gfx950.
+//
+// kv_crc_c(p, sz, seed) is the SSE4.2 crc32 instruction chain started at
+// `seed` with no pre/post inversion (key_hash.c:53-63): 8-byte steps, then
+// 4/2/1-byte steps.  CRC is byte-serial, so the chunking does not change
+// the value: it is the reflected Castagnoli CRC (polynomial 0x82F63B78) of
+// the bytes, register initialised to seed, no final xor.
+//
+// Device form: slice-by-4.  Per 4 input bytes w, x = r ^ w and
+//   r' = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3]
+// with T_k[v] = CRC of byte v followed by k zero bytes.  A tail of n < 4
+// bytes is the same step on the zero-extended bytes with tables
+// T_{n-1} .. T_0 and r shifted right by 8n.  The four tables sit in LDS
+// replicated 32 times, lane l reading copy l & 31 (the layout of the Meow
+// T-tables, meow_dev.hpp LdsTab<4>): conflict-free random lookups, one
+// v_perm_b32 per lookup address.  One LDS lookup per key byte; a 16-byte
+// key moves 20 bytes of HBM, so short keys are HBM-bound.
+//
+//   k_crc_fixed   n keys of key_len bytes at stride key_len
+//   k_crc_var     n keys by u64 offsets (lane per key)
+// Both take an optional per-key seed array (kv_crc_c_array semantics:
+// seed[i] in, crc out) and otherwise one seed for all keys.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <algorithm>
+#include <mutex>
+#include <vector>
+#include "kvh_internal.hpp"
+#include "../../include/kvh.h"
+
+using namespace kvh;
+using namespace kvh::rt;
+
+namespace {
+
+constexpr uint32_t kPoly = 0x82F63B78u;  // reflected Castagnoli
+
+struct CrcTabs {
+  uint32_t t[4][256];
+};
+
+constexpr CrcTabs make_crc_tabs() {
+  CrcTabs c{};
+  for (uint32_t v = 0; v < 256; v++) {
+    uint32_t r = v;
+    for (int b = 0; b < 8; b++) r = (r >> 1) ^ ((r & 1u) ? kPoly : 0u);
+    c.t[0][v] = r;
+  }
+  for (int k = 1; k < 4; k++)
+    for (uint32_t v = 0; v < 256; v++) c.t[k][v] = (c.t[k - 1][v] >> 8) ^ c.t[0][c.t[k - 1][v] & 255u];
+  return c;
+}
+constexpr CrcTabs kCrc = make_crc_tabs();
+static_assert(kCrc.t[0][1] == 0xF26B8303u, "CRC32C table");  // standard Castagnoli table entry
+
+__constant__ CrcTabs c_crc = kCrc;
+
+constexpr int kBlock = 1024;
+constexpr int kWords = 4 * 8192;  // 4 tables x 256 entries x 32 copies
+
+// LDS slot s holds table T_{3-s}, so slot s is indexed by byte s of x.
+// Byte address of (slot s, value v, lane copy c):
+//   (s >> 1) << 16 | v << 8 | (s & 1) << 7 | c << 2
+__device__ __forceinline__ void fill_crc(uint32_t* lds) {
+  for (uint32_t i = threadIdx.x; i < (uint32_t)kWords; i += blockDim.x) {
+    const uint32_t s = (((i >> 14) & 1u) << 1) | ((i >> 5) & 1u);
+    const uint32_t v = (i >> 6) & 255u;
+    lds[i] = c_crc.t[3 - s][v];
+  }
+}
+
+struct CrcLds {
+  const uint32_t* lds;
+  uint32_t lw[4];
+  __device__ __forceinline__ explicit CrcLds(const uint32_t* p) : lds(p) {
+    const uint32_t lane = (threadIdx.x & 31u) << 2;
+#pragma unroll
+    for (int s = 0; s < 4; s++) lw[s] = ((uint32_t)(s >> 1) << 16) | ((uint32_t)(s & 1) << 7) | lane;
+  }
+  __device__ __forceinline__ uint32_t ld(uint32_t a) const { return *(const uint32_t*)((const char*)lds + a); }
+  template <int K> static constexpr uint32_t sel() { return 0x03020000u | ((4u + K) << 8); }
+  // four bytes: r' = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3]
+  __device__ __forceinline__ uint32_t word(uint32_t r, uint32_t w) const {
+    const uint32_t x = r ^ w;
+    const uint32_t a = ld(__builtin_amdgcn_perm(x, lw[0], sel<0>()));
+    const uint32_t b = ld(__builtin_amdgcn_perm(x, lw[1], sel<1>()));
+    const uint32_t c = ld(__builtin_amdgcn_perm(x, lw[2], sel<2>()));
+    const uint32_t d = ld(__builtin_amdgcn_perm(x, lw[3], sel<3>()));
+    return xor3(a, b, c) ^ d;
+  }
+  // n in 1..3 bytes (zero-extended in w): tables T_{n-1}..T_0 = slots 4-n..3
+  __device__ __forceinline__ uint32_t tail(uint32_t r, uint32_t w, uint32_t n) const {
+    const uint32_t x = r ^ w;
+    uint32_t o = r >> (8 * n);
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t s = 4 - n + i;
+      const uint32_t a = ((s >> 1) << 16) | (((x >> (8 * i)) & 255u) << 8) | ((s & 1) << 7) | ((threadIdx.x & 31u) << 2);
+      o ^= ld(a);
+    }
+    return o;
+  }
+};
+
+// kv_crc_c over one key of len bytes; 16-byte pieces through the
+// dword-aligned loaders (no over-read past the key).
+__device__ __forceinline__ uint32_t crc_key(const uint8_t* p, uint64_t len, uint32_t r, const CrcLds& T) {
+  uint64_t o = 0;
+  for (; o + 16 <= len; o += 16) {
+    const Blk b = load16_full(p + o);
+    r = T.word(r, b.w[0]);
+    r = T.word(r, b.w[1]);
+    r = T.word(r, b.w[2]);
+    r = T.word(r, b.w[3]);
+  }
+  const uint32_t t = (uint32_t)(len - o);
+  if (t) {
+    const Blk b = load_bytes(p + o, t);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int left = (int)t - 4 * c;
+      if (left >= 4) r = T.word(r, b.w[c]);
+      else if (left > 0) r = T.tail(r, b.w[c], (uint32_t)left);
+    }
+  }
+  return r;
+}
+
+template <int U>
+__global__ void __launch_bounds__(kBlock)
+k_crc_fixed(const uint8_t* __restrict__ keys, uint32_t L, uint64_t n, const uint32_t* __restrict__ seeds,
+            uint32_t seed, uint32_t* __restrict__ out) {
+  __shared__ uint32_t lds[kWords];
+  fill_crc(lds);
+  __syncthreads();
+  const CrcLds T(lds);
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  for (uint64_t b = wave * 64 * U; b < n; b += step) {
+    uint32_t r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = std::min<uint64_t>(b + 64 * u + lane, n - 1);
+      r[u] = crc_key(keys + j * L, L, seeds ? seeds[j] : seed, T);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      if (j < n) __builtin_nontemporal_store(r[u], out + j);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_crc_var(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
+          const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out (in/out seeds)
+  __shared__ uint32_t lds[kWords];
+  fill_crc(lds);
+  __syncthreads();
+  const CrcLds T(lds);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += stride) {
+    const uint64_t a = offs[j], e = offs[j + 1];
+    out[j] = crc_key(keys + a, e - a, seeds ? seeds[j] : seed, T);
+  }
+}
+
+uint32_t grid_crc(uint64_t n, int cus) {
+  const uint64_t need = (n + kBlock - 1) / kBlock;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)cus));
+}
+
+// synchronous host drop-ins: stage keys + offsets + seeds, run k_crc_var
+struct CrcStage {
+  std::mutex mu;
+  uint8_t* dev = nullptr;
+  size_t cap = 0;
+  int device = -1;
+};
+CrcStage g_cs;
+
+size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+int crc_host(const void* const* ptrs, const size_t* lens, size_t n, uint32_t* seeds_io) {
+  if (n == 0) return set_err(0);
+  size_t kb = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (lens[i] && !ptrs[i]) return set_err(KVH_EINVAL);
+    kb += lens[i];
+  }
+  const size_t off_offs = al16(kb), off_seed = off_offs + al16(8 * (n + 1)), total = off_seed + al16(4 * n);
+  std::vector<uint8_t> host(total);
+  uint64_t* offs = (uint64_t*)(host.data() + off_offs);
+  size_t o = 0;
+  for (size_t i = 0; i < n; i++) {
+    offs[i] = o;
+    if (lens[i]) memcpy(host.data() + o, ptrs[i], lens[i]);
+    o += lens[i];
+  }
+  offs[n] = o;
+  memcpy(host.data() + off_seed, seeds_io, 4 * n);
+  std::lock_guard<std::mutex> g(g_cs.mu);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  if (!g_cs.dev || g_cs.device != dev || g_cs.cap < total) {
+    if (g_cs.dev) {
+      int cur = dev;
+      (void)hipSetDevice(g_cs.device);
+      (void)hipFree(g_cs.dev);
+      (void)hipSetDevice(cur);
+      g_cs.dev = nullptr;
+      g_cs.cap = 0;
+    }
+    e = hipMalloc(&g_cs.dev, std::max<size_t>(total, 1 << 20));
+    if (e != hipSuccess) { g_cs.dev = nullptr; return hip_err(e); }
+    g_cs.cap = std::max<size_t>(total, 1 << 20);
+    g_cs.device = dev;
+  }
+  uint8_t* d = g_cs.dev;
+  e = hipMemcpy(d, host.data(), total, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_err(e);
+  uint32_t* dseed = (uint32_t*)(d + off_seed);
+  hipLaunchKernelGGL(k_crc_var, dim3(1), dim3(kBlock), 0, 0, d, (const uint64_t*)(d + off_offs), (uint64_t)n,
+                     dseed, 0u, dseed);
+  int rc = launch_done();
+  if (rc) return rc;
+  e = hipMemcpy(seeds_io, dseed, 4 * n, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_err(e);
+  return set_err(0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kvh_crc_c_fixed(const void* keys, uint32_t key_len, size_t n, const uint32_t* seeds, uint32_t seed,
+                    uint32_t* out, void* stream) {
+  if (n == 0) return set_err(0);
+  if (!out || (key_len && !keys)) return set_err(KVH_EINVAL);
+  int cus = 0, rc = device_cus(&cus);
+  if (rc) return rc;
+  hipLaunchKernelGGL((k_crc_fixed<2>), dim3(grid_crc((n + 1) / 2, cus)), dim3(kBlock), 0, (hipStream_t)stream,
+                     (const uint8_t*)keys, key_len, (uint64_t)n, seeds, seed, out);
+  return launch_done();
+}
+
+int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uint32_t* seeds, uint32_t seed,
+                  uint32_t* out, void* stream) {
+  if (n == 0) return set_err(0);
+  if (!out || !offsets || !keys) return set_err(KVH_EINVAL);
+  int cus = 0, rc = device_cus(&cus);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_crc_var, dim3(grid_crc(n, cus)), dim3(kBlock), 0, (hipStream_t)stream,
+                     (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  return launch_done();
+}
+
+uint32_t kvh_crc_c(const void* p, size_t sz, uint32_t seed) {
+  uint32_t s = seed;
+  const void* ptrs[1] = {p};
+  if (crc_host(ptrs, &sz, 1, &s) != 0) return 0;
+  return s;
+}
+
+uint32_t kvh_hash_uint(uint32_t i) { return kvh_crc_c(&i, 4, 0); }
+uint32_t kvh_hash_uint2(uint32_t r, uint32_t i) { return kvh_crc_c(&i, 4, r); }
+
+int kvh_crc_c_2_diff(const void* p, size_t sz, uint32_t* seed, const void* p2, size_t sz2, uint32_t* seed2) {
+  if (!seed || !seed2) return set_err(KVH_EINVAL);
+  const void* ptrs[2] = {p, p2};
+  const size_t lens[2] = {sz, sz2};
+  uint32_t s[2] = {*seed, *seed2};
+  const int rc = crc_host(ptrs, lens, 2, s);
+  if (rc == 0) { *seed = s[0]; *seed2 = s[1]; }
+  return rc;
+}
+
+int kvh_crc_c_4_diff(const void* p, size_t sz, uint32_t* seed, const void* p2, size_t sz2, uint32_t* seed2,
+                     const void* p3, size_t sz3, uint32_t* seed3, const void* p4, size_t sz4, uint32_t* seed4) {
+  if (!seed || !seed2 || !seed3 || !seed4) return set_err(KVH_EINVAL);
+  const void* ptrs[4] = {p, p2, p3, p4};
+  const size_t lens[4] = {sz, sz2, sz3, sz4};
+  uint32_t s[4] = {*seed, *seed2, *seed3, *seed4};
+  const int rc = crc_host(ptrs, lens, 4, s);
+  if (rc == 0) { *seed = s[0]; *seed2 = s[1]; *seed3 = s[2]; *seed4 = s[3]; }
+  return rc;
+}
+
+int kvh_crc_c_array(const void** p, size_t* psz, uint32_t* seed, size_t count) {
+  if (count && (!p || !psz || !seed)) return set_err(KVH_EINVAL);
+  return crc_host(p, psz, count, seed);
+}
+
+int kvh_crc_c_key_array(const void* p, size_t* psz, uint32_t* seed, size_t count) {
+  if (count && (!psz || !seed)) return set_err(KVH_EINVAL);
+  std::vector<const void*> ptrs(count, p);
+  return crc_host(ptrs.data(), psz, count, seed);
+}
+
+}  // extern "C"

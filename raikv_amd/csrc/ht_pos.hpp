@@ -103,7 +103,7 @@ __device__ __forceinline__ void cuckoo_positions_loop(const HtGeom& g, uint64_t 
 }
 
 // Straight-line common case: alt1 = h2 and every alternate's first
-// xoroshiro candidate clear of the earlier slots (all but ~1 key in 1000
+// xoroshiro candidate clear of the earlier slots (all but ~1 key in 1400
 // for A = 4).  Lanes where any candidate clashes redo the key through the
 // loop form; both forms produce the reference's slots.
 template <int A, typename W>

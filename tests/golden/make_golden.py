@@ -8,7 +8,7 @@ reference's own functions (kv_hash_meow128 and its batched / streaming /
 vec variants, key_hash.c:1413-2020); the inputs are our own seeded random
 data.  The fixtures are data only (inputs + expected outputs).
 
-    python tests/golden/make_golden.py [--only-cuckoo]
+    python tests/golden/make_golden.py [--only-cuckoo | --only-crc]
 
 The table-position fixtures (cuckoo_*.npz) come from the reference's
 ht_init.cpp + ht_cuckoo.cpp compiled where they lie into
@@ -264,7 +264,58 @@ def make_cuckoo():
         print(name, "ht_size", int(geom[3]), "pos[0]", pos[:a])
 
 
+def make_crc():
+    """kv_crc_c family (key_hash.c:27-179) outputs of the reference itself."""
+    lib = load_ref()
+    S = C.c_size_t
+    lib.kv_crc_c.argtypes = [P, S, C.c_uint32]
+    lib.kv_crc_c.restype = C.c_uint32
+    lib.kv_hash_uint.argtypes = [C.c_uint32]
+    lib.kv_hash_uint.restype = C.c_uint32
+    lib.kv_hash_uint2.argtypes = [C.c_uint32, C.c_uint32]
+    lib.kv_hash_uint2.restype = C.c_uint32
+    lib.kv_crc_c_array.argtypes = [P, P, P, S]
+    lib.kv_crc_c_key_array.argtypes = [P, P, P, S]
+    rng = np.random.default_rng(20261016)
+    # every length 0..300 x 3 seeds, one random buffer per length
+    maxl = 300
+    keys = rng.integers(0, 256, size=(maxl + 1, maxl), dtype=np.uint8)
+    seeds = np.array([0, 0xFFFFFFFF, 0x9E3779B9], dtype=np.uint32)
+    lens = np.zeros((maxl + 1, len(seeds)), dtype=np.uint32)
+    for L in range(maxl + 1):
+        b = np.ascontiguousarray(keys[L, :L])
+        buf = C.create_string_buffer(b.tobytes(), max(1, L))
+        for si, sd in enumerate(seeds):
+            lens[L, si] = lib.kv_crc_c(buf, L, int(sd))
+    # zipf variable-length batch with per-key seeds through kv_crc_c_array
+    kb, offs, ln = var_keys(3000, 1, 256, seed=91)
+    n = len(ln)
+    ps = (P * n)(*[kb.ctypes.data + int(offs[i]) for i in range(n)])
+    psz = (C.c_size_t * n)(*[int(x) for x in ln])
+    sd = rng.integers(0, 2 ** 32, n, dtype=np.uint32)
+    arr = sd.copy()
+    lib.kv_crc_c_array(ps, psz, arr.ctypes.data, n)
+    # kv_crc_c_key_array: prefixes of one 200-byte buffer
+    one = rng.integers(0, 256, 200, dtype=np.uint8)
+    pl = np.array([0, 1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 32, 33, 63, 64, 65, 100, 199, 200], dtype=np.uint64)
+    pseed = rng.integers(0, 2 ** 32, len(pl), dtype=np.uint32)
+    pout = pseed.copy()
+    psz2 = (C.c_size_t * len(pl))(*[int(x) for x in pl])
+    lib.kv_crc_c_key_array(one.ctypes.data, psz2, pout.ctypes.data, len(pl))
+    ui = rng.integers(0, 2 ** 32, 64, dtype=np.uint32)
+    uo = np.array([lib.kv_hash_uint(int(x)) for x in ui], dtype=np.uint32)
+    uo2 = np.array([lib.kv_hash_uint2(int(x), int(y)) for x, y in zip(ui, ui[::-1])], dtype=np.uint32)
+    np.savez_compressed(os.path.join(HERE, "crc32c.npz"), len_keys=keys, len_seeds=seeds, len_out=lens,
+                        var_keys=kb, var_offsets=offs, var_seeds=sd, var_out=arr,
+                        prefix_buf=one, prefix_lens=pl, prefix_seeds=pseed, prefix_out=pout,
+                        uint_in=ui, uint_out=uo, uint2_out=uo2)
+    print("crc32c fixtures: len", lens.shape, "var", n)
+
+
 if __name__ == "__main__":
-    if "--only-cuckoo" not in sys.argv:
+    if "--only-cuckoo" not in sys.argv and "--only-crc" not in sys.argv:
         main()
-    make_cuckoo()
+    if "--only-crc" not in sys.argv:
+        make_cuckoo()
+    if "--only-cuckoo" not in sys.argv:
+        make_crc()

@@ -138,3 +138,41 @@ def load_ref_ht():
                                      C.c_int]
     lib.ref_cuckoo_bench.restype = C.c_double
     return lib
+
+
+# ------------------------------------------------------------ CRC32C (§8 f4)
+def crc_sigs(lib):
+    lib.orc_crc_c.argtypes = [P, SZ, C.c_uint32]
+    lib.orc_crc_c.restype = C.c_uint32
+    lib.orc_hash_uint2.argtypes = [C.c_uint32, C.c_uint32]
+    lib.orc_hash_uint2.restype = C.c_uint32
+    lib.orc_crc_batch_var.argtypes = [P, P, SZ, P, C.c_uint32, P]
+    lib.orc_crc_batch_fixed.argtypes = [P, SZ, SZ, P, C.c_uint32, P]
+    return lib
+
+
+def orc_crc(lib, data: bytes, seed: int) -> int:
+    crc_sigs(lib)
+    buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+    return int(lib.orc_crc_c(buf, len(data), seed))
+
+
+def orc_crc_var(lib, keys: np.ndarray, offs: np.ndarray, seeds=None, seed: int = 0) -> np.ndarray:
+    crc_sigs(lib)
+    n = offs.size - 1
+    out = np.zeros(n, dtype=np.uint32)
+    kb = keys if keys.size else np.zeros(1, np.uint8)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    lib.orc_crc_batch_var(kb.ctypes.data, np.ascontiguousarray(offs, dtype=np.uint64).ctypes.data, n,
+                          None if sd is None else sd.ctypes.data, seed, out.ctypes.data)
+    return out
+
+
+def orc_crc_fixed(lib, keys: np.ndarray, key_len: int, seeds=None, seed: int = 0) -> np.ndarray:
+    crc_sigs(lib)
+    n = keys.size // key_len if key_len else 0
+    out = np.zeros(n, dtype=np.uint32)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, dtype=np.uint32)
+    lib.orc_crc_batch_fixed(keys.ctypes.data, key_len, n, None if sd is None else sd.ctypes.data, seed,
+                            out.ctypes.data)
+    return out

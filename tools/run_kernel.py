@@ -29,10 +29,21 @@ torch.cuda.set_device(0)
 g = torch.Generator(device="cuda")
 g.manual_seed(1)
 cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1),
-       "f1": (100_000_000, 16, -1), "f1p": (100_000_000, 16, -2)}
+       "f1": (100_000_000, 16, -1), "f1p": (100_000_000, 16, -2), "f4": (100_000_000, 16, -4),
+       "f4v": (100_000_000, 0, -4)}
 n, L, ar = cfg[a.config]
 n = a.n or n
-if ar < 0:  # table positions, geometry as bench.py F1_GEOM
+if ar == -4:  # CRC32C
+    co = torch.empty((n,), dtype=torch.int32, device="cuda")
+    if L == 0:
+        offs = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=3))
+        keys = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device="cuda", generator=g)
+        doff = torch.from_numpy(offs.view(np.int64)).cuda()
+        f = lambda: kvh.crc_c_var(keys, doff, 0, out=co)
+    else:
+        keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+        f = lambda: kvh.crc_c_fixed(keys, L, 0, out=co)
+elif ar < 0:  # table positions, geometry as bench.py F1_GEOM
     geom = kvh.HtGeom.from_map(64 << 30, 64, 1.0, 4, 4)
     keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
     hh = torch.empty((n, 2), dtype=torch.int64, device="cuda")
