@@ -127,6 +127,55 @@ __device__ __forceinline__ uint32_t crc_key(const uint8_t* p, uint64_t len, uint
   return r;
 }
 
+// Compile-time length: every piece of the U keys of a chunk is loaded
+// before the first table step (U*ceil(L/16) 16-byte loads per lane in
+// flight), then the slice-by-4 chains run.
+template <int L, int U>
+__global__ void __launch_bounds__(kBlock)
+k_crc_fixed_ct(const uint8_t* __restrict__ keys, uint64_t n, const uint32_t* __restrict__ seeds, uint32_t seed,
+               uint32_t* __restrict__ out) {
+  constexpr int NP = (L + 15) / 16;
+  __shared__ uint32_t lds[kWords];
+  fill_crc(lds);
+  __syncthreads();
+  const CrcLds T(lds);
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  for (uint64_t b = wave * 64 * U; b < n; b += step) {
+    Blk D[U][NP];
+    uint32_t r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = std::min<uint64_t>(b + 64 * u + lane, n - 1);
+      const uint8_t* p = keys + j * L;
+#pragma unroll
+      for (int c = 0; c < NP; c++) {
+        D[u][c] = (16 * c + 16 <= L) ? load16_full(p + 16 * c) : load_bytes(p + 16 * c, L - 16 * c);
+      }
+      r[u] = seeds ? seeds[j] : seed;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int c = 0; c < NP; c++) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          const int left = L - 16 * c - 4 * w;
+          if (left >= 4) r[u] = T.word(r[u], D[u][c].w[w]);
+          else if (left > 0) r[u] = T.tail(r[u], D[u][c].w[w], (uint32_t)left);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      if (j < n) __builtin_nontemporal_store(r[u], out + j);
+    }
+  }
+}
+
 template <int U>
 __global__ void __launch_bounds__(kBlock)
 k_crc_fixed(const uint8_t* __restrict__ keys, uint32_t L, uint64_t n, const uint32_t* __restrict__ seeds,
@@ -242,8 +291,22 @@ int kvh_crc_c_fixed(const void* keys, uint32_t key_len, size_t n, const uint32_t
   if (!out || (key_len && !keys)) return set_err(KVH_EINVAL);
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
-  hipLaunchKernelGGL((k_crc_fixed<2>), dim3(grid_crc((n + 1) / 2, cus)), dim3(kBlock), 0, (hipStream_t)stream,
-                     (const uint8_t*)keys, key_len, (uint64_t)n, seeds, seed, out);
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t* k = (const uint8_t*)keys;
+  switch (key_len) {
+#define KVH_CRC_L(Lv, Uv)                                                                                   \
+  case Lv:                                                                                                  \
+    hipLaunchKernelGGL((k_crc_fixed_ct<Lv, Uv>), dim3(grid_crc((n + Uv - 1) / Uv, cus)), dim3(kBlock), 0, st, k, \
+                       (uint64_t)n, seeds, seed, out);                                                       \
+    return launch_done();
+    KVH_CRC_L(4, 8) KVH_CRC_L(8, 8) KVH_CRC_L(12, 8) KVH_CRC_L(16, 8) KVH_CRC_L(24, 4) KVH_CRC_L(32, 4)
+    KVH_CRC_L(48, 2) KVH_CRC_L(64, 2)
+#undef KVH_CRC_L
+    default:
+      break;
+  }
+  hipLaunchKernelGGL((k_crc_fixed<2>), dim3(grid_crc((n + 1) / 2, cus)), dim3(kBlock), 0, st, k, key_len,
+                     (uint64_t)n, seeds, seed, out);
   return launch_done();
 }
 
