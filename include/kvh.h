@@ -234,6 +234,42 @@ int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
                                 void *pos, uint32_t flags, void *stream);
 
 /* ---------------------------------------------------------------------
+ * Key ingest: the key formats raikv produces, hashed on
+ * the device without host repacking.
+ * ------------------------------------------------------------------- */
+#define KVH_NULTERM   0x4u  /* hash span + one 0 byte (kv_set_key_frag_string, key_ctx.cpp:1764-1772) */
+
+/* Whitespace tokenizer of test/ctest.c:202-233: tokens are maximal runs of
+ * bytes other than ' ', '\n', '\t' in text[0, nbytes) (device buffer);
+ * a token of i bytes is kept when i < max_token (MAX_TOKEN_SIZE 256,
+ * ctest.c:23).  Writes the first min(count, cap) kept tokens' byte offsets
+ * and lengths in text order and the kept count to *count (all device
+ * memory).  scratch: device buffer of kvh_tokenize_scratch_bytes(nbytes). */
+size_t kvh_tokenize_scratch_bytes(size_t nbytes);
+int kvh_tokenize(const void *text, size_t nbytes, uint32_t max_token,
+                 uint64_t *tok_offs, uint32_t *tok_lens, size_t cap,
+                 uint64_t *count, void *scratch, size_t scratch_bytes,
+                 void *stream);
+
+/* Meow128 of n keys given as (offset, length) spans into buf (device).
+ * With KVH_NULTERM the hashed key is the span followed by one 0 byte that
+ * need not be in buf: a token becomes the kv_key_frag_t "token\0" of
+ * ctest.c:223 (keylen = len + 1).  KVH_FIXUP as elsewhere; with the
+ * table's db-0 seed this is kv_hash_key_frag (key_ctx.cpp:1774-1783). */
+int kvh_meow128_spans(const void *buf, const uint64_t *offs,
+                      const uint32_t *lens, size_t n, uint64_t seed1,
+                      uint64_t seed2, uint64_t *out, uint32_t flags,
+                      void *stream);
+
+/* Meow128 of n packed kv_key_frag_t records {u16 keylen, keylen bytes,
+ * pad to 2} (hash_entry.h:28-36, kv_make_key_frag key_ctx.cpp:1737-1745):
+ * rec_offs[i] is the byte offset of record i in buf (ctest.c's xh[].frag
+ * pointers relative to its buffer).  Same result as kv_hash_key_frag. */
+int kvh_meow128_frags(const void *buf, const uint64_t *rec_offs, size_t n,
+                      uint64_t seed1, uint64_t seed2, uint64_t *out,
+                      uint32_t flags, void *stream);
+
+/* ---------------------------------------------------------------------
  * CRC32C: raikv's kv_crc_c family (key_hash.c:27-179),
  * the SSE4.2 crc32 chain from `seed`, no pre/post inversion.
  * ------------------------------------------------------------------- */

@@ -133,3 +133,51 @@ extern "C" double ref_cuckoo_bench(uint64_t ht_size, uint64_t mask, uint64_t fra
   ::free(ht);
   return (double) (t1.tv_sec - t0.tv_sec) + 1e-9 * (double) (t1.tv_nsec - t0.tv_nsec);
 }
+
+/* f3 golden vectors: ctest.c's ingest (ctest.c:202-233) through the
+ * reference's own key-fragment functions.  Tokens (maximal runs of bytes
+ * other than ' ', '\n', '\t', kept when shorter than max_token) are packed
+ * with kv_make_key_frag + kv_set_key_frag_string (key_ctx.cpp:1737-1772)
+ * into `frag_buf` (record offsets -> rec_offs) and hashed with
+ * kv_hash_key_frag (key_ctx.cpp:1774-1783) against a malloc'd HashTab whose
+ * db-0 seed is returned in seed_out.  Returns the token count or -1. */
+extern "C" long ref_ctest_frags(const char *text, size_t n, uint32_t max_token, uint8_t *frag_buf, size_t frag_cap,
+                                uint64_t *rec_offs, uint64_t *hashes, size_t max_tok, uint64_t *seed_out) {
+  HashTabGeom g;
+  memset(&g, 0, sizeof(g));
+  g.map_size = 8 << 20;
+  g.hash_entry_size = 64;
+  g.hash_value_ratio = 1.0f;
+  g.cuckoo_buckets = 4;
+  g.cuckoo_arity = 2;
+  HashTab *ht = HashTab::alloc_map(g);
+  if (ht == NULL) return -1;
+  HashSeed hs;
+  ht->hdr.get_hash_seed(0, hs);
+  seed_out[0] = hs.hash1;
+  seed_out[1] = hs.hash2;
+  uint8_t *in = frag_buf, *end = frag_buf + frag_cap;
+  long cnt = 0;
+  size_t i = 0;
+  for (size_t p = 0;; p++) {
+    const bool tok = p < n && !(text[p] == ' ' || text[p] == '\n' || text[p] == '\t');
+    if (tok) {
+      i++;
+      continue;
+    }
+    if (i > 0 && i < max_token) {
+      void *out = NULL;
+      kv_key_frag_t *frag = kv_make_key_frag((uint16_t)(i + 1), (size_t)(end - in), in, &out);
+      if (frag == NULL || (size_t)cnt >= max_tok) { ::free(ht); return -1; }
+      kv_set_key_frag_string(frag, &text[p - i], (uint16_t)i);
+      rec_offs[cnt] = (uint64_t)((uint8_t *)frag - frag_buf);
+      kv_hash_key_frag((kv_hash_tab_t *)ht, frag, &hashes[2 * cnt], &hashes[2 * cnt + 1]);
+      cnt++;
+      in = (uint8_t *)out;
+    }
+    i = 0;
+    if (p >= n) break;
+  }
+  ::free(ht);
+  return cnt;
+}

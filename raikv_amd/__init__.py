@@ -12,6 +12,10 @@ from .binding import (  # noqa: F401
     KVH_POS32,
     HtGeom,
     crc_c_fixed,
+    tokenize,
+    meow128_spans,
+    meow128_frags,
+    KVH_NULTERM,
     crc_c_var,
     kv_crc_c,
     ht_positions,
@@ -36,4 +40,5 @@ __all__ = [
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
     "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
+    "tokenize", "meow128_spans", "meow128_frags", "KVH_NULTERM",
 ]

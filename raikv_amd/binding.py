@@ -20,6 +20,7 @@ except Exception:  # pragma: no cover - torch is part of the image
 
 KVH_FIXUP = 0x1
 KVH_POS32 = 0x2
+KVH_NULTERM = 0x4
 KVH_MAX_ARITY = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -105,6 +106,10 @@ def _load():
         "kvh_crc_c_4_diff": (I, [P, SZ, P, P, SZ, P, P, SZ, P, P, SZ, P]),
         "kvh_crc_c_array": (I, [P, P, P, SZ]),
         "kvh_crc_c_key_array": (I, [P, P, P, SZ]),
+        "kvh_tokenize_scratch_bytes": (SZ, [SZ]),
+        "kvh_tokenize": (I, [P, SZ, U32, P, P, SZ, P, P, SZ, P]),
+        "kvh_meow128_spans": (I, [P, P, P, SZ, U64, U64, P, U32, P]),
+        "kvh_meow128_frags": (I, [P, P, SZ, U64, U64, P, U32, P]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
         "kvh_version": (C.c_char_p, []),
@@ -191,6 +196,47 @@ def meow128_fixed_positions(keys, key_len: int, seed: Tuple[int, int], geom: "Ht
                                           _dev_ptr(out) if n else None, KVH_POS32 if pos32 else 0,
                                           _stream_ptr(stream)), "kvh_meow128_fixed_positions")
     return hashes, out
+
+
+def tokenize(text, max_token: int = 256, cap: Optional[int] = None, stream=None):
+    """ctest.c:202-233 whitespace tokenizer on a uint8 device tensor ->
+    (offsets int64 [k], lengths int32 [k]) of the kept tokens in order."""
+    n = text.numel()
+    cnt = torch.zeros((1,), dtype=torch.int64, device=text.device)
+    scratch = torch.empty((max(1, lib.kvh_tokenize_scratch_bytes(n) // 8),), dtype=torch.int64, device=text.device)
+    if cap is None:
+        cap = n // 2 + 1
+    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=text.device)
+    lens = torch.empty((max(cap, 1),), dtype=torch.int32, device=text.device)
+    check(lib.kvh_tokenize(_dev_ptr(text) if n else None, n, max_token, _dev_ptr(offs), _dev_ptr(lens), cap,
+                           _dev_ptr(cnt), _dev_ptr(scratch), scratch.numel() * 8, _stream_ptr(stream)), "kvh_tokenize")
+    k = int(cnt.item())
+    return offs[:min(k, cap)], lens[:min(k, cap)]
+
+
+def meow128_spans(buf, offs, lens, seed: Tuple[int, int], out=None, fixup: bool = True, nulterm: bool = True,
+                  stream=None):
+    """Meow128 of (offset, length) spans of a device buffer; nulterm hashes
+    each span + one 0 byte (the kv_key_frag_t of a token)."""
+    n = offs.numel()
+    if out is None:
+        out = _new_out((n, 2), offs)
+    check(lib.kvh_meow128_spans(_dev_ptr(buf), _dev_ptr(offs) if n else None, _dev_ptr(lens) if n else None, n,
+                                U64(seed[0] & (2**64 - 1)), U64(seed[1] & (2**64 - 1)), _dev_ptr(out) if n else None,
+                                (KVH_FIXUP if fixup else 0) | (KVH_NULTERM if nulterm else 0), _stream_ptr(stream)),
+          "kvh_meow128_spans")
+    return out
+
+
+def meow128_frags(buf, rec_offs, seed: Tuple[int, int], out=None, fixup: bool = True, stream=None):
+    """Meow128 of packed kv_key_frag_t records at byte offsets rec_offs."""
+    n = rec_offs.numel()
+    if out is None:
+        out = _new_out((n, 2), rec_offs)
+    check(lib.kvh_meow128_frags(_dev_ptr(buf), _dev_ptr(rec_offs) if n else None, n, U64(seed[0] & (2**64 - 1)),
+                                U64(seed[1] & (2**64 - 1)), _dev_ptr(out) if n else None,
+                                KVH_FIXUP if fixup else 0, _stream_ptr(stream)), "kvh_meow128_frags")
+    return out
 
 
 def crc_c_fixed(keys, key_len: int, seed: int = 0, seeds=None, out=None, stream=None):

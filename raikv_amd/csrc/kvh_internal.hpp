@@ -47,6 +47,35 @@ __device__ __forceinline__ void store_h(uint64_t* __restrict__ out, uint64_t idx
   if constexpr (NTM) __builtin_nontemporal_store(v, q); else *q = v;
 }
 
+constexpr int kLT = 64;   // full per-length constant records (L < 64)
+constexpr int kNF = 256;  // F-only records for 64 <= L < 64 + kNF
+
+// Per-length folding constants of a variable-length batch from LDS tables
+// (k_generic, k_keysrc): full records for L < kLT, first-absorb folds for
+// kLT <= L < kLT + kNF, in-lane folds beyond.
+template <class Tab>
+struct LdsK {
+  const MeowConst* full;   // [kLT]
+  const Blk* ftab;         // [kNF][4]
+  uint32_t L;
+  Blk m;
+  const Tab& T;
+  __device__ __forceinline__ LdsK(const MeowConst* f, const Blk* ft, uint32_t len, uint64_t s1,
+                                  uint64_t s2, const Tab& t)
+      : full(f), ftab(ft), L(len), m(mixer(s1, s2, len)), T(t) {}
+  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ Blk M() const { return m; }
+  __device__ __forceinline__ Blk F(int i) const {
+    if (L < (uint32_t)kLT) return full[L].F[i];
+    if (L < (uint32_t)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
+    return aesT(bxor(ramp(i), m), T);
+  }
+  __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
+  __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
+  __device__ __forceinline__ Blk CS2b() const { return full[li()].CS2b; }
+  __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
+};
+
 namespace rt {
 // thread-local last error (kvh_last_error); returns e
 int set_err(int e);

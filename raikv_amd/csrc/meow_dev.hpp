@@ -323,6 +323,22 @@ struct LdsLd {
   }
 };
 
+// Bytes at or past `end` read as zero: a key whose hashed length runs one
+// byte past its stored bytes (a token hashed with the NUL that
+// kv_set_key_frag_string appends, key_ctx.cpp:1764-1772) never reads the
+// separator that follows it in the buffer.
+struct MaskLd {
+  const uint8_t* end;
+  __device__ __forceinline__ Blk full(const uint8_t* p) const {
+    if (p + 16 <= end) return load16_full(p);
+    return p < end ? load_bytes(p, (uint32_t)(end - p)) : bzero();
+  }
+  __device__ __forceinline__ Blk part(const uint8_t* p, uint32_t n) const {
+    const uint32_t m = p + n <= end ? n : (p < end ? (uint32_t)(end - p) : 0u);
+    return m ? load_bytes(p, m) : bzero();
+  }
+};
+
 // Source of per-length constants for the runtime path.
 struct ConstRef {
   const MeowConst* k;
@@ -332,18 +348,19 @@ struct ConstRef {
 // wave-uniform when every lane has the same length (generic fixed-length
 // kernel) and lane-divergent (masked) for variable-length batches.
 template <class Tab, class KGet, class Ld = GlobalLd>
-__device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet& K, const Tab& T) {
+__device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet& K, const Tab& T,
+                                       const Ld& ld = Ld{}) {
   const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
   Blk S0, S1, S2, S3;
   if (nb > 0) {
-    Blk k0 = Ld::full(p), k1 = Ld::full(p + 16), k2 = Ld::full(p + 32),
-        k3 = Ld::full(p + 48);
+    Blk k0 = ld.full(p), k1 = ld.full(p + 16), k2 = ld.full(p + 32),
+        k3 = ld.full(p + 48);
     S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
     S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
     for (uint32_t b = 1; b < nb; b++) {
       const uint8_t* q = p + 64 * b;
-      k0 = Ld::full(q); k1 = Ld::full(q + 16);
-      k2 = Ld::full(q + 32); k3 = Ld::full(q + 48);
+      k0 = ld.full(q); k1 = ld.full(q + 16);
+      k2 = ld.full(q + 32); k3 = ld.full(q + 48);
       S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
       S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
     }
@@ -352,19 +369,19 @@ __device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet&
   const uint8_t* q = p + 64 * nb;
   // trail (key_hash.c:1200-1210); a state's first absorb is folded
   if (t) {
-    const Blk k = Ld::part(q + C, t);
+    const Blk k = ld.part(q + C, t);
     S3 = first ? aesdec(bxor(K.F(3), k), k, T) : aesdec(aesdec(S3, k, T), k, T);
   }
   if (C >= 48) {
-    const Blk k = Ld::full(q + 32);
+    const Blk k = ld.full(q + 32);
     S2 = first ? aesdec(bxor(K.F(2), k), k, T) : aesdec(aesdec(S2, k, T), k, T);
   }
   if (C >= 32) {
-    const Blk k = Ld::full(q + 16);
+    const Blk k = ld.full(q + 16);
     S1 = first ? aesdec(bxor(K.F(1), k), k, T) : aesdec(aesdec(S1, k, T), k, T);
   }
   if (C >= 16) {
-    const Blk k = Ld::full(q);
+    const Blk k = ld.full(q);
     S0 = first ? aesdec(bxor(K.F(0), k), k, T) : aesdec(aesdec(S0, k, T), k, T);
   }
   const bool T0 = !first || C >= 16, T1 = !first || C >= 32, T2 = !first || C >= 48,

@@ -8,7 +8,7 @@ reference's own functions (kv_hash_meow128 and its batched / streaming /
 vec variants, key_hash.c:1413-2020); the inputs are our own seeded random
 data.  The fixtures are data only (inputs + expected outputs).
 
-    python tests/golden/make_golden.py [--only-cuckoo | --only-crc]
+    python tests/golden/make_golden.py [--only-cuckoo | --only-crc | --only-ingest]
 
 The table-position fixtures (cuckoo_*.npz) come from the reference's
 ht_init.cpp + ht_cuckoo.cpp compiled where they lie into
@@ -312,10 +312,54 @@ def make_crc():
     print("crc32c fixtures: len", lens.shape, "var", n)
 
 
+def make_ingest():
+    """ctest.c ingest: tokens -> kv_make_key_frag/kv_set_key_frag_string
+    records -> kv_hash_key_frag, all by the reference's own functions."""
+    ref = load_ref_ht()
+    ref.ref_ctest_frags.argtypes = [P, C.c_size_t, C.c_uint32, P, C.c_size_t, P, P, C.c_size_t, P]
+    ref.ref_ctest_frags.restype = C.c_long
+    rng = np.random.default_rng(20261017)
+    # words of zipf-ish lengths 1..300 (some >= 256: dropped), runs of 1-3
+    # separators from ' ', '\n', '\t', printable + high bytes, spanning
+    # several 64 KiB device chunks; starts and ends without a separator
+    parts = []
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789._-:/", dtype=np.uint8)
+    total = 0
+    while total < 300_000:
+        r = rng.random()
+        L = int(rng.integers(1, 12)) if r < 0.8 else (int(rng.integers(12, 255)) if r < 0.97 else int(rng.integers(255, 300)))
+        w = rng.choice(alpha, L)
+        if rng.random() < 0.05:
+            w[rng.integers(0, L)] = rng.integers(128, 256)
+        parts.append(w.astype(np.uint8))
+        sep = rng.choice(np.frombuffer(b" \n\t", dtype=np.uint8), int(rng.integers(1, 4)))
+        parts.append(sep.astype(np.uint8))
+        total += L + len(sep)
+    parts.append(np.frombuffer(b"last_token_no_separator", dtype=np.uint8))
+    text = np.concatenate(parts)
+    n = len(text)
+    tbuf = C.create_string_buffer(text.tobytes(), n + 2)
+    cap_tok = n // 2 + 1
+    frag = np.zeros(n * 2 + 64, dtype=np.uint8)
+    roffs = np.zeros(cap_tok, dtype=np.uint64)
+    hashes = np.zeros(2 * cap_tok, dtype=np.uint64)
+    seed = np.zeros(2, dtype=np.uint64)
+    cnt = ref.ref_ctest_frags(tbuf, n, 256, ptr(frag), frag.size, ptr(roffs), ptr(hashes), cap_tok, ptr(seed))
+    assert cnt > 0
+    used = int(roffs[cnt - 1]) + 2 + int(frag[int(roffs[cnt - 1])] | (frag[int(roffs[cnt - 1]) + 1] << 8))
+    used = (used + 1) & ~1
+    np.savez_compressed(os.path.join(HERE, "ingest.npz"), text=text, max_token=np.array([256], np.uint32),
+                        frags=frag[:used], rec_offs=roffs[:cnt], hashes=hashes[:2 * cnt].reshape(-1, 2), seed=seed)
+    print("ingest fixtures:", n, "bytes,", cnt, "tokens, seed", [hex(int(x)) for x in seed])
+
+
 if __name__ == "__main__":
-    if "--only-cuckoo" not in sys.argv and "--only-crc" not in sys.argv:
+    only = [a for a in sys.argv[1:] if a.startswith("--only-")]
+    if not only:
         main()
-    if "--only-crc" not in sys.argv:
+    if not only or "--only-cuckoo" in only:
         make_cuckoo()
-    if "--only-cuckoo" not in sys.argv:
+    if not only or "--only-crc" in only:
         make_crc()
+    if not only or "--only-ingest" in only:
+        make_ingest()

@@ -176,3 +176,34 @@ def orc_crc_fixed(lib, keys: np.ndarray, key_len: int, seeds=None, seed: int = 0
     lib.orc_crc_batch_fixed(keys.ctypes.data, key_len, n, None if sd is None else sd.ctypes.data, seed,
                             out.ctypes.data)
     return out
+
+
+# ------------------------------------------------------------ ingest (§8 f3)
+def ingest_sigs(lib):
+    lib.orc_tokenize.argtypes = [P, SZ, C.c_uint32, P, P, SZ]
+    lib.orc_tokenize.restype = SZ
+    lib.orc_hash_spans.argtypes = [P, P, P, SZ, U64, U64, C.c_int, C.c_int, P]
+    return lib
+
+
+def orc_tokenize(lib, text: np.ndarray, max_token: int = 256):
+    ingest_sigs(lib)
+    n = text.size
+    cap = n // 2 + 1
+    offs = np.zeros(cap, dtype=np.uint64)
+    lens = np.zeros(cap, dtype=np.uint32)
+    tb = text if n else np.zeros(1, np.uint8)
+    cnt = lib.orc_tokenize(tb.ctypes.data, n, max_token, offs.ctypes.data, lens.ctypes.data, cap)
+    return offs[:cnt], lens[:cnt]
+
+
+def orc_hash_spans(lib, buf: np.ndarray, offs, lens, seed, nul=True, fix=True) -> np.ndarray:
+    ingest_sigs(lib)
+    n = len(offs)
+    out = np.zeros((n, 2), dtype=np.uint64)
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    l = np.ascontiguousarray(lens, dtype=np.uint32)
+    bb = buf if buf.size else np.zeros(1, np.uint8)
+    lib.orc_hash_spans(bb.ctypes.data, o.ctypes.data, l.ctypes.data, n, U64(seed[0]), U64(seed[1]), int(nul),
+                       int(fix), out.ctypes.data)
+    return out
