@@ -6,7 +6,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-pass-failed
 INC      := -Iinclude
 
 LIB      := raikv_amd/libkvh.so
-SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/ht_pos.hip raikv_amd/csrc/crc32c.hip raikv_amd/csrc/ingest.hip
+SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/ht_pos.hip raikv_amd/csrc/crc32c.hip raikv_amd/csrc/ingest.hip raikv_amd/csrc/ht_sort.hip
 OBJS     := $(SRCS:.hip=.o)
 HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/csrc/kvh_internal.hpp \
             raikv_amd/csrc/ht_pos.hpp include/kvh.h include/raikv_amd/key_hash.hpp
@@ -19,8 +19,8 @@ all: $(LIB) oracle cpptests
 raikv_amd/csrc/%.o: raikv_amd/csrc/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c -o $@ $<
 
-$(LIB): $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJS)
+$(LIB): $(OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(OBJS)
 
 oracle:
 	$(MAKE) -C oracle

@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 METRIC = "128-bit key hashes/sec device-resident, 16–64B keys; GB/s vs HBM peak"
 METRIC_F1 = "keys/sec -> hash + cuckoo table positions, device-resident (SURVEY.md §8 f1)"
 METRIC_F4 = "CRC32C (kv_crc_c) keys/sec, device-resident (SURVEY.md §8 f4)"
+METRIC_F3 = "tokens/sec: text -> tokenize -> NUL-terminated key hashes, device-resident (SURVEY.md §8 f3)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 
 CONFIGS = {
@@ -58,6 +59,10 @@ CONFIGS = {
                n=100_000_000, key_len=16, arity=1, var=False, crc=True),
     "f4v": dict(workload="F4v: 100M zipf 8-256 B keys (C2 shape) -> kv_crc_c, u32 out",
                 n=100_000_000, key_len=0, arity=1, var=True, crc=True),
+    # ctest-style ingest of a text buffer
+    "f3": dict(workload="F3: 1 GiB whitespace-separated text (≈25% separators) -> device tokenizer (ctest.c) -> "
+                        "NUL-terminated key hashes with fixup (kv_hash_key_frag semantics)",
+               n=1 << 30, key_len=0, arity=1, var=False, ingest=True),
 }
 F1_GEOM = dict(map_size=64 << 30, hash_entry_size=64, hash_value_ratio=1.0, cuckoo_buckets=4, cuckoo_arity=4)
 
@@ -190,6 +195,38 @@ def cpu_baseline_crc(cfg, seconds: float):
                       f"kv_crc_c_array, {threads} threads (ctypes releases the GIL), {total_t:.1f} s"}
 
 
+def cpu_baseline_ingest(seconds: float, text):
+    """ctest.c's per-token path through the reference's own functions
+    (kv_make_key_frag + kv_set_key_frag_string + kv_hash_key_frag,
+    oracle/ref_cuckoo.cpp ref_ctest_frags), one thread, on 4 MiB slices of
+    the same text."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_ref_ht  # checker only
+    import ctypes as C
+    ref = load_ref_ht()
+    if ref is None:
+        return {"value": None, "error": "oracle/_ref/libkvref_ht.so not built"}
+    ref.ref_ctest_frags.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_size_t, C.c_void_p,
+                                    C.c_void_p, C.c_size_t, C.c_void_p]
+    ref.ref_ctest_frags.restype = C.c_long
+    m = 4 << 20
+    sl = np.ascontiguousarray(text[:m + 16].cpu().numpy())
+    frag = np.zeros(2 * m + 64, np.uint8)
+    ro = np.zeros(m // 2 + 1, np.uint64)
+    hh = np.zeros(m + 2, np.uint64)
+    sd = np.zeros(2, np.uint64)
+    total_t, total_n = 0.0, 0
+    while total_t < seconds:
+        t0 = time.perf_counter()
+        k = ref.ref_ctest_frags(sl.ctypes.data, m, 256, frag.ctypes.data, frag.size, ro.ctypes.data, hh.ctypes.data,
+                                ro.size, sd.ctypes.data)
+        total_t += time.perf_counter() - t0
+        total_n += int(k)
+    return {"value": total_n / total_t, "unit": "key/s", "cores": 1, "kind": "reference",
+            "sample": f"{total_n} tokens from 4 MiB slices x ctest ingest (tokenize + kv_make_key_frag + "
+                      f"kv_set_key_frag_string + kv_hash_key_frag), 1 thread, {total_t:.1f} s"}
+
+
 def load_traffic(config_name: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -235,7 +272,33 @@ def main():
     gen.manual_seed(1000 + rank)
 
     # ---- synthetic keys resident in HBM (each rank its own shard)
-    if cfg.get("crc"):
+    if cfg.get("ingest"):
+        r = torch.randint(0, 8, (n,), dtype=torch.uint8, device="cuda", generator=gen)
+        text = torch.where(r == 0, 32, torch.where(r == 1, 10, 97 + r)).to(torch.uint8)
+        del r
+        t_offs, t_lens = kvh.tokenize(text, 256)
+        ntok = t_offs.numel()
+        cap = ntok + 16
+        t_offs = torch.empty((cap,), dtype=torch.int64, device="cuda")
+        t_lens = torch.empty((cap,), dtype=torch.int32, device="cuda")
+        t_cnt = torch.zeros((1,), dtype=torch.int64, device="cuda")
+        t_scr = torch.empty((kvh.lib.kvh_tokenize_scratch_bytes(n) // 8 + 1,), dtype=torch.int64, device="cuda")
+        t_out = torch.empty((ntok, 2), dtype=torch.int64, device="cuda")
+        import ctypes as _C
+
+        def run(out):
+            st = torch.cuda.current_stream().cuda_stream
+            rc = kvh.lib.kvh_tokenize(text.data_ptr(), n, 256, t_offs.data_ptr(), t_lens.data_ptr(), cap,
+                                      t_cnt.data_ptr(), t_scr.data_ptr(), t_scr.numel() * 8, st)
+            assert rc == 0
+            rc = kvh.lib.kvh_meow128_spans(text.data_ptr(), t_offs.data_ptr(), t_lens.data_ptr(), ntok,
+                                           _C.c_uint64(seed[0]), _C.c_uint64(seed[1]), t_out.data_ptr(),
+                                           kvh.KVH_FIXUP | kvh.KVH_NULTERM, st)
+            assert rc == 0
+        # text read twice (count + emit passes) + spans written/read + key bytes gathered + hashes
+        alg_bytes = n + 12 * ntok + 16 * ntok
+        cfg["tokens"] = ntok
+    elif cfg.get("crc"):
         crc_out = torch.empty((n,), dtype=torch.int32, device="cuda")
         if cfg["var"]:
             lens = zipf_lengths(n, 8, 256, seed=3 + rank)
@@ -279,7 +342,7 @@ def main():
             run = lambda out: kvh.meow128_fixed(keys, L, seed, out=out)
         else:
             run = lambda out: kvh.meow128_multiseed(keys, L, list(C3_SEEDS[:arity]), out=out)
-    out = None if (cfg.get("positions") or cfg.get("crc")) else \
+    out = None if (cfg.get("positions") or cfg.get("crc") or cfg.get("ingest")) else \
         torch.empty((n, arity, 2) if arity > 1 else (n, 2), dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
 
@@ -302,14 +365,16 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     wall = kdist.reduce_max(wall, world)
 
-    n_hash = n * arity * args.steps * world  # keys for the f1 configs
+    units = cfg["tokens"] if cfg.get("ingest") else n * arity
+    n_hash = units * args.steps * world  # keys for the f1/f3/f4 configs
     value = n_hash / wall
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic, tsrc = load_traffic(args.config)
     res = {
-        "metric": METRIC_F1 if cfg.get("positions") else (METRIC_F4 if cfg.get("crc") else METRIC),
+        "metric": METRIC_F1 if cfg.get("positions") else (METRIC_F4 if cfg.get("crc") else
+                                                          (METRIC_F3 if cfg.get("ingest") else METRIC)),
         "value": value,
-        "unit": "key/s" if (cfg.get("positions") or cfg.get("crc")) else "hash/s",
+        "unit": "key/s" if (cfg.get("positions") or cfg.get("crc") or cfg.get("ingest")) else "hash/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -319,7 +384,8 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded uniform random key bytes generated on device; zipf lengths for C2)",
-        "config": {"workload": cfg["workload"], "config": args.config, "keys_per_gpu": n,
+        "config": {"workload": cfg["workload"], "config": args.config,
+                   "keys_per_gpu": cfg.get("tokens", n), **({"text_bytes": n} if cfg.get("ingest") else {}),
                    "key_len": L if L else "zipf 8-256", "hashes_per_key": arity,
                    "seed": ["0x%016x" % seed[0], "0x%016x" % seed[1]],
                    "parallelism": f"shard x{world} (index ranges, no collective)"},
@@ -338,6 +404,8 @@ def main():
                 res["cpu_baseline"] = cpu_baseline_positions(cfg, seed, args.cpu_seconds, geom)
             elif cfg.get("crc"):
                 res["cpu_baseline"] = cpu_baseline_crc(cfg, args.cpu_seconds)
+            elif cfg.get("ingest"):
+                res["cpu_baseline"] = cpu_baseline_ingest(args.cpu_seconds, text)
             else:
                 res["cpu_baseline"] = cpu_baseline(cfg, seed, args.cpu_seconds)
         except Exception as e:  # report, never hide

@@ -234,6 +234,36 @@ int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
                                 void *pos, uint32_t flags, void *stream);
 
 /* ---------------------------------------------------------------------
+ * Batch order by table position: kv_ht_radix_sort
+ * (src/radix_sort.cpp:31-41) + ctest.c:96-104's duplicate marking.
+ * Order: by ht_mod(h1) ascending (the reference's order); equal slots,
+ * which the reference leaves in unspecified order, are ordered by
+ * (h1 << 1, h1, h2) so that all duplicates are adjacent.
+ * ------------------------------------------------------------------- */
+#define KVH_DEDUP     0x8u  /* zero h1 of an element equal (h1,h2) to its successor, count it */
+
+/* layout of kv_ht_sort_t (include/raikv/radix_sort.h:8-11) */
+typedef struct {
+  uint64_t key, key2;
+  void    *item;
+} kvh_ht_sort_t;
+
+/* device scratch for n elements (0 on error) */
+size_t kvh_ht_sort_scratch_bytes(size_t n);
+/* n < 2^32 device (h1,h2) pairs (+ optional u64 items, NULL = carry the
+ * input index) -> hashes_out / items_out in table order; with KVH_DEDUP
+ * the duplicate count is written to *dup_count (device u64, optional). */
+int kvh_ht_sort(const uint64_t *hashes, const uint64_t *items, size_t n,
+                const kvh_ht_geom_t *geom, uint64_t *hashes_out,
+                uint64_t *items_out, uint64_t *dup_count, uint32_t flags,
+                void *scratch, size_t scratch_bytes, void *stream);
+/* host drop-in for kv_ht_radix_sort(ar, ar_size, ht) (radix_sort.h:19-20):
+ * sorts ar[] in place (synchronous, on the current GPU); the table is
+ * given by its geometry. */
+int kvh_ht_radix_sort(kvh_ht_sort_t *ar, uint32_t ar_size,
+                      const kvh_ht_geom_t *geom);
+
+/* ---------------------------------------------------------------------
  * Key ingest: the key formats raikv produces, hashed on
  * the device without host repacking.
  * ------------------------------------------------------------------- */

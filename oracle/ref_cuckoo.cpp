@@ -181,3 +181,43 @@ extern "C" long ref_ctest_frags(const char *text, size_t n, uint32_t max_token, 
   ::free(ht);
   return cnt;
 }
+
+/* f2 golden vectors: the reference's kv_ht_radix_sort (radix_sort.cpp:31-41)
+ * on a malloc'd HashTab of the given geometry; items carry input indices.
+ * Then ctest.c:96-104's adjacent-duplicate marking on that order (dup_out
+ * = count; the zeroed hashes are written to out_h). */
+#include <raikv/radix_sort.h>
+extern "C" int ref_ht_sort(uint64_t map_size, uint32_t entry_size, float ratio, uint16_t buckets, uint8_t arity,
+                           const uint64_t *h, size_t n, uint64_t *out_h, uint64_t *out_item, uint64_t *dup_out) {
+  HashTabGeom g;
+  memset(&g, 0, sizeof(g));
+  g.map_size = map_size;
+  g.hash_entry_size = entry_size;
+  g.hash_value_ratio = ratio;
+  g.cuckoo_buckets = buckets;
+  g.cuckoo_arity = arity;
+  HashTab *ht = HashTab::alloc_map(g);
+  if (ht == NULL) return -1;
+  kv_ht_sort_t *ar = (kv_ht_sort_t *) ::malloc(sizeof(kv_ht_sort_t) * (n ? n : 1));
+  for (size_t i = 0; i < n; i++) {
+    ar[i].key = h[2 * i];
+    ar[i].key2 = h[2 * i + 1];
+    ar[i].item = (void *) (uintptr_t) i;
+  }
+  kv_ht_radix_sort(ar, (uint32_t) n, (kv_hash_tab_t *) ht);
+  uint64_t dups = 0;
+  for (size_t k = 1; k < n; k++)
+    if (ar[k - 1].key == ar[k].key && ar[k - 1].key2 == ar[k].key2) {
+      ar[k - 1].key = 0;
+      dups++;
+    }
+  for (size_t i = 0; i < n; i++) {
+    out_h[2 * i] = ar[i].key;
+    out_h[2 * i + 1] = ar[i].key2;
+    out_item[i] = (uint64_t) (uintptr_t) ar[i].item;
+  }
+  *dup_out = dups;
+  ::free(ar);
+  ::free(ht);
+  return 0;
+}

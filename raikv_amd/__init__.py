@@ -13,6 +13,8 @@ from .binding import (  # noqa: F401
     HtGeom,
     crc_c_fixed,
     tokenize,
+    HtSorter,
+    KVH_DEDUP,
     meow128_spans,
     meow128_frags,
     KVH_NULTERM,
@@ -40,5 +42,5 @@ __all__ = [
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
     "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
-    "tokenize", "meow128_spans", "meow128_frags", "KVH_NULTERM",
+    "tokenize", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP",
 ]

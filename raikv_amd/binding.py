@@ -21,6 +21,7 @@ except Exception:  # pragma: no cover - torch is part of the image
 KVH_FIXUP = 0x1
 KVH_POS32 = 0x2
 KVH_NULTERM = 0x4
+KVH_DEDUP = 0x8
 KVH_MAX_ARITY = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -110,6 +111,9 @@ def _load():
         "kvh_tokenize": (I, [P, SZ, U32, P, P, SZ, P, P, SZ, P]),
         "kvh_meow128_spans": (I, [P, P, P, SZ, U64, U64, P, U32, P]),
         "kvh_meow128_frags": (I, [P, P, SZ, U64, U64, P, U32, P]),
+        "kvh_ht_sort_scratch_bytes": (SZ, [SZ]),
+        "kvh_ht_sort": (I, [P, P, SZ, P, P, P, P, U32, P, SZ, P]),
+        "kvh_ht_radix_sort": (I, [P, U32, P]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
         "kvh_version": (C.c_char_p, []),
@@ -196,6 +200,33 @@ def meow128_fixed_positions(keys, key_len: int, seed: Tuple[int, int], geom: "Ht
                                           _dev_ptr(out) if n else None, KVH_POS32 if pos32 else 0,
                                           _stream_ptr(stream)), "kvh_meow128_fixed_positions")
     return hashes, out
+
+
+class HtSorter:
+    """Device order-by-table-position of hash batches up to `cap` elements
+    (kv_ht_radix_sort + ctest dedup); holds its scratch buffer."""
+
+    def __init__(self, geom: "HtGeom", cap: int, device="cuda"):
+        self.geom, self.cap = geom, cap
+        nb = lib.kvh_ht_sort_scratch_bytes(cap)
+        if nb == 0:
+            raise KvhError("kvh_ht_sort_scratch_bytes failed")
+        self.scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device=device)
+        self.dups = torch.zeros((1,), dtype=torch.int64, device=device)
+
+    def sort(self, hashes, items=None, dedup: bool = False, out=None, items_out=None, stream=None):
+        n = hashes.numel() // 2
+        if n > self.cap:
+            raise KvhError(f"batch {n} > sorter capacity {self.cap}")
+        if out is None:
+            out = _new_out((n, 2), hashes)
+        if items_out is None:
+            items_out = torch.empty((n,), dtype=torch.int64, device=hashes.device)
+        check(lib.kvh_ht_sort(_dev_ptr(hashes) if n else None, _dev_ptr(items) if items is not None else None, n,
+                              C.byref(self.geom), _dev_ptr(out) if n else None, _dev_ptr(items_out) if n else None,
+                              _dev_ptr(self.dups), KVH_DEDUP if dedup else 0, _dev_ptr(self.scratch),
+                              self.scratch.numel() * 8, _stream_ptr(stream)), "kvh_ht_sort")
+        return out, items_out
 
 
 def tokenize(text, max_token: int = 256, cap: Optional[int] = None, stream=None):

@@ -1,0 +1,248 @@
+// ht_sort.hip -- SURVEY.md §8 row f2: order a hashed batch by hash-table
+// position and mark duplicates, on the device.
+//
+// Reference: kv_ht_radix_sort (src/radix_sort.cpp:31-41) sorts kv_ht_sort_t
+// {key, key2, item} by ht_mod(key) with an in-place MSD radix sort over the
+// bits of ht_size (include/raikv/radix_sort.h:29-316); elements whose slots
+// are equal keep an unspecified order.  ctest.c:96-104 then zeroes the
+// `hash` of every element equal (hash, hash2) to its successor and counts it.
+//
+// Here the order is total and deterministic: by slot, then by h1 (bit 63
+// ignored first, as the key below does), then h1, then h2 -- a refinement of
+// the reference's order, so every adjacent-equal pair the reference could
+// find is adjacent here, and all duplicates of a key are contiguous.
+//   1. k_sort_keys   key64 = slot << (64 - sbits) | (h1 << 1) >> sbits,
+//                    idx = i (u32)
+//   2. radix sort of (key64, idx) pairs: rocPRIM's onesweep
+//      rocprim::radix_sort_pairs (the library primitive; ROCm's own)
+//   3. k_sort_gather records[j] = (h1, h2, item) of idx[j]
+//   4. k_sort_fixup  runs of equal key64 (equal slot and equal top h1
+//                    bits: duplicates, in practice) insertion-sorted by the
+//                    full comparator; O(run) when the run is all equal
+//   5. k_sort_emit   hashes_out / items_out, with KVH_DEDUP the h1 of an
+//                    element equal to its successor set to 0 and counted
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <algorithm>
+#include <mutex>
+#include <vector>
+#include <rocprim/device/device_radix_sort.hpp>
+#include "kvh_internal.hpp"
+#include "ht_pos.hpp"
+#include "../../include/kvh.h"
+
+using namespace kvh;
+using namespace kvh::rt;
+
+namespace {
+
+constexpr int kSB = 256;
+
+struct Rec {
+  uint64_t h1, h2, item;
+};
+
+__device__ __forceinline__ bool rec_less(const Rec& a, const Rec& b) {
+  const uint64_t a0 = a.h1 << 1, b0 = b.h1 << 1;
+  if (a0 != b0) return a0 < b0;
+  if (a.h1 != b.h1) return a.h1 < b.h1;
+  return a.h2 < b.h2;
+}
+
+__global__ void __launch_bounds__(kSB)
+k_sort_keys(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sbits, uint64_t* __restrict__ key,
+            uint32_t* __restrict__ idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * kSB + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h1 = h[2 * i];
+  const uint64_t slot = ht_mod(g, h1);
+  key[i] = sbits >= 64 ? slot : (slot << (64 - sbits)) | ((h1 << 1) >> sbits);
+  idx[i] = (uint32_t)i;
+}
+
+__global__ void __launch_bounds__(kSB)
+k_sort_gather(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, const uint32_t* __restrict__ idx,
+              uint64_t n, Rec* __restrict__ rec) {
+  const uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t s = idx[j];
+  Rec r;
+  r.h1 = h[2 * (uint64_t)s];
+  r.h2 = h[2 * (uint64_t)s + 1];
+  r.item = items ? items[s] : (uint64_t)s;
+  rec[j] = r;
+}
+
+__global__ void __launch_bounds__(kSB)
+k_sort_fixup(const uint64_t* __restrict__ key, uint64_t n, Rec* __restrict__ rec) {
+  const uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x;
+  if (j + 1 >= n || key[j + 1] != key[j] || (j > 0 && key[j - 1] == key[j])) return;  // run starts only
+  uint64_t e = j + 2;
+  while (e < n && key[e] == key[j]) e++;
+  for (uint64_t a = j + 1; a < e; a++) {  // insertion sort of [j, e)
+    const Rec v = rec[a];
+    uint64_t b = a;
+    while (b > j && rec_less(v, rec[b - 1])) {
+      rec[b] = rec[b - 1];
+      b--;
+    }
+    if (b != a) rec[b] = v;
+  }
+}
+
+__global__ void __launch_bounds__(kSB)
+k_sort_emit(const Rec* __restrict__ rec, uint64_t n, uint64_t* __restrict__ h, uint64_t* __restrict__ items,
+            uint32_t dedup, unsigned long long* __restrict__ dups) {
+  const uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x;
+  uint32_t d = 0;
+  if (j < n) {
+    const Rec r = rec[j];
+    uint64_t h1 = r.h1;
+    if (dedup && j + 1 < n) {
+      const Rec s = rec[j + 1];
+      if (s.h1 == r.h1 && s.h2 == r.h2) { h1 = 0; d = 1; }
+    }
+    h[2 * j] = h1;
+    h[2 * j + 1] = r.h2;
+    if (items) items[j] = r.item;
+  }
+  if (dedup && dups) {
+    for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
+    if ((threadIdx.x & 63) == 0 && d) atomicAdd(dups, (unsigned long long)d);
+  }
+}
+
+size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct SortLayout {
+  size_t key_in, key_out, idx_in, idx_out, rec, tmp, tmp_bytes, total;
+};
+
+int sort_layout(size_t n, SortLayout* L) {
+  size_t tmp = 0;
+  hipError_t e = rocprim::radix_sort_pairs((void*)nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u, 64u,
+                                           (hipStream_t)0);
+  if (e != hipSuccess) return hip_err(e);
+  size_t o = 0;
+  L->key_in = o; o += al256(8 * n);
+  L->key_out = o; o += al256(8 * n);
+  L->idx_in = o; o += al256(4 * n);
+  L->idx_out = o; o += al256(4 * n);
+  L->rec = o; o += al256(sizeof(Rec) * n);
+  L->tmp = o; o += al256(tmp);
+  L->tmp_bytes = tmp;
+  L->total = o;
+  return 0;
+}
+
+uint32_t slot_bits(uint64_t ht_size) {
+  uint32_t b = 1;
+  while (b < 64 && (ht_size >> b) != 0) b++;
+  return b;
+}
+
+int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh_ht_geom_t* geom, uint64_t* h_out,
+              uint64_t* items_out, uint64_t* dup_count, uint32_t flags, void* scratch, size_t scratch_bytes,
+              hipStream_t st) {
+  if (!geom || geom->ht_size == 0 || geom->ht_mod_shift >= 64 || geom->ht_mod_fraction >= (1ull << 32))
+    return set_err(KVH_EINVAL);
+  const bool dedup = (flags & KVH_DEDUP) != 0;
+  if (dedup && dup_count) {
+    hipError_t e = hipMemsetAsync(dup_count, 0, 8, st);
+    if (e != hipSuccess) return hip_err(e);
+  }
+  if (n == 0) return set_err(0);
+  if (n >= (1ull << 32) || !hashes || !h_out || !scratch) return set_err(KVH_EINVAL);
+  SortLayout L;
+  int rc = sort_layout(n, &L);
+  if (rc) return rc;
+  if (scratch_bytes < L.total) return set_err(KVH_EINVAL);
+  uint8_t* s = (uint8_t*)scratch;
+  uint64_t* kin = (uint64_t*)(s + L.key_in);
+  uint64_t* kout = (uint64_t*)(s + L.key_out);
+  uint32_t* iin = (uint32_t*)(s + L.idx_in);
+  uint32_t* iout = (uint32_t*)(s + L.idx_out);
+  Rec* rec = (Rec*)(s + L.rec);
+  HtGeom g;
+  g.size = geom->ht_size;
+  g.mask = geom->ht_mod_mask;
+  g.frac = (uint32_t)geom->ht_mod_fraction;
+  g.shift = geom->ht_mod_shift;
+  g.buckets = geom->cuckoo_buckets;
+  const uint32_t grid = (uint32_t)((n + kSB - 1) / kSB);
+  hipLaunchKernelGGL(k_sort_keys, dim3(grid), dim3(kSB), 0, st, hashes, (uint64_t)n, g, slot_bits(geom->ht_size),
+                     kin, iin);
+  rc = launch_done();
+  if (rc) return rc;
+  size_t tb = L.tmp_bytes;
+  hipError_t e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, kin, kout, iin, iout, n, 0u, 64u, st);
+  if (e != hipSuccess) return hip_err(e);
+  hipLaunchKernelGGL(k_sort_gather, dim3(grid), dim3(kSB), 0, st, hashes, items, iout, (uint64_t)n, rec);
+  rc = launch_done();
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_sort_fixup, dim3(grid), dim3(kSB), 0, st, kout, (uint64_t)n, rec);
+  rc = launch_done();
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_sort_emit, dim3(grid), dim3(kSB), 0, st, rec, (uint64_t)n, h_out, items_out,
+                     dedup ? 1u : 0u, (unsigned long long*)dup_count);
+  return launch_done();
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t kvh_ht_sort_scratch_bytes(size_t n) {
+  SortLayout L;
+  if (sort_layout(n, &L) != 0) return 0;
+  return L.total;
+}
+
+int kvh_ht_sort(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh_ht_geom_t* geom,
+                uint64_t* hashes_out, uint64_t* items_out, uint64_t* dup_count, uint32_t flags, void* scratch,
+                size_t scratch_bytes, void* stream) {
+  return sort_impl(hashes, items, n, geom, hashes_out, items_out, dup_count, flags, scratch, scratch_bytes,
+                   (hipStream_t)stream);
+}
+
+int kvh_ht_radix_sort(kvh_ht_sort_t* ar, uint32_t ar_size, const kvh_ht_geom_t* geom) {
+  if (!geom) return set_err(KVH_EINVAL);
+  if (ar_size <= 1) return set_err(0);
+  if (!ar) return set_err(KVH_EINVAL);
+  const size_t n = ar_size;
+  std::vector<uint64_t> hv(2 * n), iv(n);
+  for (size_t i = 0; i < n; i++) {
+    hv[2 * i] = ar[i].key;
+    hv[2 * i + 1] = ar[i].key2;
+    iv[i] = (uint64_t)(uintptr_t)ar[i].item;
+  }
+  const size_t sb = kvh_ht_sort_scratch_bytes(n);
+  if (sb == 0) return set_err(KVH_EINVAL);
+  const size_t off_h = 0, off_i = al256(16 * n), off_ho = off_i + al256(8 * n), off_io = off_ho + al256(16 * n),
+               off_s = off_io + al256(8 * n), total = off_s + sb;
+  uint8_t* d = nullptr;
+  hipError_t e = hipMalloc(&d, total);
+  if (e != hipSuccess) return hip_err(e);
+  int rc = 0;
+  do {
+    if ((e = hipMemcpy(d + off_h, hv.data(), 16 * n, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_err(e); break; }
+    if ((e = hipMemcpy(d + off_i, iv.data(), 8 * n, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_err(e); break; }
+    rc = sort_impl((const uint64_t*)(d + off_h), (const uint64_t*)(d + off_i), n, geom, (uint64_t*)(d + off_ho),
+                   (uint64_t*)(d + off_io), nullptr, 0, d + off_s, sb, (hipStream_t)0);
+    if (rc) break;
+    if ((e = hipMemcpy(hv.data(), d + off_ho, 16 * n, hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_err(e); break; }
+    if ((e = hipMemcpy(iv.data(), d + off_io, 8 * n, hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_err(e); break; }
+  } while (0);
+  (void)hipFree(d);
+  if (rc) return rc;
+  for (size_t i = 0; i < n; i++) {
+    ar[i].key = hv[2 * i];
+    ar[i].key2 = hv[2 * i + 1];
+    ar[i].item = (void*)(uintptr_t)iv[i];
+  }
+  return set_err(0);
+}
+
+}  // extern "C"

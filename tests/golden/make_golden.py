@@ -8,7 +8,7 @@ reference's own functions (kv_hash_meow128 and its batched / streaming /
 vec variants, key_hash.c:1413-2020); the inputs are our own seeded random
 data.  The fixtures are data only (inputs + expected outputs).
 
-    python tests/golden/make_golden.py [--only-cuckoo | --only-crc | --only-ingest]
+    python tests/golden/make_golden.py [--only-cuckoo | --only-crc | --only-ingest | --only-sort]
 
 The table-position fixtures (cuckoo_*.npz) come from the reference's
 ht_init.cpp + ht_cuckoo.cpp compiled where they lie into
@@ -353,6 +353,43 @@ def make_ingest():
     print("ingest fixtures:", n, "bytes,", cnt, "tokens, seed", [hex(int(x)) for x in seed])
 
 
+SORT_GEOMS = [  # (name, map_size, entry_size, ratio, buckets, arity, n, dup_fraction)
+    ("kat64m", 64 << 20, 64, 1.0, 4, 4, 20000, 0.05),
+    ("tiny600", (448 << 10) + 64 * 600, 64, 1.0, 8, 8, 5000, 0.10),   # many equal slots
+    ("big4g", 4 << 30, 64, 1.0, 4, 4, 50000, 0.02),
+]
+
+
+def make_sort():
+    """kv_ht_radix_sort (radix_sort.cpp:31-41) + ctest.c:96-104 dedup by the
+    reference itself (oracle/ref_cuckoo.cpp ref_ht_sort)."""
+    ref = load_ref_ht()
+    ref.ref_ht_sort.argtypes = [U64, C.c_uint32, C.c_float, C.c_uint16, C.c_uint8, P, C.c_size_t, P, P, P]
+    ref.ref_ht_sort.restype = C.c_int
+    lib = load_ref()
+    rng = np.random.default_rng(20261018)
+    for name, ms, es, ratio, b, a, n, dupf in SORT_GEOMS:
+        kb = rng.integers(0, 256, size=n * 16, dtype=np.uint8)
+        hh = np.zeros(2 * n, dtype=np.uint64)
+        lib.ref_batch_fixed(ptr(kb), 16, n, U64(STATIC_SEED[0]), U64(STATIC_SEED[1]), ptr(hh))
+        hh = hh.reshape(n, 2)
+        hh[:, 0] &= np.uint64((1 << 63) - 1)
+        hh[hh[:, 0] <= 1, 0] = 2
+        nd = int(n * dupf)  # duplicated keys (copies of earlier rows), scattered
+        src = rng.integers(0, n - nd, nd)
+        dst = rng.choice(np.arange(n - nd, n), nd, replace=False)
+        hh[dst] = hh[src]
+        hh = np.ascontiguousarray(hh)
+        oh = np.zeros(2 * n, dtype=np.uint64)
+        oi = np.zeros(n, dtype=np.uint64)
+        dups = np.zeros(1, dtype=np.uint64)
+        assert ref.ref_ht_sort(ms, es, ratio, b, a, ptr(hh), n, ptr(oh), ptr(oi), ptr(dups)) == 0
+        np.savez_compressed(os.path.join(HERE, f"sort_{name}.npz"), hashes=hh, out_hashes=oh.reshape(n, 2),
+                            out_items=oi, dups=dups, params=np.array([ms, es, b, a], dtype=np.uint64),
+                            ratio=np.array([ratio], dtype=np.float32))
+        print("sort", name, n, "ref dups", int(dups[0]))
+
+
 if __name__ == "__main__":
     only = [a for a in sys.argv[1:] if a.startswith("--only-")]
     if not only:
@@ -363,3 +400,5 @@ if __name__ == "__main__":
         make_crc()
     if not only or "--only-ingest" in only:
         make_ingest()
+    if not only or "--only-sort" in only:
+        make_sort()

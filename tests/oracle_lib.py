@@ -207,3 +207,43 @@ def orc_hash_spans(lib, buf: np.ndarray, offs, lens, seed, nul=True, fix=True) -
     lib.orc_hash_spans(bb.ctypes.data, o.ctypes.data, l.ctypes.data, n, U64(seed[0]), U64(seed[1]), int(nul),
                        int(fix), out.ctypes.data)
     return out
+
+
+# ------------------------------------------------------------ table order (§8 f2)
+def np_ht_mod(geom, h1: np.ndarray) -> np.ndarray:
+    """FileHdr::ht_mod (shm_ht.h:181-184) in u64 numpy arithmetic (wraps)."""
+    x = h1 & np.uint64(geom.ht_mod_mask)
+    with np.errstate(over="ignore"):
+        return (x * np.uint64(geom.ht_mod_fraction)) >> np.uint64(geom.ht_mod_shift)
+
+
+def np_ht_sort(geom, hashes: np.ndarray, items=None, dedup=False):
+    """Restatement of kv_ht_radix_sort's order (radix_sort.cpp:31-41: by
+    ht_mod(key)) with the device's deterministic tie order (h1 << 1, h1,
+    h2), plus ctest.c:96-104's marking (earlier of an equal adjacent pair
+    gets h1 = 0).  Returns (hashes, items, dup_count)."""
+    h = np.ascontiguousarray(hashes, dtype=np.uint64).reshape(-1, 2)
+    n = len(h)
+    it = np.arange(n, dtype=np.uint64) if items is None else np.asarray(items, dtype=np.uint64)
+    slot = np_ht_mod(geom, h[:, 0])
+    order = np.lexsort((h[:, 1], h[:, 0], h[:, 0] << np.uint64(1), slot))
+    oh = h[order].copy()
+    oi = it[order].copy()
+    dups = 0
+    if dedup and n > 1:
+        eq = (oh[:-1, 0] == oh[1:, 0]) & (oh[:-1, 1] == oh[1:, 1])
+        oh[:-1, 0][eq] = 0
+        dups = int(eq.sum())
+    return oh, oi, dups
+
+
+def sort_fixtures():
+    import glob
+    out = []
+    for f in sorted(glob.glob(os.path.join(GOLDEN, "sort_*.npz"))):
+        d = np.load(f)
+        ms, es, b, a = (int(x) for x in d["params"])
+        out.append(dict(name=os.path.basename(f)[5:-4], map_size=ms, entry_size=es, buckets=b, arity=a,
+                        ratio=float(d["ratio"][0]), hashes=d["hashes"], out_hashes=d["out_hashes"],
+                        out_items=d["out_items"], dups=int(d["dups"][0])))
+    return out

@@ -1,0 +1,117 @@
+"""GPU parity for SURVEY.md §8 row f2 (batch order by table position +
+duplicate marking): kvh_ht_sort and the kvh_ht_radix_sort drop-in vs the
+oracle order (oracle_lib.np_ht_sort, itself checked against the
+reference's kv_ht_radix_sort in test_sort_oracle.py) on the golden inputs,
+plus edge cases and a full-size property test.  Bit-exact."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle_lib import load_oracle, np_ht_mod, np_ht_sort, orc_geom, sort_fixtures  # noqa: E402
+
+FIX = sort_fixtures()
+ORC = load_oracle()
+
+
+@pytest.fixture(scope="module")
+def kvh():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
+    import raikv_amd
+    return raikv_amd
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint64)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
+
+
+@pytest.mark.parametrize("f", FIX, ids=[f["name"] for f in FIX])
+def test_sort_golden(kvh, f):
+    g = kvh.HtGeom.from_map(f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    og = orc_geom(ORC, f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    h = f["hashes"]
+    srt = kvh.HtSorter(g, len(h))
+    for dedup in (False, True):
+        oh, oi = srt.sort(dev(h), dedup=dedup)
+        wh, wi, wd = np_ht_sort(og, h, dedup=dedup)
+        np.testing.assert_array_equal(host(oh), wh)
+        np.testing.assert_array_equal(host(oi), wi)
+        if dedup:
+            assert int(srt.dups.item()) == wd >= f["dups"]
+    # items carried through
+    items = np.arange(len(h), dtype=np.uint64) * np.uint64(7919) + np.uint64(3)
+    oh, oi = srt.sort(dev(h), items=dev(items))
+    np.testing.assert_array_equal(host(oi), np_ht_sort(og, h, items=items)[1])
+
+
+def test_radix_sort_drop_in(kvh):
+    f = FIX[0]
+    g = kvh.HtGeom.from_map(f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    og = orc_geom(ORC, f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    h = f["hashes"][:3000]
+
+    class SortT(C.Structure):
+        _fields_ = [("key", C.c_uint64), ("key2", C.c_uint64), ("item", C.c_void_p)]
+    ar = (SortT * len(h))(*[SortT(int(a), int(b), i + 1) for i, (a, b) in enumerate(h)])
+    assert kvh.lib.kvh_ht_radix_sort(ar, len(h), C.byref(g)) == 0
+    wh, wi, _ = np_ht_sort(og, h, items=np.arange(1, len(h) + 1, dtype=np.uint64))
+    np.testing.assert_array_equal(np.array([[x.key, x.key2] for x in ar], dtype=np.uint64), wh)
+    np.testing.assert_array_equal(np.array([x.item for x in ar], dtype=np.uint64), wi)
+
+
+def test_edges(kvh):
+    g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
+    og = orc_geom(ORC, 64 << 20, 64, 1.0, 4, 4)
+    srt = kvh.HtSorter(g, 5000)
+    rng = np.random.default_rng(2)
+    for n in (1, 2, 3, 255, 256, 257, 4999):
+        h = rng.integers(0, 2 ** 63, size=(n, 2), dtype=np.uint64)
+        oh, oi = srt.sort(dev(h), dedup=True)
+        wh, wi, wd = np_ht_sort(og, h, dedup=True)
+        np.testing.assert_array_equal(host(oh), wh)
+        np.testing.assert_array_equal(host(oi), wi)
+    # all identical: one run, n-1 duplicates
+    h = np.tile(np.array([[12345, 678]], dtype=np.uint64), (3000, 1))
+    oh, oi = srt.sort(dev(h), dedup=True)
+    assert int(srt.dups.item()) == 2999
+    assert np.all(host(oh)[:-1, 0] == 0) and host(oh)[-1, 0] == 12345
+
+
+def test_full_size_properties(kvh):
+    """100M fixed-up hashes of C1 keys with 1% duplicates into a 64 GiB
+    table: output slots non-decreasing, items a permutation, rows equal the
+    gathered inputs, duplicate count = n - unique, oracle on a window."""
+    n = 100_000_000
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(3)
+    keys = torch.randint(0, 256, (n * 16,), dtype=torch.uint8, device="cuda", generator=gen)
+    h = kvh.meow128_fixed(keys, 16, kvh.STATIC_SEED, fixup=True)
+    del keys
+    nd = n // 100
+    dst = torch.randperm(n, device="cuda", generator=gen)[:nd]
+    src = torch.randint(0, n, (nd,), device="cuda", generator=gen)
+    h[dst] = h[src]
+    g = kvh.HtGeom.from_map(64 << 30, 64, 1.0, 4, 4)
+    srt = kvh.HtSorter(g, n)
+    oh, oi = srt.sort(h, dedup=False)
+    mask, frac, shift = int(g.ht_mod_mask), int(g.ht_mod_fraction), int(g.ht_mod_shift)
+    slot = ((oh[:, 0] & mask) * frac) >> shift  # < 2^62: no int64 overflow for this geometry
+    assert bool((slot[1:] >= slot[:-1]).all())
+    assert bool(torch.equal(torch.sort(oi).values, torch.arange(n, device="cuda")))
+    assert bool(torch.equal(oh, h[oi]))
+    uniq = torch.unique(h, dim=0).shape[0]
+    _, _ = srt.sort(h, dedup=True)
+    assert int(srt.dups.item()) == n - uniq
+    og = orc_geom(ORC, 64 << 30, 64, 1.0, 4, 4)
+    hs = host(h)
+    w = np.flatnonzero(np.isin(host(oi), np.arange(0, n, 997)))  # a spread-out sample of rows
+    assert np.all(np.diff(np_ht_mod(og, hs[host(oi)[w].astype(np.int64), 0]).astype(np.int64)) >= 0)
