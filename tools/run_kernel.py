@@ -30,10 +30,18 @@ g = torch.Generator(device="cuda")
 g.manual_seed(1)
 cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1),
        "f1": (100_000_000, 16, -1), "f1p": (100_000_000, 16, -2), "f4": (100_000_000, 16, -4),
-       "f4v": (100_000_000, 0, -4)}
+       "f4v": (100_000_000, 0, -4), "f3": (1 << 30, 0, -3)}
 n, L, ar = cfg[a.config]
 n = a.n or n
-if ar == -4:  # CRC32C
+if ar == -3:  # ingest: tokenize + NUL-terminated span hashes
+    r = torch.randint(0, 8, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    text = torch.where(r == 0, 32, torch.where(r == 1, 10, 97 + r)).to(torch.uint8)
+    del r
+
+    def f():
+        o, l = kvh.tokenize(text, 256)
+        kvh.meow128_spans(text, o, l, kvh.STATIC_SEED)
+elif ar == -4:  # CRC32C
     co = torch.empty((n,), dtype=torch.int32, device="cuda")
     if L == 0:
         offs = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=3))
