@@ -37,6 +37,11 @@ METRIC_F1 = "keys/sec -> hash + cuckoo table positions, device-resident (SURVEY.
 METRIC_F4 = "CRC32C (kv_crc_c) keys/sec, device-resident (SURVEY.md §8 f4)"
 METRIC_F3 = "tokens/sec: text -> tokenize -> NUL-terminated key hashes, device-resident (SURVEY.md §8 f3)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
+# LDS table-lookup ceiling: ds_read_b32 serves 32 lanes per LDS cycle per CU
+# (MI355X_MICROARCH.md §LDS, 128 B/clk), 256 CUs, 2.4 GHz peak engine clock
+LDS_PEAK_LOOKUPS = 32 * 256 * 2.4e9
+# T-table lookups per unit of work (16 per AES round; folded rounds)
+LOOKUPS_PER_UNIT = {"c1": 5 * 16, "c4": 7 * 16, "c3": 4 * 7 * 16, "f1": 5 * 16, "f4": 16}
 
 CONFIGS = {
     "c1": dict(workload="C1: 100M fixed 16-byte keys resident in HBM, one lane per key, bit-exact vs reference",
@@ -227,6 +232,18 @@ def cpu_baseline_ingest(seconds: float, text):
                       f"kv_set_key_frag_string + kv_hash_key_frag), 1 thread, {total_t:.1f} s"}
 
 
+def lds_line(config_name, units, kern_ms):
+    """The Meow/CRC kernels are bound by LDS table lookups, not HBM
+    (DESIGN.md §3.3): lookups per launch / kernel time vs the LDS ceiling."""
+    lk = LOOKUPS_PER_UNIT.get(config_name)
+    if lk is None:
+        return None
+    ach = units * lk / (kern_ms * 1e-3)
+    return {"lookups_per_unit": lk, "achieved": ach, "peak": LDS_PEAK_LOOKUPS, "unit": "lookups/s",
+            "frac": ach / LDS_PEAK_LOOKUPS,
+            "note": "peak at the 2.4 GHz engine clock; under this load the chip holds 1.7-1.9 GHz"}
+
+
 def load_traffic(config_name: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -395,6 +412,7 @@ def main():
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
                      "traffic_source": tsrc},
         "hashes_per_s_per_gpu": n * arity / (kern_ms * 1e-3),
+        "lds_roofline": lds_line(args.config, units, kern_ms),
     }
     if args.e2e and rank == 0:
         res["e2e_pcie"] = e2e(kvh, cfg, seed)
