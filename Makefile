@@ -9,9 +9,10 @@ LIB      := raikv_amd/libkvh.so
 SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/ht_pos.hip raikv_amd/csrc/crc32c.hip raikv_amd/csrc/ingest.hip raikv_amd/csrc/ht_sort.hip
 OBJS     := $(SRCS:.hip=.o)
 HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/csrc/kvh_internal.hpp \
-            raikv_amd/csrc/ht_pos.hpp include/kvh.h include/raikv_amd/key_hash.hpp
+            raikv_amd/csrc/ht_pos.hpp raikv_amd/csrc/bs_prelude.hpp raikv_amd/csrc/bs_aes.hpp \
+            raikv_amd/csrc/bs_meow.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
-CPP_TESTS := tests/cpp/hash_test_gpu
+CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test
 
 all: $(LIB) oracle cpptests
 
@@ -31,6 +32,10 @@ tests/cpp/hash_test_gpu: tests/cpp/hash_test_gpu.cpp $(LIB) include/raikv_amd/ke
 	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
 	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
+
+# TEST ONLY: the bitsliced Meow chain run on the host against the oracle
+tests/cpp/bs_host_test: tests/cpp/bs_host_test.cpp raikv_amd/csrc/bs_aes.hpp raikv_amd/csrc/bs_meow.hpp oracle
+	g++ -O2 -std=c++17 -o $@ $< -Loracle -loracle -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 clean:
 	rm -f $(LIB) $(OBJS) $(CPP_TESTS)

@@ -344,7 +344,8 @@ int         kvh_device_synchronize(void);
  * 1 = workgroups per CU multiplier, 2 = force generic kernel (0/1),
  * 3 = keys per lane per step in the fixed-length kernel (1, 2 or 4),
  * 5 = ablation mode of the 16/32-byte kernel (0 product, 1 copy-only,
- *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3).
+ *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3),
+ * 10 = register prefetch of the next chunk in the fixed-length kernel (0/1).
  * Returns the previous value or KVH_EINVAL. */
 int         kvh_set_tuning(int knob, int value);
 /* diagnostics: per-wave phase cycle stamps of the last stamped launch */

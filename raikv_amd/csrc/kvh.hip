@@ -18,6 +18,7 @@
 #include <vector>
 #include <algorithm>
 #include "meow_dev.hpp"
+#include "bs_prelude.hpp"
 #include "kvh_internal.hpp"
 #include "../../include/kvh.h"
 
@@ -49,7 +50,7 @@ constexpr int kBlock = 1024;          // threads per workgroup (16 waves)
 // 1 = copy keys to out without hashing (memory-only); 2 = no key loads (keys
 // synthesised from the index: LDS + stores); 3 = no stores (hashes folded
 // into one value per lane: LDS + loads).
-template <int L, int NT, bool A16, int U, int MODE = 0>
+template <int L, int NT, bool A16, int U, int MODE = 0, bool PF = false>
 __global__ void __launch_bounds__(kBlock)
 k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
         uint64_t* __restrict__ out, uint32_t flags) {
@@ -65,8 +66,7 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
   const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
   const uint64_t last = n - 1;
   Blk acc = bzero();
-  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
-    Blk D[U][NC];
+  auto load_chunk = [&](uint64_t b, Blk (&D)[U][NC]) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint64_t j = b + 64 * u + lane;
@@ -78,6 +78,24 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
       } else {
         load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
       }
+    }
+  };
+  // PF: the next chunk's loads are issued before this chunk's rounds, so
+  // each wave keeps its HBM reads in flight across its whole compute phase
+  // (U*NC*4 more VGPRs; the past-the-end prefetch of the last trip reads the
+  // clamped key n-1 and is dropped)
+  Blk Dn[U][NC];
+  if constexpr (PF) load_chunk(wave * 64 * U, Dn);
+  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
+    Blk D[U][NC];
+    if constexpr (PF) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int c = 0; c < NC; c++) D[u][c] = Dn[u][c];
+      load_chunk(b + step, Dn);
+    } else {
+      load_chunk(b, D);
     }
     Blk h[U];
 #pragma unroll
@@ -1003,6 +1021,97 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
   }
 }
 
+// ---------------------------------------------------------------------
+// k_hybrid: the LDS T-table round and the bitsliced VALU round (bs_meow.hpp)
+// side by side in one workgroup per CU.  The T-table keys are bound by the
+// LDS lookup rate (16 ds_read_b32 per key-round) with the VALU about a third
+// busy; the bitsliced keys need no LDS at all.  Waves [0, 16-NBW) hash keys
+// [nB, n) exactly like k_fixed (wave-chunked, U keys per lane); waves
+// [16-NBW, 16) hash keys [0, nB) in batches of 512 (lane l takes keys
+// b + 64j + l, j < 8: every load/store instruction moves a contiguous 1 KiB
+// run).  nB is a multiple of 512 chosen by the host (kvh_set_tuning knob 11:
+// the bitsliced share in per mille).
+template <int L, int NT, int U, int NBW, int PRIO = 2>
+__global__ void __launch_bounds__(kBlock)
+k_hybrid(const uint8_t* __restrict__ keys, uint64_t n, uint64_t nB, uint64_t s1, uint64_t s2,
+         uint64_t* __restrict__ out, uint32_t flags) {
+  static_assert(L == 16 || L == 32 || L == 48, "hybrid: 16, 32 or 48-byte keys");
+  constexpr int NC = L / 16;
+  constexpr int NTW = kBlock / 64 - NBW;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint64_t lane = threadIdx.x & 63;
+  if (wv < (uint32_t)NTW) {
+    // the LDS-bound waves win VALU issue arbitration; the bitsliced waves
+    // fill the VALU slots they leave
+    if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+    const uint64_t gw = (uint64_t)blockIdx.x * NTW + wv, tw = (uint64_t)gridDim.x * NTW;
+    const uint64_t last = n - 1;
+    for (uint64_t b = nB + gw * 64 * U; b < n; b += tw * 64 * U) {
+      Blk D[U][NC];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t j = b + 64 * u + lane;
+        load_fixed<L, true, true>(keys + (j < last ? j : last) * L, D[u]);
+      }
+      Blk h[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t j = b + 64 * u + lane;
+        store_h<true>(out, j < last ? j : last, h[u], fix);
+      }
+    }
+  } else {
+    // constant masks, lane t < 32 holds register t's (bs_meow.hpp KeySrc)
+    bs::KeySrc ks;
+    {
+      const uint32_t t = (uint32_t)lane & 31u;
+      const uint32_t zero[4] = {0, 0, 0, 0};
+      auto mk = [&](const Blk& z, int kind) {
+        const uint32_t zz[4] = {z.w[0], z.w[1], z.w[2], z.w[3]};
+        return bs::mask_of(zz, t, kind);
+      };
+      ks.lv[bs::KeySrc::kZero] = bs::mask_of(zero, t, bs::kKap);
+      ks.lv[bs::KeySrc::kA0] = mk(K.F[0], bs::kKapX);
+      ks.lv[bs::KeySrc::kA1] = mk(K.F[1], bs::kKapX);
+      ks.lv[bs::KeySrc::kA2] = mk(K.F[2], bs::kKapX);
+      ks.lv[bs::KeySrc::kM] = mk(K.M, bs::kKap);
+      ks.lv[bs::KeySrc::kG1] = mk(K.G[1], bs::kKap);
+      ks.lv[bs::KeySrc::kG3] = mk(K.G[3], bs::kKap);
+      ks.lv[bs::KeySrc::kCS2b] = mk(K.CS2b, bs::kKap);
+      ks.lv[bs::KeySrc::kMstd] = mk(K.M, bs::kStd);
+    }
+    const uint64_t gw = (uint64_t)blockIdx.x * NBW + (wv - NTW), tw = (uint64_t)gridDim.x * NBW;
+    for (uint64_t b = gw * 512; b < nB; b += tw * 512) {
+      uint32_t w[NC][8][4];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint8_t* p = keys + (b + 64 * j + lane) * L;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          const v4u v = __builtin_nontemporal_load((const v4u*)(p + 16 * c));
+          w[c][j][0] = v.x; w[c][j][1] = v.y; w[c][j][2] = v.z; w[c][j][3] = v.w;
+        }
+      }
+      uint32_t h[8][4];
+      bs::meow_bs<L>(w, ks, h);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        Blk x;
+        x.w[0] = h[j][0]; x.w[1] = h[j][1]; x.w[2] = h[j][2]; x.w[3] = h[j][3];
+        store_h<true>(out, b + 64 * j + lane, x, fix);
+      }
+    }
+  }
+}
+
 // straight-line restatement, one thread per key, per-key seeds
 __global__ void __launch_bounds__(256)
 k_seeded(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
@@ -1084,10 +1193,14 @@ int launch_done() {
 namespace {
 
 // ------------------------------------------------------------ host side
-int g_tune_nt = 2;        // tables per LDS: 2 or 4
+int g_tune_nt = 0;        // tables per LDS: 2 or 4 (0 = per-length default)
 int g_tune_wgmul = 1;     // workgroups per CU multiplier
 int g_tune_generic = 0;   // force the generic kernel
-int g_tune_kpl = 2;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8)
+int g_tune_kpl = 0;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8; 0 = per-length default)
+int g_tune_pf = 0;
+int g_tune_bs = 0;        // hybrid kernel: bitsliced share of the keys in per mille (0 = k_fixed)
+int g_tune_bsw = 4;
+int g_tune_prio = 2;      // hybrid kernel: s_setprio of the T-table waves (0, 2, 3)       // hybrid kernel: bitsliced waves per 16-wave workgroup        // k_fixed: 1 = register prefetch of the next chunk
 int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
 int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
 int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
@@ -1102,15 +1215,15 @@ uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
 }
 
 
-template <int L, int NT, int U, int MODE = 0>
+template <int L, int NT, int U, int MODE = 0, bool PF = false>
 int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,
              hipStream_t st, int cus) {
   const bool a16 = ((uintptr_t)keys & 15) == 0;
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
   if (a16)
-    hipLaunchKernelGGL((k_fixed<L, NT, true, U, MODE>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+    hipLaunchKernelGGL((k_fixed<L, NT, true, U, MODE, PF>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
   else
-    hipLaunchKernelGGL((k_fixed<L, NT, false, U, MODE>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+    hipLaunchKernelGGL((k_fixed<L, NT, false, U, MODE, PF>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
   return launch_done();
 }
 
@@ -1120,6 +1233,10 @@ template <int L>
 int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
                     uint32_t flags, hipStream_t st, int cus) {
   if constexpr (L == 16 || L == 32) {
+    // per-length defaults from tools/tune.py: Td0..Td3 in LDS
+    // (no rotations), 4 keys per lane at 16 B, 2 at 32 B
+    const int nt = g_tune_nt ? g_tune_nt : 4;
+    const int kpl = g_tune_kpl ? g_tune_kpl : (L == 16 ? 4 : 2);
     if (g_tune_ablate) {
       switch (g_tune_ablate) {
         case 1: return launch_k<L, 2, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
@@ -1129,7 +1246,7 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
       }
     }
     if (g_tune_dma && ((uintptr_t)keys & 15) == 0) {
-      const int dk = g_tune_nt * 10 + g_tune_dma;
+      const int dk = (g_tune_nt ? g_tune_nt : 2) * 10 + g_tune_dma;
       const uint32_t grid = grid_for(n, cus, 1);
       switch (dk) {
 #define KVH_DMA(NTv, Rv)                                                                              \
@@ -1145,8 +1262,27 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
         default: break;
       }
     }
-    const int key = g_tune_nt * 100 + g_tune_kpl;
+    if (L == 16 && g_tune_bs > 0 && ((uintptr_t)keys & 15) == 0) {
+      const uint64_t nB = (uint64_t)((double)n * g_tune_bs / 1000.0) / 512 * 512;
+      const uint32_t grid = grid_for(n, cus, 1);
+      const int hk = g_tune_prio * 1000 + nt * 100 + kpl * 10 + g_tune_bsw;
+      switch (hk) {
+#define KVH_HY(Pv, NTv, Uv, Wv)                                                                               \
+  case Pv * 1000 + NTv * 100 + Uv * 10 + Wv:                                                                 \
+    hipLaunchKernelGGL((k_hybrid<16, NTv, Uv, Wv, Pv>), dim3(grid), dim3(kBlock), 0, st, keys, n, nB, s1, s2, \
+                       out, flags);                                                                          \
+    return launch_done();
+        KVH_HY(0, 4, 4, 4) KVH_HY(2, 4, 4, 4) KVH_HY(2, 4, 2, 4) KVH_HY(2, 4, 4, 8) KVH_HY(2, 4, 4, 2)
+#undef KVH_HY
+        default: return set_err(KVH_EINVAL);
+      }
+    }
+    const int key = g_tune_pf * 1000 + nt * 100 + kpl;
     switch (key) {
+      case 1201: return launch_k<L, 2, 1, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+      case 1202: return launch_k<L, 2, 2, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+      case 1204: return launch_k<L, 2, 4, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+      case 1402: return launch_k<L, 4, 2, 0, true>(keys, n, s1, s2, out, flags, st, cus);
       case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
       case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
       case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
@@ -1227,9 +1363,9 @@ int stage_reserve(size_t bytes) {  // caller holds g_stage.mu
   if (g_stage.dev && g_stage.device == dev && g_stage.cap >= bytes) return 0;
   if (g_stage.dev) {
     int cur = dev;
-    hipSetDevice(g_stage.device);
-    hipFree(g_stage.dev);
-    hipSetDevice(cur);
+    (void)hipSetDevice(g_stage.device);  // best-effort release of the old staging buffer
+    (void)hipFree(g_stage.dev);
+    (void)hipSetDevice(cur);
     g_stage.dev = nullptr;
   }
   size_t cap = std::max<size_t>(bytes, 1 << 20);
@@ -1500,11 +1636,12 @@ int kvh_meow128_fixed_host(const void* keys, uint32_t key_len, size_t n, uint64_
   for (int s = 0; s < NS; s++) {
     int r2 = st[s] ? drain(s) : 0;
     if (!rc) rc = r2;
-    if (st[s]) hipStreamDestroy(st[s]);
-    if (dk[s]) hipFree(dk[s]);
-    if (dout[s]) hipFree(dout[s]);
-    if (hk[s]) hipHostFree(hk[s]);
-    if (ho[s]) hipHostFree(ho[s]);
+    // teardown: the first error (rc) is what the caller sees
+    if (st[s]) (void)hipStreamDestroy(st[s]);
+    if (dk[s]) (void)hipFree(dk[s]);
+    if (dout[s]) (void)hipFree(dout[s]);
+    if (hk[s]) (void)hipHostFree(hk[s]);
+    if (ho[s]) (void)hipHostFree(ho[s]);
   }
   return rc ? rc : set_err(0);
 }
@@ -1713,10 +1850,14 @@ int kvh_device_synchronize(void) {
 int kvh_set_tuning(int knob, int value) {
   int prev;
   switch (knob) {
-    case 0: if (value != 2 && value != 4) return KVH_EINVAL; prev = g_tune_nt; g_tune_nt = value; return prev;
+    case 0: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL; prev = g_tune_nt; g_tune_nt = value; return prev;
     case 1: if (value < 1 || value > 8) return KVH_EINVAL; prev = g_tune_wgmul; g_tune_wgmul = value; return prev;
     case 2: prev = g_tune_generic; g_tune_generic = value ? 1 : 0; return prev;
-    case 3: if (value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_kpl; g_tune_kpl = value; return prev;
+    case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_kpl; g_tune_kpl = value; return prev;
+    case 11: if (value < 0 || value > 1000) return KVH_EINVAL; prev = g_tune_bs; g_tune_bs = value; return prev;
+    case 12: if (value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_bsw; g_tune_bsw = value; return prev;
+    case 13: if (value != 0 && value != 2 && value != 3) return KVH_EINVAL; prev = g_tune_prio; g_tune_prio = value; return prev;
+    case 10: prev = g_tune_pf; g_tune_pf = value ? 1 : 0; return prev;
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
     case 9: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_var_mode; g_tune_var_mode = value; return prev;
     case 8: prev = g_tune_ms_lanes; g_tune_ms_lanes = value ? 1 : 0; return prev;

@@ -6,6 +6,7 @@
 //
 // Exit status 0 = all checks passed.  Prints one line per failed check.
 #include <stdio.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 #include <inttypes.h>
@@ -15,6 +16,7 @@
 
 static int failures = 0, checks = 0;
 #define EXPECT(c, ...) do { checks++; if (!(c)) { failures++; printf("FAIL: " __VA_ARGS__); printf("\n"); } } while (0)
+#define HC(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("FAIL: %s -> hip error %d\n", #x, (int)e_); exit(2); } } while (0)
 
 int main() {
   using namespace kvh;
@@ -105,17 +107,17 @@ int main() {
     koff[nk] = T * 128;
     for (size_t i = 0; i < nk; i++) { seeds[2 * i] = 10101; seeds[2 * i + 1] = 20202; }
     void *dk, *doff, *dseed, *do1, *do2;
-    hipMalloc(&dk, keys.size()); hipMalloc(&doff, 8 * koff.size()); hipMalloc(&dseed, 8 * seeds.size());
-    hipMalloc(&do1, 16 * nk); hipMalloc(&do2, 16 * nk);
-    hipMemcpy(dk, keys.data(), keys.size(), hipMemcpyHostToDevice);
-    hipMemcpy(doff, koff.data(), 8 * koff.size(), hipMemcpyHostToDevice);
-    hipMemcpy(dseed, seeds.data(), 8 * seeds.size(), hipMemcpyHostToDevice);
+    HC(hipMalloc(&dk, keys.size())); HC(hipMalloc(&doff, 8 * koff.size())); HC(hipMalloc(&dseed, 8 * seeds.size()));
+    HC(hipMalloc(&do1, 16 * nk)); HC(hipMalloc(&do2, 16 * nk));
+    HC(hipMemcpy(dk, keys.data(), keys.size(), hipMemcpyHostToDevice));
+    HC(hipMemcpy(doff, koff.data(), 8 * koff.size(), hipMemcpyHostToDevice));
+    HC(hipMemcpy(dseed, seeds.data(), 8 * seeds.size(), hipMemcpyHostToDevice));
     check(kvh_meow128_var(dk, (const uint64_t*)doff, nk, 10101, 20202, (uint64_t*)do1, 0, nullptr), "var");
     check(kvh_meow128_var_seeded(dk, (const uint64_t*)doff, nk, (const uint64_t*)dseed, (uint64_t*)do2, 0,
                                  nullptr), "seeded");
     std::vector<uint64_t> r1(2 * nk), r2(2 * nk);
-    hipMemcpy(r1.data(), do1, 16 * nk, hipMemcpyDeviceToHost);
-    hipMemcpy(r2.data(), do2, 16 * nk, hipMemcpyDeviceToHost);
+    HC(hipMemcpy(r1.data(), do1, 16 * nk, hipMemcpyDeviceToHost));
+    HC(hipMemcpy(r2.data(), do2, 16 * nk, hipMemcpyDeviceToHost));
     size_t bad = 0;
     for (size_t i = 0; i < 2 * nk; i++) bad += r1[i] != r2[i];
     EXPECT(bad == 0, "part4 folded vs literal: %zu mismatching words of %zu", bad, 2 * nk);
@@ -127,7 +129,7 @@ int main() {
             "4diff");
       EXPECT(memcmp(dd, &r1[8 * t], 64) == 0, "part4 diff %zu %zu %zu", n, m, o);
     }
-    hipFree(dk); hipFree(doff); hipFree(dseed); hipFree(do1); hipFree(do2);
+    HC(hipFree(dk)); HC(hipFree(doff)); HC(hipFree(dseed)); HC(hipFree(do1)); HC(hipFree(do2));
   }
   printf("hash_test_gpu: %d checks, %d failures\n", checks, failures);
   return failures ? 1 : 0;

@@ -18,7 +18,11 @@ ap.add_argument("--n", type=int, default=0)
 ap.add_argument("--nt", type=int, default=0)
 ap.add_argument("--kpl", type=int, default=0)
 ap.add_argument("--var", type=int, default=-1)
+ap.add_argument("--knob", action="append", default=[], help="kvh_set_tuning K=V (repeatable)")
 a = ap.parse_args()
+for kv in a.knob:
+    k, v = kv.split("=")
+    assert kvh.lib.kvh_set_tuning(int(k), int(v)) >= 0, kv
 if a.nt:
     kvh.lib.kvh_set_tuning(0, a.nt)
 if a.kpl:

@@ -30,7 +30,7 @@ out = torch.empty((a.n, a.arity, 2), dtype=torch.int64, device="cuda")
 seeds = [(1, 2), (3, 4), (5, 6), (7, 8)][: a.arity]
 spec = dict(kv.split("=") for kv in a.variants.split(";"))
 axes = {k: [int(x) for x in v.split(",")] for k, v in spec.items()}
-knob = {"nt": 0, "wg": 1, "generic": 2, "kpl": 3, "dma": 6, "var": 7, "mslanes": 8}
+knob = {"nt": 0, "wg": 1, "generic": 2, "kpl": 3, "dma": 6, "var": 7, "mslanes": 8, "pf": 10, "bs": 11, "bsw": 12, "prio": 13}
 names = list(axes)
 variants = list(itertools.product(*[axes[k] for k in names]))
 ref = None
