@@ -644,12 +644,15 @@ struct LdsKV5 {
   uint32_t L;
   Blk m;
   const Tab& T;
-  __device__ __forceinline__ LdsKV5(const VConst* f, uint32_t len, uint64_t s1, uint64_t s2, const Tab& t)
-      : full(f), L(len), m(mixer(s1, s2, len)), T(t) {}
+  const Blk* ftab;  // first-absorb folds F[0..3] for kLT <= L < kLT + kNF, or null
+  __device__ __forceinline__ LdsKV5(const VConst* f, uint32_t len, uint64_t s1, uint64_t s2, const Tab& t,
+                                    const Blk* ft = nullptr)
+      : full(f), L(len), m(mixer(s1, s2, len)), T(t), ftab(ft) {}
   __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
   __device__ __forceinline__ Blk M() const { return m; }
   __device__ __forceinline__ Blk F(int i) const {
     if (L < (uint32_t)kLT) return full[L].F[i];
+    if (ftab && L < (uint32_t)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
     return aesT(bxor(ramp(i), m), T);
   }
   __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
@@ -889,11 +892,20 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
   constexpr int M = WIN / 64;
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
   __shared__ VConst kfull[kLT];
+  __shared__ Blk kf[C::kWaves * C::kPerWave + LdsTab<NT>::kWords * 4 + kLT * sizeof(VConst) + kNF * 64 <= 163840
+                    ? kNF * 4 : 1];  // F folds for 64 <= L < 320 when the LDS has room
+  constexpr bool kHaveF = sizeof(kf) == kNF * 4 * sizeof(Blk);
   __shared__ __attribute__((aligned(16))) uint8_t wavemem[C::kWaves * C::kPerWave];
   fill_tables<NT>(lds);
   __syncthreads();
   const LdsTab<NT> T(lds);
-  for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) {
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + (kHaveF ? kNF : 0)); l += blockDim.x) {
+    if (l >= (uint32_t)kLT) {
+      const Blk M = mixer(s1, s2, l);
+#pragma unroll
+      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), M), T);
+      continue;
+    }
     const MeowConst k = make_const(s1, s2, l, T);
     VConst v;
 #pragma unroll
@@ -901,6 +913,7 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     v.TG2 = k.TG2; v.CS2b = k.CS2b; v.TCS0a = k.TCS0a;
     kfull[l] = v;
   }
+  const Blk* ftab = kHaveF ? kf : nullptr;
   __syncthreads();
   const bool fix = (flags & KVH_FIXUP) != 0;
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -998,7 +1011,7 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
         ix[c] = WIN;
         if (pos < k) {
           const uint32_t kl = r_len[pos];
-          const LdsKV5<LdsTab<NT>> K(kfull, kl, s1, s2, T);
+          const LdsKV5<LdsTab<NT>> K(kfull, kl, s1, s2, T, ftab);
           hs[c] = meow_rt(base + r_off[pos], kl, K, T);
           if (fix) hs[c] = fixup(hs[c]);
           ix[c] = r_idx[pos];
