@@ -345,7 +345,9 @@ int         kvh_device_synchronize(void);
  * 3 = keys per lane per step in the fixed-length kernel (1, 2 or 4),
  * 5 = ablation mode of the 16/32-byte kernel (0 product, 1 copy-only,
  *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3),
- * 10 = register prefetch of the next chunk in the fixed-length kernel (0/1).
+ * 10 = register prefetch of the next chunk in the fixed-length kernel (0/1),
+ * 11 = bitsliced share of a 16-byte batch in per mille (0 = T-table only),
+ * 14 = variable-length CRC32C kernel (1 length-sorted windows, 0 input order).
  * Returns the previous value or KVH_EINVAL. */
 int         kvh_set_tuning(int knob, int value);
 /* diagnostics: per-wave phase cycle stamps of the last stamped launch */

@@ -216,6 +216,97 @@ k_crc_var(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, u
   }
 }
 
+// kv_crc_c over one key with the next 16-byte piece in flight while the
+// current one steps through the tables.
+__device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, uint32_t r, const CrcLds& T) {
+  uint64_t o = 0;
+  if (len >= 16) {
+    Blk cur = load16_full(p);
+    for (; o + 32 <= len; o += 16) {
+      const Blk nxt = load16_full(p + o + 16);
+      r = T.word(r, cur.w[0]); r = T.word(r, cur.w[1]);
+      r = T.word(r, cur.w[2]); r = T.word(r, cur.w[3]);
+      cur = nxt;
+    }
+    r = T.word(r, cur.w[0]); r = T.word(r, cur.w[1]);
+    r = T.word(r, cur.w[2]); r = T.word(r, cur.w[3]);
+    o += 16;
+  }
+  const uint32_t t = (uint32_t)(len - o);
+  if (t) {
+    const Blk b = load_bytes(p + o, t);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int left = (int)t - 4 * c;
+      if (left >= 4) r = T.word(r, b.w[c]);
+      else if (left > 0) r = T.tail(r, b.w[c], (uint32_t)left);
+    }
+  }
+  return r;
+}
+
+// Variable length, length-sorted per-wave windows (the k_var6 scheme of
+// kvh.hip): one lane per key in input order runs each wave as long as its
+// longest key (zipf 8-256 B: ~25 % of the lane-steps do work).  Each wave
+// counting-sorts windows of WIN consecutive keys by length
+// (wave_sort_window) and takes them 64 at a time in length order; the CRCs
+// go through the wave's LDS slice back to input order and leave as one
+// contiguous run.  NW waves per workgroup: the 128 KiB of replicated tables
+// leave room for NW * 3 KiB of window state.
+template <int WIN, int NW>
+__global__ void __launch_bounds__(NW * 64)
+k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
+                 const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out
+  constexpr int M = WIN / 64;
+  static_assert(WIN <= 256 * 4, "hist slice doubles as the CRC staging area");
+  __shared__ uint32_t lds[kWords];
+  __shared__ uint32_t hist_s[NW][WIN > 256 ? WIN : 256];
+  __shared__ uint32_t roff_s[NW][WIN];
+  __shared__ uint16_t rlen_s[NW][WIN];
+  __shared__ uint16_t ridx_s[NW][WIN];
+  fill_crc(lds);
+  __syncthreads();
+  const CrcLds T(lds);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* hist = hist_s[wv];
+  const uint64_t nwin = (n + WIN - 1) / WIN;
+  for (uint64_t w = (uint64_t)blockIdx.x * NW + wv; w < nwin; w += (uint64_t)gridDim.x * NW) {
+    const uint64_t i0 = w * WIN;
+    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    const uint64_t ws = wave_sort_window<WIN>(offs, i0, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
+    // (running the lane's M keys as interleaved chains was slower: each
+    // lane then steps as long as its longest key, chunk M-1's)
+    uint32_t crc[M], ix[M];
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t pos = 64 * c + lane;
+      ix[c] = 0xffffffffu;
+      if (pos < k) {
+        const uint32_t j = ridx_s[wv][pos];
+        uint64_t len = rlen_s[wv][pos];
+        if (len == 65535u) len = offs[i0 + j + 1] - offs[i0 + j];
+        crc[c] = crc_key_pf(keys + ws + roff_s[wv][pos], len, seeds ? seeds[i0 + j] : seed, T);
+        ix[c] = j;
+      }
+    }
+    wave_lds_sync();  // the records are read; the hist slice becomes the staging area
+#pragma unroll
+    for (int c = 0; c < M; c++)
+      if (ix[c] != 0xffffffffu) hist[ix[c]] = crc[c];
+    wave_lds_sync();
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t j = 64 * c + lane;
+      if (j < k) __builtin_nontemporal_store(hist[j], out + i0 + j);
+    }
+    wave_lds_sync();  // staging read before the next window's histogram
+  }
+}
+
+}  // namespace
+namespace kvh { namespace rt { int g_tune_crc_var = 1; } }
+namespace {
+
 uint32_t grid_crc(uint64_t n, int cus) {
   const uint64_t need = (n + kBlock - 1) / kBlock;
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)cus));
@@ -316,8 +407,15 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
   if (!out || !offsets || !keys) return set_err(KVH_EINVAL);
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_crc_var, dim3(grid_crc(n, cus)), dim3(kBlock), 0, (hipStream_t)stream,
-                     (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  if (g_tune_crc_var == 1)
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 10>), dim3(cus), dim3(640), 0, (hipStream_t)stream,
+                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  else if (g_tune_crc_var == 2)
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 8>), dim3(cus), dim3(512), 0, (hipStream_t)stream,
+                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  else
+    hipLaunchKernelGGL(k_crc_var, dim3(grid_crc(n, cus)), dim3(kBlock), 0, (hipStream_t)stream,
+                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   return launch_done();
 }
 

@@ -1870,6 +1870,7 @@ int kvh_set_tuning(int knob, int value) {
     case 11: if (value < 0 || value > 1000) return KVH_EINVAL; prev = g_tune_bs; g_tune_bs = value; return prev;
     case 12: if (value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_bsw; g_tune_bsw = value; return prev;
     case 13: if (value != 0 && value != 2 && value != 3) return KVH_EINVAL; prev = g_tune_prio; g_tune_prio = value; return prev;
+    case 14: if (value < 0 || value > 2) return KVH_EINVAL; prev = g_tune_crc_var; g_tune_crc_var = value; return prev;
     case 10: prev = g_tune_pf; g_tune_pf = value ? 1 : 0; return prev;
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
     case 9: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_var_mode; g_tune_var_mode = value; return prev;

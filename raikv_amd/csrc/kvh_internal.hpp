@@ -76,6 +76,76 @@ struct LdsK {
   __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
 };
 
+// Cross-lane LDS ordering inside one wave (its lanes' LDS writes visible to
+// its later LDS reads), without a workgroup barrier.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One wave counting-sorts a window of k <= WIN consecutive keys (u64 offsets
+// offs[i0 .. i0+k]) by length bucket min(len, 255), stably by index: LDS
+// atomics rank each key inside its bucket, one wave-wide scan of the 256
+// counts (hist[256], the wave's own) gives the bucket starts.  Writes the
+// records in length order: r_off (u32 offset from the window's first byte),
+// r_len (u16, 65535 = "re-read the offsets"), r_idx (u16 index in window).
+// Returns the window's first byte offset.  Used by the length-sorted
+// variable-length kernels (k_crc_var_sorted; k_var6 inlines the same steps).
+template <int WIN>
+__device__ __forceinline__ uint64_t wave_sort_window(const uint64_t* __restrict__ offs, uint64_t i0, uint32_t k,
+                                                     uint32_t* hist, uint32_t* r_off, uint16_t* r_len,
+                                                     uint16_t* r_idx) {
+  constexpr int M = WIN / 64;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t ws = offs[i0];
+  uint32_t o[M], L[M], r[M];
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    const uint32_t j = lane + 64 * m;
+    const uint32_t jj = j < k ? j : k - 1;
+    const uint64_t a = offs[i0 + jj], e = offs[i0 + jj + 1];
+    o[m] = (uint32_t)(a - ws);
+    L[m] = e - a < 65535 ? (uint32_t)(e - a) : 65535u;
+  }
+#pragma unroll
+  for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
+  wave_lds_sync();
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    const uint32_t j = lane + 64 * m;
+    r[m] = j < k ? atomicAdd(&hist[L[m] < 255u ? L[m] : 255u], 1u) : 0u;
+  }
+  wave_lds_sync();
+  {
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (lane >= (uint32_t)d) inc += y;
+    }
+    uint32_t run = inc - sum;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int m = 0; m < M; m++) {
+    const uint32_t j = lane + 64 * m;
+    if (j < k) {
+      const uint32_t pos = hist[L[m] < 255u ? L[m] : 255u] + r[m];
+      r_off[pos] = o[m];
+      r_len[pos] = (uint16_t)L[m];
+      r_idx[pos] = (uint16_t)j;
+    }
+  }
+  wave_lds_sync();
+  return ws;
+}
+
 namespace rt {
 // thread-local last error (kvh_last_error); returns e
 int set_err(int e);
@@ -85,6 +155,8 @@ int hip_err(hipError_t e);
 int device_cus(int* cus);
 // hipGetLastError after a launch -> 0 or the recorded error
 int launch_done();
+// variable-length CRC32C kernel: 1 = length-sorted windows (default), 0 = lane per key in input order
+extern int g_tune_crc_var;
 }  // namespace rt
 
 }  // namespace kvh

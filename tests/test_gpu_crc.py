@@ -129,3 +129,27 @@ def test_full_size_var_property(kvh):
     for i in range(3):
         s = kvh.kv_crc_c(kh[int(offs[i]):int(offs[i + 1])].tobytes(), s)
     assert c == s
+
+
+@pytest.mark.parametrize("kernel", [0, 1, 2])
+@pytest.mark.parametrize("n", [1, 255, 257, 2561])
+def test_var_kernels_vs_oracle(kvh, kernel, n):
+    """Both variable-length kernels (input order; length-sorted windows, knob
+    14), window tails, keys of 0 bytes and of >= 65535 bytes (the sorted
+    kernel's record saturates and re-reads the offsets), per-key seeds."""
+    rng = np.random.default_rng(n * 3 + kernel)
+    lens = rng.integers(0, 300, n).astype(np.uint64)
+    if n > 2:
+        lens[1] = 0
+        lens[n // 2] = 70001
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    flat = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    prev = kvh.lib.kvh_set_tuning(14, kernel)
+    try:
+        got = u32(kvh.crc_c_var(dev(flat), dev(offs.view(np.int64)), seed=0x1234567))
+        np.testing.assert_array_equal(got, orc_crc_var(ORC, flat, offs, seed=0x1234567))
+        got = u32(kvh.crc_c_var(dev(flat), dev(offs.view(np.int64)), seeds=dev(seeds.view(np.int32))))
+        np.testing.assert_array_equal(got, orc_crc_var(ORC, flat, offs, seeds))
+    finally:
+        kvh.lib.kvh_set_tuning(14, prev)
