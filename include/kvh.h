@@ -85,13 +85,20 @@ int kvh_meow128_var_seeded(const void *keys, const uint64_t *offsets,
 
 /* ---------------------------------------------------------------------
  * Host-buffer pipeline: keys and out in (pageable or pinned) host memory;
- * chunked, double-buffered H2D -> kernel -> D2H through pinned staging on
- * the current device.  Synchronous.  This is the PCIe-inclusive path
- * (keys arrive from a socket / shm segment, hashes feed the cuckoo probe).
+ * chunked H2D -> kernel -> D2H on the current device, one stream per
+ * direction so both PCIe directions run at once.  Synchronous.  This is the
+ * PCIe-inclusive path (keys arrive from a socket / shm segment, hashes feed
+ * the cuckoo probe).  Pinned buffers from kvh_host_alloc are DMA'd directly;
+ * pageable ones go through pinned bounce buffers (about half the rate).
  * ------------------------------------------------------------------- */
 int kvh_meow128_fixed_host(const void *keys, uint32_t key_len, size_t n,
                            uint64_t seed1, uint64_t seed2, uint64_t *out,
                            uint32_t flags);
+/* pinned (page-locked, DMA-able) host memory for kvh_meow128_fixed_host's
+ * key and hash buffers -- the role of raikv's shared-memory segment on the
+ * GPU side; 0 or a negative error.  Free with kvh_host_free. */
+int kvh_host_alloc(void **p, size_t bytes);
+int kvh_host_free(void *p);
 
 /* ---------------------------------------------------------------------
  * Drop-ins for include/raikv/key_hash.h (host pointers, synchronous).  They

@@ -8,6 +8,7 @@ before libkvh.so is loaded so that one HIP runtime serves both.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 import os
 from typing import Iterable, Optional, Sequence, Tuple
 
@@ -77,6 +78,8 @@ def _load():
         "kvh_meow128_batch": (I, [P, P, U32, SZ, P, U32, P, U32, P]),
         "kvh_meow128_var_seeded": (I, [P, P, SZ, P, P, U32, P]),
         "kvh_meow128_fixed_host": (I, [P, U32, SZ, U64, U64, P, U32]),
+        "kvh_host_alloc": (I, [C.POINTER(P), SZ]),
+        "kvh_host_free": (I, [P]),
         "kvh_hash_meow128": (I, [P, SZ, C.POINTER(U64), C.POINTER(U64)]),
         "kvh_hash_meow64": (U64, [P, SZ, U64]),
         "kvh_hash_meow128_2_same_length": (I, [P, P, SZ, P]),
@@ -350,6 +353,19 @@ def meow128_fixed_host(keys: np.ndarray, key_len: int, seed: Tuple[int, int],
                                      out.ctypes.data, KVH_FIXUP if fixup else 0),
           "kvh_meow128_fixed_host")
     return out
+
+
+def host_empty(shape, dtype=np.uint8) -> np.ndarray:
+    """A numpy array over pinned host memory from kvh_host_alloc (freed with
+    the array): the buffers kvh_meow128_fixed_host DMAs at full PCIe rate."""
+    dt = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dt.itemsize
+    ptr = P()
+    check(lib.kvh_host_alloc(C.byref(ptr), max(nbytes, 1)), "kvh_host_alloc")
+    buf = (C.c_uint8 * max(nbytes, 1)).from_address(ptr.value)
+    arr = np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dt).reshape(shape)
+    weakref.finalize(buf, lib.kvh_host_free, ptr.value)
+    return arr
 
 
 # ------------------------------------------------------------- drop-ins

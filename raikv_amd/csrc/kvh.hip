@@ -1441,6 +1441,57 @@ int same_len_host(const void* const* ptrs, size_t cnt, size_t sz, const uint64_t
   return seeded_host(ptrs, lens.data(), cnt, seeds.data(), x, 0);
 }
 
+// Per-device host pipeline state for kvh_meow128_fixed_host (grown on
+// demand, kept for the process lifetime).
+constexpr int kPipeSlots = 16;  // buffer slots allocated; g_tune_pipe_slots of them used
+constexpr int kMaxDev = 64;
+int g_tune_pipe_mib = 16;   // key bytes per pipeline chunk, MiB (knob 15)
+int g_tune_pipe_slots = 4;  // chunks in flight (knob 16)
+struct HostPipe {
+  std::mutex mu;
+  hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
+  hipEvent_t ev_in[kPipeSlots] = {}, ev_k[kPipeSlots] = {}, ev_out[kPipeSlots] = {};
+  uint8_t* dk[kPipeSlots] = {};
+  uint64_t* dout[kPipeSlots] = {};
+  uint8_t* hk[kPipeSlots] = {};
+  uint64_t* ho[kPipeSlots] = {};
+  size_t kcap = 0, ocap = 0, hkcap = 0, hocap = 0;
+  // slots [0, ns) of buffer array b hold `want` bytes each (grow-only)
+  template <class T, class A, class F>
+  static hipError_t regrow(T* (&b)[kPipeSlots], size_t& cap, size_t want, int ns, A alloc, F release) {
+    if (cap < want) {
+      for (int s = 0; s < kPipeSlots; s++) if (b[s]) { (void)release(b[s]); b[s] = nullptr; }
+      cap = want;
+    }
+    for (int s = 0; s < ns; s++) {
+      if (b[s]) continue;
+      const hipError_t e = alloc((void**)&b[s], cap);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  // streams, events and ns slots of buffers for chunks of kb key bytes / ob
+  // hash bytes on the current device
+  int reserve(int ns, size_t kb, size_t ob, bool need_hk, bool need_ho) {
+    hipError_t e = hipSuccess;
+    for (hipStream_t* st : {&s_in, &s_k, &s_out})
+      if (e == hipSuccess && !*st) e = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    for (int s = 0; s < kPipeSlots && e == hipSuccess; s++)
+      for (hipEvent_t* ev : {&ev_in[s], &ev_k[s], &ev_out[s]})
+        if (e == hipSuccess && !*ev) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    auto dmal = [](void** p, size_t b) { return hipMalloc(p, b); };
+    auto dfree = [](void* p) { return hipFree(p); };
+    auto hmal = [](void** p, size_t b) { return hipHostMalloc(p, b, 0); };
+    auto hfree = [](void* p) { return hipHostFree(p); };
+    if (e == hipSuccess) e = regrow(dk, kcap, kb, ns, dmal, dfree);
+    if (e == hipSuccess) e = regrow(dout, ocap, ob, ns, dmal, dfree);
+    if (e == hipSuccess && need_hk) e = regrow(hk, hkcap, kb, ns, hmal, hfree);
+    if (e == hipSuccess && need_ho) e = regrow(ho, hocap, ob, ns, hmal, hfree);
+    return e == hipSuccess ? 0 : hip_err(e);
+  }
+};
+HostPipe g_pipe[kMaxDev];
+
 }  // namespace
 
 // =============================================================== C-ABI
@@ -1595,68 +1646,82 @@ int kvh_meow128_fixed_host(const void* keys, uint32_t key_len, size_t n, uint64_
                            uint64_t* out, uint32_t flags) {
   if (n == 0) return set_err(0);
   if (!keys || !out || key_len == 0) return set_err(KVH_EINVAL);
-  // Chunked pipeline: NS streams, each with its own device key/out buffers.
-  // Host buffers are used directly when pinned (hipHostMalloc / registered);
-  // pageable memory goes through pinned bounce buffers.
-  constexpr int NS = 3;
-  const size_t chunk = std::max<size_t>(1, (size_t)(64u << 20) / key_len);  // ~64 MiB of keys per chunk
+  // Three-stage pipeline over kPipeSlots buffer slots: chunk i is copied in
+  // on the H2D stream, hashed on the compute stream once its copy-in event
+  // fires, and copied out on the D2H stream once its kernel event fires.  One
+  // stream per direction lets the two DMA directions run at once (PCIe is
+  // full duplex: ~57 GB/s each way, ~97 GB/s both; a stream carrying both
+  // directions of its chunks serialised them at ~56 GB/s in all, DESIGN.md
+  // §4.4).  A slot is refilled once its previous chunk's copy-out event has
+  // fired.  Streams, events and buffers persist per device across calls; the
+  // call holds the device's pipeline for its duration.  Host buffers are used
+  // directly when pinned; pageable memory goes through pinned bounce buffers.
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  if (dev < 0 || dev >= kMaxDev) return set_err(KVH_EINVAL);
+  HostPipe& P = g_pipe[dev];
+  std::lock_guard<std::mutex> lk(P.mu);
+  const size_t chunk = std::max<size_t>(1, ((size_t)g_tune_pipe_mib << 20) / key_len);
   hipPointerAttribute_t ak, ao;
-  bool pin_k = hipPointerGetAttributes(&ak, keys) == hipSuccess && ak.type == hipMemoryTypeHost;
-  bool pin_o = hipPointerGetAttributes(&ao, out) == hipSuccess && ao.type == hipMemoryTypeHost;
+  const bool pin_k = hipPointerGetAttributes(&ak, keys) == hipSuccess && ak.type == hipMemoryTypeHost;
+  const bool pin_o = hipPointerGetAttributes(&ao, out) == hipSuccess && ao.type == hipMemoryTypeHost;
   (void)hipGetLastError();
-  hipStream_t st[NS];
-  uint8_t* dk[NS] = {};
-  uint64_t* dout[NS] = {};
-  uint8_t* hk[NS] = {};
-  uint64_t* ho[NS] = {};
-  size_t pend_lo[NS], pend_cnt[NS];
-  int rc = 0;
-  hipError_t e = hipSuccess;
-  for (int s = 0; s < NS; s++) {
-    st[s] = nullptr; pend_cnt[s] = 0; pend_lo[s] = 0;
-    if ((e = hipStreamCreateWithFlags(&st[s], hipStreamNonBlocking)) != hipSuccess) break;
-    if ((e = hipMalloc(&dk[s], chunk * key_len)) != hipSuccess) break;
-    if ((e = hipMalloc(&dout[s], chunk * 16)) != hipSuccess) break;
-    if (!pin_k && (e = hipHostMalloc(&hk[s], chunk * key_len, 0)) != hipSuccess) break;
-    if (!pin_o && (e = hipHostMalloc(&ho[s], chunk * 16, 0)) != hipSuccess) break;
-  }
-  if (e != hipSuccess) rc = hip_err(e);
-  auto drain = [&](int s) -> int {
+  const int slots = std::min(std::max(g_tune_pipe_slots, 2), kPipeSlots);
+  int rc = P.reserve(slots, chunk * key_len, chunk * 16, !pin_k, !pin_o);
+  if (rc) return rc;
+  size_t pend_lo[kPipeSlots] = {}, pend_cnt[kPipeSlots] = {};
+  auto drain = [&](int s) -> int {  // the slot's previous chunk has left the device
     if (!pend_cnt[s]) return 0;
-    hipError_t x = hipStreamSynchronize(st[s]);
+    hipError_t x = hipEventSynchronize(P.ev_out[s]);
     if (x != hipSuccess) return hip_err(x);
-    if (!pin_o) memcpy(out + 2 * pend_lo[s], ho[s], pend_cnt[s] * 16);
+    if (!pin_o) memcpy(out + 2 * pend_lo[s], P.ho[s], pend_cnt[s] * 16);
     pend_cnt[s] = 0;
     return 0;
   };
   size_t idx = 0;
   for (size_t lo = 0; !rc && lo < n; lo += chunk, idx++) {
-    const int s = (int)(idx % NS);
+    const int s = (int)(idx % slots);
     if ((rc = drain(s))) break;
     const size_t cnt = std::min(chunk, n - lo);
     const uint8_t* src = (const uint8_t*)keys + lo * key_len;
-    if (!pin_k) { memcpy(hk[s], src, cnt * key_len); src = hk[s]; }
-    if ((e = hipMemcpyAsync(dk[s], src, cnt * key_len, hipMemcpyHostToDevice, st[s])) != hipSuccess) {
+    if (!pin_k) { memcpy(P.hk[s], src, cnt * key_len); src = P.hk[s]; }
+    uint64_t* dst = pin_o ? out + 2 * lo : P.ho[s];
+    if ((e = hipMemcpyAsync(P.dk[s], src, cnt * key_len, hipMemcpyHostToDevice, P.s_in)) != hipSuccess ||
+        (e = hipEventRecord(P.ev_in[s], P.s_in)) != hipSuccess ||
+        (e = hipStreamWaitEvent(P.s_k, P.ev_in[s], 0)) != hipSuccess) {
       rc = hip_err(e); break;
     }
-    if ((rc = kvh_meow128_fixed(dk[s], key_len, cnt, seed1, seed2, dout[s], flags, st[s]))) break;
-    uint64_t* dst = pin_o ? out + 2 * lo : ho[s];
-    if ((e = hipMemcpyAsync(dst, dout[s], cnt * 16, hipMemcpyDeviceToHost, st[s])) != hipSuccess) {
+    if ((rc = kvh_meow128_fixed(P.dk[s], key_len, cnt, seed1, seed2, P.dout[s], flags, P.s_k))) break;
+    if ((e = hipEventRecord(P.ev_k[s], P.s_k)) != hipSuccess ||
+        (e = hipStreamWaitEvent(P.s_out, P.ev_k[s], 0)) != hipSuccess ||
+        (e = hipMemcpyAsync(dst, P.dout[s], cnt * 16, hipMemcpyDeviceToHost, P.s_out)) != hipSuccess ||
+        (e = hipEventRecord(P.ev_out[s], P.s_out)) != hipSuccess) {
       rc = hip_err(e); break;
     }
     pend_lo[s] = lo; pend_cnt[s] = cnt;
   }
-  for (int s = 0; s < NS; s++) {
-    int r2 = st[s] ? drain(s) : 0;
+  for (int s = 0; s < slots; s++) {
+    const int r2 = drain(s);
     if (!rc) rc = r2;
-    // teardown: the first error (rc) is what the caller sees
-    if (st[s]) (void)hipStreamDestroy(st[s]);
-    if (dk[s]) (void)hipFree(dk[s]);
-    if (dout[s]) (void)hipFree(dout[s]);
-    if (hk[s]) (void)hipHostFree(hk[s]);
-    if (ho[s]) (void)hipHostFree(ho[s]);
+  }
+  if (rc) {  // leave the pipeline idle for the next call
+    (void)hipStreamSynchronize(P.s_in); (void)hipStreamSynchronize(P.s_k); (void)hipStreamSynchronize(P.s_out);
   }
   return rc ? rc : set_err(0);
+}
+
+int kvh_host_alloc(void** p, size_t bytes) {
+  if (!p) return set_err(KVH_EINVAL);
+  *p = nullptr;
+  const hipError_t e = hipHostMalloc(p, bytes ? bytes : 1, 0);
+  return e == hipSuccess ? set_err(0) : hip_err(e);
+}
+
+int kvh_host_free(void* p) {
+  if (!p) return set_err(0);
+  const hipError_t e = hipHostFree(p);
+  return e == hipSuccess ? set_err(0) : hip_err(e);
 }
 
 int kvh_hash_meow128(const void* p, size_t sz, uint64_t* h1, uint64_t* h2) {
@@ -1871,6 +1936,8 @@ int kvh_set_tuning(int knob, int value) {
     case 12: if (value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_bsw; g_tune_bsw = value; return prev;
     case 13: if (value != 0 && value != 2 && value != 3) return KVH_EINVAL; prev = g_tune_prio; g_tune_prio = value; return prev;
     case 14: if (value < 0 || value > 2) return KVH_EINVAL; prev = g_tune_crc_var; g_tune_crc_var = value; return prev;
+    case 16: if (value < 2 || value > 16) return KVH_EINVAL; prev = g_tune_pipe_slots; g_tune_pipe_slots = value; return prev;
+    case 15: if (value < 1 || value > 1024) return KVH_EINVAL; prev = g_tune_pipe_mib; g_tune_pipe_mib = value; return prev;
     case 10: prev = g_tune_pf; g_tune_pf = value ? 1 : 0; return prev;
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
     case 9: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_var_mode; g_tune_var_mode = value; return prev;

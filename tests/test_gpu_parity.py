@@ -221,6 +221,24 @@ def test_host_pipeline_pinned_and_pageable(kvh):
     po = torch.empty((n, 2), dtype=torch.int64).pin_memory()
     got2 = kvh.meow128_fixed_host(pk.numpy(), L, STATIC, out=po.numpy().view(np.uint64))
     np.testing.assert_array_equal(got2, want)
+    # kvh_host_alloc buffers; chunk sizes that leave a ragged last chunk; slot
+    # reuse (more chunks than slots) and one chunk only
+    hk = kvh.host_empty((n * L,), np.uint8)
+    hk[:] = kb
+    ho = kvh.host_empty((n, 2), np.uint64)
+    for mib, slots in ((1, 2), (4, 4), (64, 16)):
+        pm, ps = kvh.lib.kvh_set_tuning(15, mib), kvh.lib.kvh_set_tuning(16, slots)
+        try:
+            ho[:] = 0
+            kvh.meow128_fixed_host(hk, L, STATIC, out=ho, fixup=(mib == 4))
+            np.testing.assert_array_equal(ho, want if mib != 4 else u64(kvh.meow128_fixed(dev(kb), L, STATIC,
+                                                                                           fixup=True)))
+        finally:
+            kvh.lib.kvh_set_tuning(15, pm)
+            kvh.lib.kvh_set_tuning(16, ps)
+    # mixed: pinned keys, pageable output
+    got3 = kvh.meow128_fixed_host(hk, L, STATIC)
+    np.testing.assert_array_equal(got3, want)
 
 
 def test_full_size_c1_properties(kvh):
