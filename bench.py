@@ -262,8 +262,8 @@ def load_traffic(config_name: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 mkdir -p $OUT
 for c in $CFGS; do
   mkdir -p $OUT/$c
-  B="python3 bench.py --config $c --steps 30 --warmup 30 --no-cpu-baseline"
+  B="python3 bench.py --config $c --no-cpu-baseline"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- $B > $OUT/$c/bench.json 2> $OUT/$c/trace.err || exit 1
   R="python3 tools/run_kernel.py --config $c --reps 5"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- $R > $OUT/$c/fetch.log 2>&1 || exit 1
