@@ -36,6 +36,7 @@ METRIC = "128-bit key hashes/sec device-resident, 16–64B keys; GB/s vs HBM pea
 METRIC_F1 = "keys/sec -> hash + cuckoo table positions, device-resident (SURVEY.md §8 f1)"
 METRIC_F4 = "CRC32C (kv_crc_c) keys/sec, device-resident (SURVEY.md §8 f4)"
 METRIC_F3 = "tokens/sec: text -> tokenize -> NUL-terminated key hashes, device-resident (SURVEY.md §8 f3)"
+METRIC_F2 = "keys/sec ordered by hash-table slot with adjacent duplicates marked, device-resident (SURVEY.md §8 f2)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 # LDS table-lookup ceiling: ds_read_b32 serves 32 lanes per LDS cycle per CU
 # (MI355X_MICROARCH.md §LDS, 128 B/clk), 256 CUs, 2.4 GHz peak engine clock
@@ -59,6 +60,10 @@ CONFIGS = {
     "f1p": dict(workload="F1p: 100M resident fixed-up (h1,h2) -> cuckoo arity-4 table positions "
                          "(64 GiB map, 4 buckets), u64 positions",
                 n=100_000_000, key_len=16, arity=1, var=False, positions="only"),
+    # kv_ht_radix_sort + ctest's duplicate marking on a hashed batch
+    "f2": dict(workload="F2: 100M resident fixed-up (h1,h2) pairs of 16-byte keys (1% duplicates) + u64 items -> "
+                        "ordered by ht_mod(h1) (64 GiB map), adjacent duplicates marked (kvh_ht_sort, KVH_DEDUP)",
+               n=100_000_000, key_len=16, arity=1, var=False, sort=True),
     # batched CRC32C (kv_crc_c) on the C1 / C2 key shapes
     "f4": dict(workload="F4: 100M fixed 16-byte keys -> kv_crc_c (CRC32C, seed 0), u32 out",
                n=100_000_000, key_len=16, arity=1, var=False, crc=True),
@@ -156,6 +161,34 @@ def cpu_baseline_positions(cfg, seed, seconds: float, geom):
     return {"value": total_n / total_t, "unit": "key/s", "cores": threads, "kind": kind,
             "sample": f"{total_n} keys ({n} distinct) x {what}, arity {geom.cuckoo_arity}, "
                       f"{threads} threads, {total_t:.1f} s"}
+
+
+def cpu_baseline_sort(seconds: float, geom, hashes_np):
+    """The reference's kv_ht_radix_sort + ctest.c:96-104's duplicate marking
+    (oracle/ref_cuckoo.cpp ref_ht_sort_bench, compiled from radix_sort.cpp
+    and the KV-core sources), one thread (the reference sort is serial), on
+    4M-pair slices of the same hashes."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import load_ref_ht  # checker only
+    import ctypes as C
+    ref = load_ref_ht()
+    if ref is None:
+        return {"value": None, "error": "oracle/_ref/libkvref_ht.so not built"}
+    m = 4_000_000
+    d = np.zeros(1, np.uint64)
+    total_t, total_n, k = 0.0, 0, 0
+    while total_t < seconds:
+        sl = np.ascontiguousarray(hashes_np[(k * m) % (len(hashes_np) - m):][:m])
+        t = ref.ref_ht_sort_bench(geom.ht_size, geom.ht_mod_mask, geom.ht_mod_fraction, geom.ht_mod_shift,
+                                  sl.ctypes.data, m, d.ctypes.data)
+        if t < 0:
+            return {"value": None, "error": "ref_ht_sort_bench failed"}
+        total_t += t
+        total_n += m
+        k += 1
+    return {"value": total_n / total_t, "unit": "key/s", "cores": 1, "kind": "reference",
+            "sample": f"{total_n} hash pairs in 4M-pair slices x kv_ht_radix_sort + adjacent-duplicate marking "
+                      f"(64 GiB map geometry), 1 thread, {total_t:.1f} s"}
 
 
 def cpu_baseline_crc(cfg, seconds: float):
@@ -315,6 +348,20 @@ def main():
         # text read twice (count + emit passes) + spans written/read + key bytes gathered + hashes
         alg_bytes = n + 12 * ntok + 16 * ntok
         cfg["tokens"] = ntok
+    elif cfg.get("sort"):
+        geom = kvh.HtGeom.from_map(**F1_GEOM)
+        keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=gen)
+        s_h = kvh.meow128_fixed(keys, L, seed, fixup=True)
+        del keys
+        nd = n // 100  # 1 % duplicates
+        s_h[torch.randperm(n, device="cuda", generator=gen)[:nd]] = s_h[torch.randint(0, n, (nd,), device="cuda",
+                                                                                      generator=gen)]
+        s_items = torch.arange(n, dtype=torch.int64, device="cuda")
+        sorter = kvh.HtSorter(geom, n)
+        s_ho, s_io = torch.empty_like(s_h), torch.empty_like(s_items)
+        # hashes + items in, hashes + items out
+        alg_bytes = 2 * 24 * n
+        run = lambda out: sorter.sort(s_h, s_items, dedup=True, out=s_ho, items_out=s_io)
     elif cfg.get("crc"):
         crc_out = torch.empty((n,), dtype=torch.int32, device="cuda")
         if cfg["var"]:
@@ -359,7 +406,8 @@ def main():
             run = lambda out: kvh.meow128_fixed(keys, L, seed, out=out)
         else:
             run = lambda out: kvh.meow128_multiseed(keys, L, list(C3_SEEDS[:arity]), out=out)
-    out = None if (cfg.get("positions") or cfg.get("crc") or cfg.get("ingest")) else \
+    keyed = cfg.get("positions") or cfg.get("crc") or cfg.get("ingest") or cfg.get("sort")
+    out = None if keyed else \
         torch.empty((n, arity, 2) if arity > 1 else (n, 2), dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
 
@@ -389,9 +437,10 @@ def main():
     traffic, tsrc = load_traffic(args.config)
     res = {
         "metric": METRIC_F1 if cfg.get("positions") else (METRIC_F4 if cfg.get("crc") else
-                                                          (METRIC_F3 if cfg.get("ingest") else METRIC)),
+                                                          (METRIC_F3 if cfg.get("ingest") else
+                                                           (METRIC_F2 if cfg.get("sort") else METRIC))),
         "value": value,
-        "unit": "key/s" if (cfg.get("positions") or cfg.get("crc") or cfg.get("ingest")) else "hash/s",
+        "unit": "key/s" if keyed else "hash/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -424,6 +473,9 @@ def main():
                 res["cpu_baseline"] = cpu_baseline_crc(cfg, args.cpu_seconds)
             elif cfg.get("ingest"):
                 res["cpu_baseline"] = cpu_baseline_ingest(args.cpu_seconds, text)
+            elif cfg.get("sort"):
+                res["cpu_baseline"] = cpu_baseline_sort(args.cpu_seconds, geom,
+                                                        s_h[:16_000_000].cpu().numpy().view(np.uint64))
             else:
                 res["cpu_baseline"] = cpu_baseline(cfg, seed, args.cpu_seconds)
         except Exception as e:  # report, never hide

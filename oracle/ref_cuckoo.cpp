@@ -221,3 +221,40 @@ extern "C" int ref_ht_sort(uint64_t map_size, uint32_t entry_size, float ratio, 
   ::free(ht);
   return 0;
 }
+
+/* f2 CPU baseline: the reference's kv_ht_radix_sort (radix_sort.cpp:31-41)
+ * + ctest.c:96-104's adjacent-duplicate marking over n (h1, h2) pairs with
+ * their indices as items, against a header that carries only the table
+ * geometry (as ref_cuckoo_bench).  The reference sort is single-threaded;
+ * the array fill is not timed.  Returns seconds (or -1); *dup_out = count. */
+extern "C" double ref_ht_sort_bench(uint64_t ht_size, uint64_t mask, uint64_t frac, uint32_t shift,
+                                    const uint64_t *h, size_t n, uint64_t *dup_out) {
+  const size_t hdr_bytes = KV_HT_HDR_SIZE + KV_HT_CTX_SIZE + KV_HT_STATS_SIZE;
+  HashTab *ht = (HashTab *) ::aligned_alloc(4096, hdr_bytes);
+  kv_ht_sort_t *ar = (kv_ht_sort_t *) ::malloc(sizeof(kv_ht_sort_t) * (n ? n : 1));
+  if (ht == NULL || ar == NULL) { ::free(ht); ::free(ar); return -1.0; }
+  ::memset((void *) ht, 0, hdr_bytes);
+  ht->hdr.ht_size = ht_size;
+  ht->hdr.ht_mod_mask = mask;
+  ht->hdr.ht_mod_fraction = frac;
+  ht->hdr.ht_mod_shift = (uint8_t) shift;
+  for (size_t i = 0; i < n; i++) {
+    ar[i].key = h[2 * i];
+    ar[i].key2 = h[2 * i + 1];
+    ar[i].item = (void *) (uintptr_t) i;
+  }
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  kv_ht_radix_sort(ar, (uint32_t) n, (kv_hash_tab_t *) ht);
+  uint64_t dups = 0;
+  for (size_t k = 1; k < n; k++)
+    if (ar[k - 1].key == ar[k].key && ar[k - 1].key2 == ar[k].key2) {
+      ar[k - 1].key = 0;
+      dups++;
+    }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  *dup_out = dups;
+  ::free(ar);
+  ::free(ht);
+  return (double) (t1.tv_sec - t0.tv_sec) + 1e-9 * (double) (t1.tv_nsec - t0.tv_nsec);
+}

@@ -12,15 +12,20 @@
 // the reference's order, so every adjacent-equal pair the reference could
 // find is adjacent here, and all duplicates of a key are contiguous.
 //   1. k_sort_keys   key64 = slot << (64 - sbits) | (h1 << 1) >> sbits,
-//                    idx = i (u32)
-//   2. radix sort of (key64, idx) pairs: rocPRIM's onesweep
-//      rocprim::radix_sort_pairs (the library primitive; ROCm's own)
-//   3. k_sort_gather records[j] = (h1, h2, item) of idx[j]
-//   4. k_sort_fixup  runs of equal key64 (equal slot and equal top h1
-//                    bits: duplicates, in practice) insertion-sorted by the
-//                    full comparator; O(run) when the run is all equal
-//   5. k_sort_emit   hashes_out / items_out, with KVH_DEDUP the h1 of an
-//                    element equal to its successor set to 0 and counted
+//                    kept: that prefix; idx = i (u32)
+//   2. radix sort of (key64, idx) pairs over a prefix of key64 only: the
+//      slot bits and max(1, log2(n) + 5 - sbits) bits of h1 (100M keys, 64 GiB
+//      table: 4 onesweep passes instead of 8): rocPRIM's
+//      rocprim::radix_sort_pairs (the library primitive; ROCm's own), stable
+//   3. k_sort_pack   (with items) (h1, h2, item) -> 32-byte records
+//   4. k_sort_place  hashes_out / items_out[j] = record idx[j] (one random
+//                    read per element)
+//   5. k_sort_fixup  runs of equal sorted prefix (equal slot and equal top
+//                    h1 bits: ≈3 % of the elements, and duplicates)
+//                    insertion-sorted in the outputs by the full comparator
+//                    (O(run) when the run is all equal): the order is a full
+//                    64-bit sort's; with KVH_DEDUP the h1 of an element equal
+//                    to its successor set to 0 and counted
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -39,77 +44,111 @@ namespace {
 
 constexpr int kSB = 256;
 
-struct Rec {
-  uint64_t h1, h2, item;
+// (h1, h2, item) padded to 32 bytes: one aligned random read per record
+struct __attribute__((aligned(16))) Rec {
+  uint64_t h1, h2, item, pad;
 };
 
-__device__ __forceinline__ bool rec_less(const Rec& a, const Rec& b) {
-  const uint64_t a0 = a.h1 << 1, b0 = b.h1 << 1;
+__device__ __forceinline__ bool rec_less(uint64_t a1, uint64_t a2, uint64_t b1, uint64_t b2) {
+  const uint64_t a0 = a1 << 1, b0 = b1 << 1;
   if (a0 != b0) return a0 < b0;
-  if (a.h1 != b.h1) return a.h1 < b.h1;
-  return a.h2 < b.h2;
+  if (a1 != b1) return a1 < b1;
+  return a2 < b2;
 }
 
+// key = the top (64 - lo) bits of slot << (64 - sbits) | (h1 << 1) >> sbits,
+// shifted down to bit 0: the radix sort then runs over bits [0, 64 - lo).
+// (Not [lo, 64) in place: rocPRIM's merge-sort path, taken for n <= 1M,
+// builds its mask as (1 << (begin_bit + bits)) - 1, undefined at 64.)
 __global__ void __launch_bounds__(kSB)
-k_sort_keys(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sbits, uint64_t* __restrict__ key,
-            uint32_t* __restrict__ idx) {
+k_sort_keys(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sbits, uint32_t lo,
+            uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
   const uint64_t i = (uint64_t)blockIdx.x * kSB + threadIdx.x;
   if (i >= n) return;
   const uint64_t h1 = h[2 * i];
   const uint64_t slot = ht_mod(g, h1);
-  key[i] = sbits >= 64 ? slot : (slot << (64 - sbits)) | ((h1 << 1) >> sbits);
+  const uint64_t k64 = sbits >= 64 ? slot : (slot << (64 - sbits)) | ((h1 << 1) >> sbits);
+  key[i] = k64 >> lo;
   idx[i] = (uint32_t)i;
 }
 
+// input order: (h1, h2, item) -> 32-byte records (coalesced both ways)
 __global__ void __launch_bounds__(kSB)
-k_sort_gather(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, const uint32_t* __restrict__ idx,
-              uint64_t n, Rec* __restrict__ rec) {
+k_sort_pack(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, Rec* __restrict__ rec) {
+  const uint64_t i = (uint64_t)blockIdx.x * kSB + threadIdx.x;
+  if (i >= n) return;
+  Rec r;
+  r.h1 = h[2 * i];
+  r.h2 = h[2 * i + 1];
+  r.item = items[i];
+  r.pad = 0;
+  rec[i] = r;
+}
+
+// sorted position j <- record idx[j]: one random read (a packed record, or
+// the hash pair when the items are the indices), coalesced writes
+__global__ void __launch_bounds__(kSB)
+k_sort_place(const uint64_t* __restrict__ h, const Rec* __restrict__ rec, const uint32_t* __restrict__ idx,
+             uint64_t n, uint64_t* __restrict__ h_out, uint64_t* __restrict__ items_out) {
   const uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x;
   if (j >= n) return;
   const uint32_t s = idx[j];
-  Rec r;
-  r.h1 = h[2 * (uint64_t)s];
-  r.h2 = h[2 * (uint64_t)s + 1];
-  r.item = items ? items[s] : (uint64_t)s;
-  rec[j] = r;
-}
-
-__global__ void __launch_bounds__(kSB)
-k_sort_fixup(const uint64_t* __restrict__ key, uint64_t n, Rec* __restrict__ rec) {
-  const uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x;
-  if (j + 1 >= n || key[j + 1] != key[j] || (j > 0 && key[j - 1] == key[j])) return;  // run starts only
-  uint64_t e = j + 2;
-  while (e < n && key[e] == key[j]) e++;
-  for (uint64_t a = j + 1; a < e; a++) {  // insertion sort of [j, e)
-    const Rec v = rec[a];
-    uint64_t b = a;
-    while (b > j && rec_less(v, rec[b - 1])) {
-      rec[b] = rec[b - 1];
-      b--;
-    }
-    if (b != a) rec[b] = v;
+  uint64_t h1, h2, it;
+  if (rec) {
+    const Rec r = rec[s];
+    h1 = r.h1; h2 = r.h2; it = r.item;
+  } else {
+    h1 = h[2 * (uint64_t)s]; h2 = h[2 * (uint64_t)s + 1]; it = s;
   }
+  h_out[2 * j] = h1;
+  h_out[2 * j + 1] = h2;
+  if (items_out) items_out[j] = it;
 }
 
+// Runs of equal sorted prefix (equal slot and top h1 bits) are put in the
+// full order (h1 << 1, h1, h2) by insertion sort -- O(run) for an all-equal
+// run -- and, with dedup, every element equal (h1, h2) to its successor gets
+// h1 = 0 (ctest.c:96-104).  Equal pairs share a prefix, so runs are the only
+// place duplicates occur.  Grid-stride; one atomic per workgroup.
 __global__ void __launch_bounds__(kSB)
-k_sort_emit(const Rec* __restrict__ rec, uint64_t n, uint64_t* __restrict__ h, uint64_t* __restrict__ items,
-            uint32_t dedup, unsigned long long* __restrict__ dups) {
-  const uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x;
+k_sort_fixup(const uint64_t* __restrict__ key, uint64_t n, uint64_t* __restrict__ h, uint64_t* __restrict__ items,
+             uint32_t dedup, unsigned long long* __restrict__ dups) {
+  __shared__ uint32_t wsum[kSB / 64];
   uint32_t d = 0;
-  if (j < n) {
-    const Rec r = rec[j];
-    uint64_t h1 = r.h1;
-    if (dedup && j + 1 < n) {
-      const Rec s = rec[j + 1];
-      if (s.h1 == r.h1 && s.h2 == r.h2) { h1 = 0; d = 1; }
+  const uint64_t stride = (uint64_t)gridDim.x * kSB;
+  for (uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x; j + 1 < n; j += stride) {
+    if (key[j + 1] != key[j] || (j > 0 && key[j - 1] == key[j])) continue;  // run starts only
+    uint64_t e = j + 2;
+    while (e < n && key[e] == key[j]) e++;
+    for (uint64_t a = j + 1; a < e; a++) {  // insertion sort of [j, e)
+      const uint64_t v1 = h[2 * a], v2 = h[2 * a + 1], vi = items ? items[a] : 0;
+      uint64_t b = a;
+      while (b > j && rec_less(v1, v2, h[2 * (b - 1)], h[2 * (b - 1) + 1])) {
+        h[2 * b] = h[2 * (b - 1)];
+        h[2 * b + 1] = h[2 * (b - 1) + 1];
+        if (items) items[b] = items[b - 1];
+        b--;
+      }
+      if (b != a) {
+        h[2 * b] = v1;
+        h[2 * b + 1] = v2;
+        if (items) items[b] = vi;
+      }
     }
-    h[2 * j] = h1;
-    h[2 * j + 1] = r.h2;
-    if (items) items[j] = r.item;
+    if (dedup) {
+      for (uint64_t a = j; a + 1 < e; a++)
+        if (h[2 * a] == h[2 * (a + 1)] && h[2 * a + 1] == h[2 * (a + 1) + 1]) { h[2 * a] = 0; d++; }
+    }
   }
   if (dedup && dups) {
     for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
-    if ((threadIdx.x & 63) == 0 && d) atomicAdd(dups, (unsigned long long)d);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = d;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < kSB / 64; w++) t += wsum[w];
+      if (t) atomicAdd(dups, (unsigned long long)t);
+    }
   }
 }
 
@@ -172,25 +211,43 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   g.shift = geom->ht_mod_shift;
   g.buckets = geom->cuckoo_buckets;
   const uint32_t grid = (uint32_t)((n + kSB - 1) / kSB);
-  hipLaunchKernelGGL(k_sort_keys, dim3(grid), dim3(kSB), 0, st, hashes, (uint64_t)n, g, slot_bits(geom->ht_size),
-                     kin, iin);
+  // Sort a prefix of key64 (shifted down to bits [0, nb)): all slot bits
+  // plus enough h1 bits that the prefix space holds >= 32x n values, so
+  // equal-prefix runs stay rare (≈3 % of the elements, mostly pairs);
+  // k_sort_fixup orders them by the full comparator.  100M keys into a
+  // 64 GiB table: 32 bits, 4 radix passes instead of 8.
+  const uint32_t sb = slot_bits(geom->ht_size);
+  uint32_t lg = 0;
+  while (lg < 63 && (1ull << lg) < (uint64_t)n) lg++;
+  uint32_t nb = g_tune_sort_bits ? sb + (uint32_t)g_tune_sort_bits : std::max(sb + 1, lg + 5);
+  if (nb > 64) nb = 64;
+  const uint32_t lo = 64u - nb;
+  hipLaunchKernelGGL(k_sort_keys, dim3(grid), dim3(kSB), 0, st, hashes, (uint64_t)n, g, sb, lo, kin, iin);
   rc = launch_done();
   if (rc) return rc;
+  if (items) {  // carried items: packed with their hashes for a single random read per record
+    hipLaunchKernelGGL(k_sort_pack, dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, rec);
+    rc = launch_done();
+    if (rc) return rc;
+  }
   size_t tb = L.tmp_bytes;
-  hipError_t e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, kin, kout, iin, iout, n, 0u, 64u, st);
+  hipError_t e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, kin, kout, iin, iout, n, 0u, 64u - lo, st);
   if (e != hipSuccess) return hip_err(e);
-  hipLaunchKernelGGL(k_sort_gather, dim3(grid), dim3(kSB), 0, st, hashes, items, iout, (uint64_t)n, rec);
+  hipLaunchKernelGGL(k_sort_place, dim3(grid), dim3(kSB), 0, st, hashes, items ? rec : (const Rec*)nullptr, iout,
+                     (uint64_t)n, h_out, items_out);
   rc = launch_done();
   if (rc) return rc;
-  hipLaunchKernelGGL(k_sort_fixup, dim3(grid), dim3(kSB), 0, st, kout, (uint64_t)n, rec);
-  rc = launch_done();
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_sort_emit, dim3(grid), dim3(kSB), 0, st, rec, (uint64_t)n, h_out, items_out,
+  int cus = 0;
+  if ((rc = device_cus(&cus))) return rc;
+  const uint32_t fgrid = (uint32_t)std::min<uint64_t>(grid, (uint64_t)cus * 8);
+  hipLaunchKernelGGL(k_sort_fixup, dim3(fgrid), dim3(kSB), 0, st, kout, (uint64_t)n, h_out, items_out,
                      dedup ? 1u : 0u, (unsigned long long*)dup_count);
   return launch_done();
 }
 
 }  // namespace
+
+namespace kvh { namespace rt { int g_tune_sort_bits = 0; } }
 
 extern "C" {
 

@@ -157,6 +157,8 @@ int device_cus(int* cus);
 int launch_done();
 // variable-length CRC32C kernel: 1 = length-sorted windows (default), 0 = lane per key in input order
 extern int g_tune_crc_var;
+// table-order sort: h1 bits sorted below the slot bits (0 = by batch size; 64 = the full key)
+extern int g_tune_sort_bits;
 }  // namespace rt
 
 }  // namespace kvh

@@ -137,6 +137,8 @@ def load_ref_ht():
     lib.ref_cuckoo_bench.argtypes = [U64, U64, U64, C.c_uint32, C.c_uint16, C.c_uint8, P, SZ, SZ, U64, U64, P, P,
                                      C.c_int]
     lib.ref_cuckoo_bench.restype = C.c_double
+    lib.ref_ht_sort_bench.argtypes = [U64, U64, U64, C.c_uint32, P, SZ, P]
+    lib.ref_ht_sort_bench.restype = C.c_double
     return lib
 
 

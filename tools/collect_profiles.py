@@ -11,6 +11,9 @@ os.makedirs(dst, exist_ok=True)
 HOT = ("k_fixed", "k_var", "k_generic", "k_fixed_ms", "k_fixed_dma")
 HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",), "f4": ("k_crc_fixed",), "f4v": ("k_crc_var",),
               "f3": ("k_tok<true>", "k_keysrc"), "c2": ("k_var6",), "c3": ("k_fixed_lanes",)}
+# configs whose unit of work is one call of several kernels: (kernel name parts,
+# calls in the PMC run (run_kernel.py --reps), calls in the traced bench run (W + K))
+MULTI = {"f2": (("k_sort", "onesweep", "radix", "rocprim"), 5, 200)}
 tpath = os.path.join(root, "profiles", "pmc_traffic.json")
 spath = os.path.join(dst, "summary.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
@@ -25,6 +28,19 @@ for c in sorted(os.listdir(src)):
     if bj:
         shutil.copy(os.path.join(d, "bench.json"), os.path.join(dst, f"{c}_bench_under_rocprof.json"))
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
+    if c in MULTI:  # one call = several kernels: per-call sums over the call's kernels
+        names, reps, calls = MULTI[c]
+        pmc = json.load(open(os.path.join(d, "pmc_summary.json")))
+        hbm = sum((v["FETCH_SIZE"] * 2 + v["WRITE_SIZE"]) * 1024 * v["_dispatches"] / reps
+                  for k, v in pmc.items() if any(h in k for h in names) and "FETCH_SIZE" in v)
+        traffic[c] = {"hbm_bytes_per_launch": hbm, "kernel": "+".join(names),
+                      "source": f"profiles/{rnd}/{c}_pmc_summary.json (sum over the call's kernels: "
+                                f"(FETCH_SIZE x2 + WRITE_SIZE) x1024 x dispatches / {reps} calls)"}
+        tot = sum(float(r["TotalDurationNs"]) for r in stats if any(h in r["Name"] for h in names))
+        summary[c] = {"kernel": "+".join(names), "avg_ns": tot / calls, "calls": calls, "hbm_bytes_per_launch": hbm,
+                      "clock_GHz_est": None, "lds_util": None,
+                      "kernels": {r["Name"][:80]: int(r["Calls"]) for r in stats if any(h in r["Name"] for h in names)}}
+        continue
     hot_names = HOT_BY_CFG.get(c, HOT)
     hot = [r for r in stats if any(h in r["Name"] for h in hot_names)]
     pmc = json.load(open(os.path.join(d, "pmc_summary.json")))

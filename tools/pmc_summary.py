@@ -15,4 +15,7 @@ for path in sys.argv[1:]:
 out = {}
 for k, cs in rows.items():
     out[k[:120]] = {c: sum(v) / len(v) for c, v in cs.items()}
+    # dispatches of this kernel in the profiled run (rows of its first counter;
+    # one row per dispatch per counter)
+    out[k[:120]]["_dispatches"] = max(len(v) for v in cs.values())
 print(json.dumps(out, indent=1))

@@ -34,10 +34,21 @@ g = torch.Generator(device="cuda")
 g.manual_seed(1)
 cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1),
        "f1": (100_000_000, 16, -1), "f1p": (100_000_000, 16, -2), "f4": (100_000_000, 16, -4),
-       "f4v": (100_000_000, 0, -4), "f3": (1 << 30, 0, -3)}
+       "f4v": (100_000_000, 0, -4), "f3": (1 << 30, 0, -3), "f2": (100_000_000, 16, -5)}
 n, L, ar = cfg[a.config]
 n = a.n or n
-if ar == -3:  # ingest: tokenize + NUL-terminated span hashes
+if ar == -5:  # table order, as bench.py's f2
+    geom = kvh.HtGeom.from_map(64 << 30, 64, 1.0, 4, 4)
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    sh = kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, fixup=True)
+    del keys
+    nd = n // 100
+    sh[torch.randperm(n, device="cuda", generator=g)[:nd]] = sh[torch.randint(0, n, (nd,), device="cuda", generator=g)]
+    si = torch.arange(n, dtype=torch.int64, device="cuda")
+    sorter = kvh.HtSorter(geom, n)
+    sho, sio = torch.empty_like(sh), torch.empty_like(si)
+    f = lambda: sorter.sort(sh, si, dedup=True, out=sho, items_out=sio)
+elif ar == -3:  # ingest: tokenize + NUL-terminated span hashes
     r = torch.randint(0, 8, (n,), dtype=torch.uint8, device="cuda", generator=g)
     text = torch.where(r == 0, 32, torch.where(r == 1, 10, 97 + r)).to(torch.uint8)
     del r
