@@ -354,7 +354,11 @@ int         kvh_device_synchronize(void);
  *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3),
  * 10 = register prefetch of the next chunk in the fixed-length kernel (0/1),
  * 11 = bitsliced share of a 16-byte batch in per mille (0 = T-table only),
- * 14 = variable-length CRC32C kernel (1 length-sorted windows, 0 input order).
+ * 14 = variable-length CRC32C kernel (1 length-sorted windows, 0 input order),
+ * 15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort key bits (0 auto),
+ * 18 = span-hash kernel (2/1 short spans in place + per-wave long queue,
+ *      loads 2/1 chunks ahead; 0 lane per span),
+ * 19 = tokenizer (1 wave-chunked, 0 workgroup-chunked).
  * Returns the previous value or KVH_EINVAL. */
 int         kvh_set_tuning(int knob, int value);
 /* diagnostics: per-wave phase cycle stamps of the last stamped launch */

@@ -36,15 +36,21 @@ constexpr uint64_t kTokChunk = 16 * kTokPass;               // 64 KiB per workgr
 constexpr int kScanBlock = 1024;
 constexpr int64_t kNoStart = INT64_MIN / 2;
 
-__device__ __forceinline__ bool is_ws(uint32_t c) { return c == ' ' || c == '\n' || c == '\t'; }
+__device__ __forceinline__ bool is_ws(uint32_t c) { return (c == ' ') | (c == '\n') | (c == '\t'); }
 
-// 4 bytes -> 4-bit mask of separator bytes (SWAR: a byte equal to c has
-// (x ^ c*0x01010101) == 0 in that lane)
+// 4 bytes -> 4-bit mask of separator bytes, branch-free SWAR: for each
+// separator c, z = w ^ c*0x01010101 has a zero byte exactly where w holds c,
+// and ((z & 0x7f7f7f7f) + 0x7f7f7f7f) | z has that byte's top bit clear
+// exactly then (no carry crosses a byte).  The top bits of the bytes that are
+// a separator (bits 7, 15, 23, 31) are gathered into bits 0-3 by one
+// multiply whose partial products never overlap.
 __device__ __forceinline__ uint32_t ws_bits(uint32_t w) {
-  uint32_t m = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) m |= (uint32_t)is_ws((w >> (8 * k)) & 255u) << k;
-  return m;
+  const uint32_t z0 = w ^ 0x20202020u, z1 = w ^ 0x0a0a0a0au, z2 = w ^ 0x09090909u;
+  const uint32_t n0 = ((z0 & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z0;
+  const uint32_t n1 = ((z1 & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z1;
+  const uint32_t n2 = ((z2 & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z2;
+  const uint32_t t = (~(n0 & n1 & n2) & 0x80808080u) >> 7;  // bits 0, 8, 16, 24
+  return (t * 0x00204081u) >> 21 & 15u;
 }
 
 // Segments are 16-byte blocks at ABSOLUTE 16-byte alignment, so every load
@@ -86,6 +92,15 @@ __device__ __forceinline__ int64_t wave_max_scan(int64_t v, uint32_t lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const int64_t y = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v = v > y ? v : y;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int32_t wave_max_scan32(int32_t v, uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int32_t y = __shfl_up(v, d, 64);
     if (lane >= (uint32_t)d) v = v > y ? v : y;
   }
   return v;
@@ -194,6 +209,165 @@ k_tok(const uint8_t* __restrict__ t, TokGeo G, uint32_t max_token, uint64_t* __r
   }
 }
 
+// Wave-chunked tokenizer (default; kvh_set_tuning(19, 0) selects k_tok).
+// Each wave owns a 16 KiB chunk (16 passes of 64 segments) and needs no
+// workgroup barrier: all 16 segment loads are issued up front; the start of
+// a token running into the chunk comes from one 256-byte window per wave
+// (ballot over separator bytes) instead of a byte-serial backward walk; the
+// pass-to-pass carry (running last start, neighbour separator bits) stays in
+// registers.  With max_token > 16 the count is popc(ends) minus the first
+// end's token when that one is too long (every later end in a segment has
+// its start in the segment, hence length <= 16).  EMIT stages a pass's
+// (offset, length) records in LDS and writes them out coalesced.
+constexpr uint64_t kTok2Passes = 16;
+constexpr uint64_t kTok2Chunk = kTok2Passes * 64 * kTokSeg;  // 16 KiB per wave
+
+__device__ __forceinline__ v4u seg_ld(const TokGeo& G, uint64_t g) {
+  return __builtin_nontemporal_load((const v4u*)(G.base + 16 * (g < G.nseg ? g : 0)));
+}
+__device__ __forceinline__ uint32_t seg_ws2(const TokGeo& G, uint64_t g, const v4u v) {
+  const bool in = g < G.nseg;
+  uint32_t m = ws_bits(v.x) | ws_bits(v.y) << 4 | ws_bits(v.z) << 8 | ws_bits(v.w) << 12;
+  const int64_t p0 = (int64_t)(16 * g) - G.lead;
+  if (p0 < 0) m |= (1u << (uint32_t)(-p0)) - 1u;
+  if (p0 + 16 > G.n) m |= 0xffffu & ~((1u << (uint32_t)(G.n - p0 > 0 ? G.n - p0 : 0)) - 1u);
+  return in ? m : 0xffffu;
+}
+
+__device__ __forceinline__ int64_t wave_max64(int64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const int64_t y = __shfl_xor(v, d, 64);
+    v = v > y ? v : y;
+  }
+  return v;
+}
+
+template <bool EMIT>
+__global__ void __launch_bounds__(256)
+k_tok2(const uint8_t* __restrict__ t, TokGeo G, uint32_t max_token, uint64_t* __restrict__ chunk_cnt,
+       uint64_t nchunks, uint64_t* __restrict__ offs, uint32_t* __restrict__ lens, uint64_t cap) {
+  __shared__ uint64_t so[4][512];  // <= 8 token ends per 16-byte segment
+  __shared__ uint32_t sl[4][512];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t w = (uint64_t)blockIdx.x * 4 + wv;
+  if (w >= nchunks) return;
+  const uint64_t g0 = w * (kTok2Chunk / kTokSeg);
+  // segment loads run kPf passes ahead of the pass being tokenized
+  constexpr uint32_t kPf = 3;
+  v4u raw[kPf];
+#pragma unroll
+  for (uint32_t d = 0; d < kPf; d++) raw[d] = seg_ld(G, g0 + (1 + d) * 64 + lane);
+  uint32_t Wc = seg_ws2(G, g0 + lane, seg_ld(G, g0 + lane)), Wnx = 0, prevW = 0;
+  const int64_t p = (int64_t)(16 * g0) - G.lead;  // text index of the chunk's first byte
+  const uint32_t after_chunk = (uint32_t)ws_at(t, G.n, p + (int64_t)kTok2Chunk);
+  // Token running in: the last separator before p, searched back in 256-byte
+  // windows (4 bytes per lane, dword aligned since p + lead is); indices < 0
+  // are separators, so the search ends at the text start.  A start at or
+  // before lim = p-1-max_token only has to make the token too long.
+  int64_t carry = kNoStart;
+  uint32_t before_chunk = 1;
+  if (p > 0) {
+    const int64_t lim = p - 1 - (int64_t)max_token;
+    int64_t hi = p, ls = INT64_MIN;
+    for (;;) {
+      const int64_t i0 = hi - 256 + 4 * (int64_t)lane;
+      uint32_t bytes = 0;
+      if (i0 + 3 >= 0) bytes = *(const uint32_t*)(t + i0);  // the aligned dword holding a text byte stays in its page
+      int64_t mine = INT64_MIN;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (i0 + k < 0 || is_ws((bytes >> (8 * k)) & 255u)) mine = i0 + k;
+      if (hi == p) before_chunk = (uint32_t)__shfl(mine == p - 1 ? 1 : 0, 63, 64);
+      ls = wave_max64(mine);
+      if (ls != INT64_MIN || hi - 256 <= lim) break;
+      hi -= 256;
+    }
+    if (!before_chunk) carry = ls + 1 > lim ? ls + 1 : lim;
+  }
+  uint32_t total = 0;
+  uint64_t k0 = EMIT ? chunk_cnt[w] : 0;
+#pragma unroll 1
+  for (uint32_t ps = 0; ps < kTok2Passes; ps++) {
+    const int64_t p0 = p + (int64_t)(16 * (ps * 64 + lane));
+    if (ps + 1 < kTok2Passes) Wnx = seg_ws2(G, g0 + (ps + 1) * 64 + lane, raw[0]);
+#pragma unroll
+    for (uint32_t d = 0; d + 1 < kPf; d++) raw[d] = raw[d + 1];
+    if (ps + 1 + kPf < kTok2Passes) raw[kPf - 1] = seg_ld(G, g0 + (ps + 1 + kPf) * 64 + lane);
+    const uint32_t Wp = __shfl_up(Wc, 1, 64), Wn = __shfl_down(Wc, 1, 64);
+    const uint32_t prev63 = ps ? (uint32_t)__shfl(prevW, 63, 64) >> 15 & 1u : before_chunk;
+    const uint32_t next0 = ps + 1 < kTok2Passes ? (uint32_t)__shfl(Wnx, 0, 64) & 1u : after_chunk;
+    const uint32_t before = lane ? (Wp >> 15) & 1u : prev63;
+    const uint32_t after = lane < 63 ? Wn & 1u : next0;
+    const uint32_t S = ~Wc & ((Wc << 1) | before) & 0xffffu;
+    const uint32_t E = ~Wc & ((Wc >> 1) | (after << 15)) & 0xffffu;
+    // last start at or before each segment, as an offset into this pass
+    // (-1: none in the pass so far, then the carry from earlier passes)
+    const int64_t pp = p + (int64_t)(16 * 64 * ps);
+    const int32_t mine = S ? (int32_t)(16 * lane + 31 - __builtin_clz(S)) : -1;
+    const int32_t inc = wave_max_scan32(mine, lane);
+    const int32_t up = __shfl_up(inc, 1, 64);  // all lanes: a source lane must be active
+    const int32_t exr = lane ? up : -1;
+    const int64_t ex = exr >= 0 ? pp + exr : carry;
+    {
+      const int32_t last = __shfl(inc, 63, 64);
+      if (last >= 0) carry = pp + last;
+    }
+    uint32_t c;
+    if (max_token > 16) {
+      c = (uint32_t)__builtin_popcount(E);
+      if (E) {
+        const uint32_t i = (uint32_t)__builtin_ctz(E);
+        const uint32_t sm = S & ((2u << i) - 1u);
+        const int64_t st = sm ? p0 + 31 - __builtin_clz(sm) : ex;
+        c -= (p0 + (int64_t)i - st + 1) >= (int64_t)max_token;
+      }
+    } else {
+      c = 0;
+      for (uint32_t e = E; e; e &= e - 1) {
+        const uint32_t i = (uint32_t)__builtin_ctz(e);
+        const uint32_t sm = S & ((2u << i) - 1u);
+        const int64_t st = sm ? p0 + 31 - __builtin_clz(sm) : ex;
+        c += (p0 + (int64_t)i - st + 1) < (int64_t)max_token;
+      }
+    }
+    if constexpr (EMIT) {
+      const uint32_t ci = wave_sum_scan(c, lane);
+      const uint32_t tot = (uint32_t)__shfl(ci, 63, 64);
+      uint32_t slot = ci - c;
+      for (uint32_t e = c ? E : 0u; e; e &= e - 1) {
+        const uint32_t i = (uint32_t)__builtin_ctz(e);
+        const uint32_t sm = S & ((2u << i) - 1u);
+        const int64_t st = sm ? p0 + 31 - __builtin_clz(sm) : ex;
+        const int64_t L = p0 + (int64_t)i - st + 1;
+        if (L < (int64_t)max_token) {
+          so[wv][slot] = (uint64_t)st;
+          sl[wv][slot] = (uint32_t)L;
+          slot++;
+        }
+      }
+      wave_lds_sync();
+      for (uint32_t j = lane; j < tot; j += 64) {
+        const uint64_t k = k0 + j;
+        if (k < cap) {
+          offs[k] = so[wv][j];
+          lens[k] = sl[wv][j];
+        }
+      }
+      wave_lds_sync();
+      k0 += tot;
+    } else {
+      total += c;
+    }
+    prevW = Wc;
+    Wc = Wnx;
+  }
+  if constexpr (!EMIT) {
+    for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
+    if (lane == 0) chunk_cnt[w] = total;
+  }
+}
+
 // exclusive scan of nc chunk counts in place; total -> *total (one workgroup)
 __global__ void __launch_bounds__(kScanBlock)
 k_tok_scan(uint64_t* __restrict__ cnt, uint64_t nc, uint64_t* __restrict__ total) {
@@ -263,6 +437,124 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
   }
 }
 
+// Spans (kvh_meow128_spans): one lane per span in 64-span chunks per wave.
+// Text tokens are short (f3: mean 3 bytes), and a span hashing 1..15 bytes
+// touches only S3, so kv_hash_meow128 (key_hash.c:1413-1429) folds
+//  to four table rounds with no branch:
+//   S3 = AESDEC(F3 ^ k, k); S3 = AESDEC(S3, M)          Meow_Loop_Trail + Mix
+//   S2 = AESDEC(TG2 ^ S3, M)                            Compress_Meow2
+//   h  = AESDEC(TCS0a ^ S2, M)                          Compress_Meow
+// But ~1 % of the tokens are longer, which in a lane-per-span kernel puts a
+// longer path (8+ rounds) into most chunks.  So each wave hashes its short
+// spans in place and appends the indices of the others to its own LDS queue
+// (ballot + mbcnt compaction, no atomics), and runs the runtime-length path
+// only when 64 of them are queued (and once for the remainder at the end):
+// the long path then runs on full, mostly same-shape waves.
+template <int NT, int P>
+__global__ void __launch_bounds__(1024)
+k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
+        uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags) {
+  constexpr int NW = 1024 / 64;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ MeowConst kfull[kLT];
+  __shared__ Blk kf[kNF * 4];
+  __shared__ uint64_t queue[NW][128];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + kNF); l += blockDim.x) {
+    if (l < (uint32_t)kLT) {
+      kfull[l] = make_const(s1, s2, l, T);
+    } else {
+      const Blk M = mixer(s1, s2, l);
+#pragma unroll
+      for (int s = 0; s < 4; s++) kf[(l - kLT) * 4 + s] = aesT(bxor(ramp(s), M), T);
+    }
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t nul = (flags & KVH_NULTERM) ? 1u : 0u;
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t* q = queue[threadIdx.x >> 6];
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = ((uint64_t)gridDim.x * blockDim.x) & ~(uint64_t)63;
+  uint32_t qn = 0;  // wave-uniform queue length
+  auto long_path = [&](uint32_t cnt) {  // hash q[0 .. cnt) (cnt <= 64), lane per entry
+    if (lane < cnt) {
+      const uint64_t j = q[lane];
+      const uint8_t* p = buf + offs[j];
+      const uint32_t D = lens[j], H = D + nul;
+      const LdsK<LdsTab<NT>> K(kfull, kf, H, s1, s2, T);
+      const MaskLd ld{p + D};
+      store_h(out, j, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>>, MaskLd>(p, H, K, T, ld), fix);
+    }
+  };
+  // Software pipeline over this wave's chunks: while chunk b is hashed, the
+  // text of chunks b+step .. b+P*step and the offsets/lengths of chunk
+  // b+(P+1)*step are in flight (each span's text load depends on its offset).
+  auto meta = [&](uint64_t bb, uint64_t& o, uint32_t& D) {
+    const uint64_t jj = std::min<uint64_t>(bb + lane, n - 1);
+    o = offs[jj];
+    D = lens[jj];
+  };
+  auto text = [&](uint64_t bb, uint64_t o, uint32_t D) {  // short spans only; NUL and padding read as zero
+    return (bb + lane < n && D + nul - 1u < 15u && D) ? load_bytes(buf + o, D) : bzero();
+  };
+  uint64_t b = wave * 64, oN;
+  uint32_t Dq[P + 1], DN;
+  Blk kq[P];
+#pragma unroll
+  for (int s = 0; s < P; s++) {
+    uint64_t o;
+    meta(b + s * step, o, Dq[s]);
+    kq[s] = text(b + s * step, o, Dq[s]);
+  }
+  meta(b + P * step, oN, DN);
+  for (; b < n; b += step) {  // wave-uniform trip count
+    Dq[P] = DN;
+    const Blk kn = text(b + P * step, oN, DN);
+    meta(b + (P + 1) * step, oN, DN);
+    const Blk k0 = kq[0];
+    const uint32_t D0 = Dq[0];
+    const uint64_t j = b + lane;
+    const bool valid = j < n;
+    const uint32_t H = D0 + nul;
+    const bool shrt = H - 1u < 15u;
+    if (valid && shrt) {
+      const MeowConst& c = kfull[H];
+      const Blk M = c.M;
+      Blk S3 = aesdec(bxor(c.F[3], k0), k0, T);
+      S3 = aesdec(S3, M, T);
+      const Blk S2 = aesdec(bxor(c.TG2, S3), M, T);
+      store_h(out, j, aesdec(bxor(c.TCS0a, S2), M, T), fix);
+    }
+    const uint64_t lm = __ballot(valid && !shrt);
+    if (lm) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+      if (valid && !shrt) q[qn + below] = j;
+      qn += (uint32_t)__popcll(lm);
+      wave_lds_sync();
+      if (qn >= 64) {
+        long_path(64);
+        wave_lds_sync();
+        qn -= 64;
+        if (lane < qn) q[lane] = q[64 + lane];  // move the overflow to the front
+        wave_lds_sync();
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < P - 1; s++) kq[s] = kq[s + 1];
+    kq[P - 1] = kn;
+#pragma unroll
+    for (int s = 0; s < P; s++) Dq[s] = Dq[s + 1];
+  }
+  if (qn) long_path(qn);
+}
+
+}  // namespace
+namespace kvh { namespace rt { int g_tune_spans = 2; int g_tune_tok = 1; } }
+namespace {
+
 TokGeo tok_geo(const void* text, size_t nbytes) {
   TokGeo G;
   G.lead = (int64_t)((uintptr_t)text & 15);
@@ -281,7 +573,7 @@ uint64_t tok_chunks(const void* text, size_t nbytes) {
 extern "C" {
 
 size_t kvh_tokenize_scratch_bytes(size_t nbytes) {
-  return 8 * ((nbytes + 31 + kTokChunk - 1) / kTokChunk + 1);  // any text alignment
+  return 8 * ((nbytes + 31 + kTok2Chunk - 1) / kTok2Chunk + 1);  // either kernel, any text alignment
 }
 
 int kvh_tokenize(const void* text, size_t nbytes, uint32_t max_token, uint64_t* tok_offs, uint32_t* tok_lens,
@@ -295,9 +587,24 @@ int kvh_tokenize(const void* text, size_t nbytes, uint32_t max_token, uint64_t* 
   if (!text || !scratch || scratch_bytes < kvh_tokenize_scratch_bytes(nbytes) || (cap && (!tok_offs || !tok_lens)))
     return set_err(KVH_EINVAL);
   const TokGeo G = tok_geo(text, nbytes);
-  const uint64_t nc = tok_chunks(text, nbytes);
   uint64_t* cc = (uint64_t*)scratch;
   const uint8_t* t = (const uint8_t*)text;
+  if (g_tune_tok) {
+    const uint64_t nc = (G.nseg * kTokSeg + kTok2Chunk - 1) / kTok2Chunk;
+    const uint32_t grid = (uint32_t)((nc + 3) / 4);
+    hipLaunchKernelGGL(k_tok2<false>, dim3(grid), dim3(256), 0, st, t, G, max_token, cc, nc, (uint64_t*)nullptr,
+                       (uint32_t*)nullptr, (uint64_t)0);
+    int rc = launch_done();
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_tok_scan, dim3(1), dim3(kScanBlock), 0, st, cc, nc, count);
+    rc = launch_done();
+    if (rc) return rc;
+    if (cap == 0) return set_err(0);
+    hipLaunchKernelGGL(k_tok2<true>, dim3(grid), dim3(256), 0, st, t, G, max_token, cc, nc, tok_offs, tok_lens,
+                       (uint64_t)cap);
+    return launch_done();
+  }
+  const uint64_t nc = tok_chunks(text, nbytes);
   hipLaunchKernelGGL(k_tok<false>, dim3((uint32_t)nc), dim3(kTokBlock), 0, st, t, G, max_token, cc,
                      (uint64_t*)nullptr, (uint32_t*)nullptr, (uint64_t)0);
   int rc = launch_done();
@@ -318,8 +625,16 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
-  hipLaunchKernelGGL((k_keysrc<SRC_SPANS, 4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream,
-                     (const uint8_t*)buf, offs, lens, (uint64_t)n, seed1, seed2, out, flags);
+  if (g_tune_spans)
+    if (g_tune_spans == 2)
+      hipLaunchKernelGGL((k_spans<2, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+                         lens, (uint64_t)n, seed1, seed2, out, flags);
+    else
+      hipLaunchKernelGGL((k_spans<2, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+                         lens, (uint64_t)n, seed1, seed2, out, flags);
+  else
+    hipLaunchKernelGGL((k_keysrc<SRC_SPANS, 4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream,
+                       (const uint8_t*)buf, offs, lens, (uint64_t)n, seed1, seed2, out, flags);
   return launch_done();
 }
 

@@ -159,6 +159,9 @@ int launch_done();
 extern int g_tune_crc_var;
 // table-order sort: h1 bits sorted below the slot bits (0 = by batch size; 64 = the full key)
 extern int g_tune_sort_bits;
+// span hashing: 1 = wave-chunked kernel with the short-key path (default), 0 = lane per span
+extern int g_tune_spans;
+extern int g_tune_tok;
 }  // namespace rt
 
 }  // namespace kvh

@@ -47,8 +47,16 @@ def test_frag_records_golden(kvh):
     np.testing.assert_array_equal(host(kvh.meow128_frags(frags, ro, SEED)), G["hashes"])
 
 
+@pytest.fixture(params=[1, 0], ids=["tok_wave", "tok_wg"])
+def tok_kernel(kvh, request):
+    """Both tokenizers (kvh_set_tuning(19, v): 1 wave-chunked, 0 workgroup-chunked)."""
+    prev = kvh.lib.kvh_set_tuning(19, request.param)
+    yield request.param
+    kvh.lib.kvh_set_tuning(19, prev)
+
+
 @pytest.mark.parametrize("shift", [0, 1, 2, 3, 5, 15])
-def test_tokenize_unaligned_and_edges(kvh, shift):
+def test_tokenize_unaligned_and_edges(kvh, tok_kernel, shift):
     rng = np.random.default_rng(shift)
     cases = [b"", b"   ", b"a", b" a", b"a ", b"x" * 255 + b" y", b"x" * 256 + b"\ty", b"\n\n\tq\t\n",
              bytes(rng.choice(np.frombuffer(b"ab \n\t", dtype=np.uint8), 70000))]
@@ -65,6 +73,37 @@ def test_tokenize_unaligned_and_edges(kvh, shift):
                                                                    SEED))
 
 
+def _mixed_text(rng, n):
+    """Tokens of 1..8 bytes, runs of separators, and some of 200..40000
+    bytes so that tokens cross 16 KiB / 64 KiB chunk seams and the backward
+    carry search needs several 256-byte windows."""
+    parts, size = [], 0
+    while size < n:
+        u = rng.random()
+        if u < 0.02:
+            k = int(rng.integers(200, 40000))
+        elif u < 0.1:
+            k = int(rng.integers(9, 40))
+        else:
+            k = int(rng.integers(1, 9))
+        parts.append(bytes(rng.integers(33, 127, k, dtype=np.uint8)))
+        parts.append(bytes(rng.choice(np.frombuffer(b" \n\t", dtype=np.uint8), int(rng.integers(1, 4)))))
+        size += k + 3
+    return np.frombuffer(b"".join(parts)[:n], dtype=np.uint8).copy()
+
+
+@pytest.mark.parametrize("max_token", [1, 5, 16, 17, 256, 5000, 100000])
+def test_tokenize_kernels_vs_oracle(kvh, tok_kernel, max_token):
+    rng = np.random.default_rng(max_token)
+    for shift, n in ((0, 1 << 20), (3, 300001), (13, 16384 * 3 + 5)):
+        arr = np.concatenate([np.full(shift, 35, np.uint8), _mixed_text(rng, n)])
+        dev = torch.from_numpy(arr).cuda()[shift:]
+        offs, lens = kvh.tokenize(dev, max_token)
+        wo, wl = orc_tokenize(ORC, arr[shift:], max_token)
+        np.testing.assert_array_equal(host(offs), wo)
+        np.testing.assert_array_equal(host(lens), wl)
+
+
 def test_spans_without_nul_match_var(kvh):
     rng = np.random.default_rng(4)
     buf = rng.integers(0, 256, 100000, dtype=np.uint8)
@@ -76,7 +115,7 @@ def test_spans_without_nul_match_var(kvh):
     np.testing.assert_array_equal(host(h), orc_hash_spans(ORC, buf, offs, lens, SEED, nul=False, fix=False))
 
 
-def test_cap_truncates_but_counts(kvh):
+def test_cap_truncates_but_counts(kvh, tok_kernel):
     text = torch.from_numpy(G["text"]).cuda()
     offs, lens = kvh.tokenize(text, 256, cap=100)
     want_o, _ = orc_tokenize(ORC, G["text"], 256)
@@ -84,7 +123,7 @@ def test_cap_truncates_but_counts(kvh):
     np.testing.assert_array_equal(host(offs), want_o[:100])
 
 
-def test_large_text_property(kvh):
+def test_large_text_property(kvh, tok_kernel):
     """1 GiB of synthetic text (≈ 180M tokens): device tokens equal the
     oracle on sampled 64 KiB windows away from chunk seams, counts are
     consistent, and spans hash == packed-record hash on a sample."""
@@ -107,3 +146,27 @@ def test_large_text_property(kvh):
         a = np.searchsorted(o, start + wo[inner])
         np.testing.assert_array_equal(o[a], start + wo[inner])
         np.testing.assert_array_equal(l[a], wl[inner])
+
+
+@pytest.mark.parametrize("kernel", [0, 1, 2])
+@pytest.mark.parametrize("nulterm", [True, False])
+def test_spans_kernels_vs_oracle(kvh, kernel, nulterm):
+    """Both span kernels (lane per span; short spans in place with the long
+    ones queued per wave, knob 18) on spans of 0..40 bytes with a long one
+    every so often, so that chunks are all short, all long and mixed; odd
+    counts for the chunk tails; 600001 mostly-long spans so that each wave
+    walks several chunks and its queue overflows 64 and carries over."""
+    rng = np.random.default_rng(17 + kernel + 2 * nulterm)
+    buf = rng.integers(0, 256, 400000, dtype=np.uint8)
+    for n in (1, 63, 129, 4097, 50001, 600001):
+        lens = rng.integers(0, 16 if n not in (4097, 600001) else 41, n).astype(np.uint32)
+        if n > 1000:
+            lens[rng.integers(0, n, n // 500)] = rng.integers(16, 300, n // 500).astype(np.uint32)
+        offs = rng.integers(0, 400000 - 300, n).astype(np.uint64)
+        prev = kvh.lib.kvh_set_tuning(18, kernel)
+        try:
+            h = kvh.meow128_spans(torch.from_numpy(buf).cuda(), torch.from_numpy(offs.view(np.int64)).cuda(),
+                                  torch.from_numpy(lens.view(np.int32)).cuda(), SEED, nulterm=nulterm)
+            np.testing.assert_array_equal(host(h), orc_hash_spans(ORC, buf, offs, lens, SEED, nul=nulterm))
+        finally:
+            kvh.lib.kvh_set_tuning(18, prev)
