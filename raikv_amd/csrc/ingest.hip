@@ -393,6 +393,48 @@ k_tok_scan(uint64_t* __restrict__ cnt, uint64_t nc, uint64_t* __restrict__ total
   if (threadIdx.x == kScanBlock - 1) *total = part[kScanBlock - 1];
 }
 
+// Exclusive scan of the wave-chunked tokenizer's chunk counts (cnt -> pre,
+// total -> *total) over many workgroups with no inter-workgroup hand-off:
+// the counts are all in memory, so workgroup b sums every count before its
+// block of kScan3 (coalesced 16-byte loads; at most a few hundred KB per
+// workgroup for a GiB of text) and scans its own block.
+constexpr uint32_t kScan3 = 2 * kScanBlock;
+__global__ void __launch_bounds__(kScanBlock)
+k_tok_scan3(const uint64_t* __restrict__ cnt, uint64_t nc, uint64_t* __restrict__ pre, uint64_t* __restrict__ total) {
+  __shared__ uint64_t wpart[kScanBlock / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint64_t lo = (uint64_t)blockIdx.x * kScan3;
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+  uint64_t s = 0;
+  for (uint64_t i = 2 * tid; i < lo; i += kScan3) {  // lo is a multiple of kScan3: i + 1 < lo
+    const u64x2 v = *(const u64x2*)(cnt + i);
+    s += v.x + v.y;
+  }
+  const uint64_t i0 = lo + 2 * tid;
+  const uint64_t x0 = i0 < nc ? cnt[i0] : 0, x1 = i0 + 1 < nc ? cnt[i0 + 1] : 0;
+  // block reduce of s and block scan of x0 + x1 together
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  uint64_t inc = x0 + x1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  __shared__ uint64_t wsum[kScanBlock / 64];
+  if (lane == 63) wpart[wv] = inc;
+  if (lane == 0) wsum[wv] = s;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+  for (uint32_t k = 0; k < kScanBlock / 64; k++) {
+    base += wsum[k] + (k < wv ? wpart[k] : 0);
+    tot += wsum[k] + wpart[k];
+  }
+  const uint64_t ex = base + inc - (x0 + x1);
+  if (i0 < nc) pre[i0] = ex;
+  if (i0 + 1 < nc) pre[i0 + 1] = ex + x0;
+  if (lo + kScan3 >= nc && tid == 0) *total = tot;
+}
+
 enum { SRC_SPANS = 0, SRC_FRAGS = 1 };
 
 template <int SRC, int NT>
@@ -437,6 +479,24 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
   }
 }
 
+// hash the queued spans q[0 .. cnt) (cnt <= 64), lane per entry, runtime length
+template <int NT>
+__device__ __forceinline__ void spans_long(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
+                                           const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
+                                           const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t wave, uint64_t step,
+                                           uint32_t nul, bool fix, const MeowConst* kfull, uint64_t s1, uint64_t s2,
+                                           const LdsTab<NT>& T) {
+  if (lane < cnt) {
+    const uint32_t e = q[lane];
+    const uint64_t j = wave * 64 + (uint64_t)(e >> 6) * step + (e & 63u);
+    const uint8_t* p = buf + offs[j];
+    const uint32_t D = lens[j], H = D + nul;
+    const LdsK<LdsTab<NT>> K(kfull, nullptr, H, s1, s2, T);
+    const MaskLd ld{p + D};
+    store_h(out, j, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>>, MaskLd>(p, H, K, T, ld), fix);
+  }
+}
+
 // Spans (kvh_meow128_spans): one lane per span in 64-span chunks per wave.
 // Text tokens are short (f3: mean 3 bytes), and a span hashing 1..15 bytes
 // touches only S3, so kv_hash_meow128 (key_hash.c:1413-1429) folds
@@ -446,10 +506,44 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
 //   h  = AESDEC(TCS0a ^ S2, M)                          Compress_Meow
 // But ~1 % of the tokens are longer, which in a lane-per-span kernel puts a
 // longer path (8+ rounds) into most chunks.  So each wave hashes its short
-// spans in place and appends the indices of the others to its own LDS queue
-// (ballot + mbcnt compaction, no atomics), and runs the runtime-length path
-// only when 64 of them are queued (and once for the remainder at the end):
-// the long path then runs on full, mostly same-shape waves.
+// spans in place and appends the others to its own LDS queue (ballot +
+// mbcnt compaction, no atomics), and runs the runtime-length path only when
+// 64 of them are queued (and once for the remainder at the end): the long
+// path then runs on full, mostly same-shape waves.  Loads run P chunks
+// ahead (a span's text load depends on its offset load).  LDS: all four
+// tables (no rotates in the round), full constant records for L < 64 (the
+// first-absorb folds of longer spans are made in-lane), u32 queue entries.
+// A short span's bytes come from two aligned 16-byte blocks, the one holding
+// its first byte and the one holding its last (the same block when the span
+// does not cross), so no load leaves the span's pages; a funnel shift by
+// p & 15 and a byte mask give the key block.
+__device__ __forceinline__ Blk load_short(const uint8_t* __restrict__ p, uint32_t D) {
+  // pointer arithmetic (not integer masks) keeps these global, not flat, loads
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t e = D ? D - 1 : 0;
+  const v4u A = *(const v4u*)(p - (a & 15));
+  const v4u B = *(const v4u*)(p + e - ((a + e) & 15));
+  const uint32_t s = (uint32_t)a & 15u;
+  uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+  // rotate the 8 words down by s >> 2 (two mux stages), then funnel by s & 3
+  if (s & 8) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) w[i] = w[i + 2];
+  }
+  if (s & 4) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = w[i + 1];
+  }
+  Blk r;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(w[c + 1], w[c], s & 3u);
+    const int keep = (int)D - 4 * c;
+    r.w[c] = v & (keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u));
+  }
+  return r;
+}
+
 template <int NT, int P>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
@@ -457,63 +551,45 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   constexpr int NW = 1024 / 64;
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
   __shared__ MeowConst kfull[kLT];
-  __shared__ Blk kf[kNF * 4];
-  __shared__ uint64_t queue[NW][128];
+  __shared__ uint32_t queue[NW][128];
   fill_tables<NT>(lds);
   __syncthreads();
   const LdsTab<NT> T(lds);
-  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + kNF); l += blockDim.x) {
-    if (l < (uint32_t)kLT) {
-      kfull[l] = make_const(s1, s2, l, T);
-    } else {
-      const Blk M = mixer(s1, s2, l);
-#pragma unroll
-      for (int s = 0; s < 4; s++) kf[(l - kLT) * 4 + s] = aesT(bxor(ramp(s), M), T);
-    }
-  }
+  for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) kfull[l] = make_const(s1, s2, l, T);
   __syncthreads();
   const bool fix = (flags & KVH_FIXUP) != 0;
   const uint32_t nul = (flags & KVH_NULTERM) ? 1u : 0u;
   const uint32_t lane = threadIdx.x & 63;
-  uint64_t* q = queue[threadIdx.x >> 6];
+  uint32_t* q = queue[threadIdx.x >> 6];
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t step = ((uint64_t)gridDim.x * blockDim.x) & ~(uint64_t)63;
+  // queue entry e = 64 * (chunk iteration) + lane  ->  span wave*64 + (e>>6)*step + (e&63)
   uint32_t qn = 0;  // wave-uniform queue length
-  auto long_path = [&](uint32_t cnt) {  // hash q[0 .. cnt) (cnt <= 64), lane per entry
-    if (lane < cnt) {
-      const uint64_t j = q[lane];
-      const uint8_t* p = buf + offs[j];
-      const uint32_t D = lens[j], H = D + nul;
-      const LdsK<LdsTab<NT>> K(kfull, kf, H, s1, s2, T);
-      const MaskLd ld{p + D};
-      store_h(out, j, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>>, MaskLd>(p, H, K, T, ld), fix);
-    }
-  };
-  // Software pipeline over this wave's chunks: while chunk b is hashed, the
-  // text of chunks b+step .. b+P*step and the offsets/lengths of chunk
-  // b+(P+1)*step are in flight (each span's text load depends on its offset).
-  auto meta = [&](uint64_t bb, uint64_t& o, uint32_t& D) {
-    const uint64_t jj = std::min<uint64_t>(bb + lane, n - 1);
-    o = offs[jj];
-    D = lens[jj];
-  };
-  auto text = [&](uint64_t bb, uint64_t o, uint32_t D) {  // short spans only; NUL and padding read as zero
-    return (bb + lane < n && D + nul - 1u < 15u && D) ? load_bytes(buf + o, D) : bzero();
-  };
   uint64_t b = wave * 64, oN;
+  uint32_t it = 0;
   uint32_t Dq[P + 1], DN;
   Blk kq[P];
 #pragma unroll
   for (int s = 0; s < P; s++) {
-    uint64_t o;
-    meta(b + s * step, o, Dq[s]);
-    kq[s] = text(b + s * step, o, Dq[s]);
+    const uint64_t jj = std::min<uint64_t>(b + s * step + lane, n - 1);
+    const uint64_t o = offs[jj];
+    Dq[s] = lens[jj];
+    kq[s] = (b + s * step + lane < n && Dq[s] && Dq[s] + nul - 1u < 15u) ? load_short(buf + o, Dq[s]) : bzero();
   }
-  meta(b + P * step, oN, DN);
-  for (; b < n; b += step) {  // wave-uniform trip count
+  {
+    const uint64_t jj = std::min<uint64_t>(b + P * step + lane, n - 1);
+    oN = offs[jj];
+    DN = lens[jj];
+  }
+  for (; b < n; b += step, it++) {  // wave-uniform trip count
     Dq[P] = DN;
-    const Blk kn = text(b + P * step, oN, DN);
-    meta(b + (P + 1) * step, oN, DN);
+    // a 0-byte span reads nothing: its address may be one past the buffer
+    const Blk kn = (b + P * step + lane < n && DN && DN + nul - 1u < 15u) ? load_short(buf + oN, DN) : bzero();
+    {
+      const uint64_t jj = std::min<uint64_t>(b + (P + 1) * step + lane, n - 1);
+      oN = offs[jj];
+      DN = lens[jj];
+    }
     const Blk k0 = kq[0];
     const uint32_t D0 = Dq[0];
     const uint64_t j = b + lane;
@@ -531,11 +607,11 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
     const uint64_t lm = __ballot(valid && !shrt);
     if (lm) {
       const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-      if (valid && !shrt) q[qn + below] = j;
+      if (valid && !shrt) q[qn + below] = 64u * it + lane;
       qn += (uint32_t)__popcll(lm);
       wave_lds_sync();
       if (qn >= 64) {
-        long_path(64);
+        spans_long<NT>(buf, offs, lens, out, q, 64, lane, wave, step, nul, fix, kfull, s1, s2, T);
         wave_lds_sync();
         qn -= 64;
         if (lane < qn) q[lane] = q[64 + lane];  // move the overflow to the front
@@ -548,8 +624,9 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
 #pragma unroll
     for (int s = 0; s < P; s++) Dq[s] = Dq[s + 1];
   }
-  if (qn) long_path(qn);
+  if (qn) spans_long<NT>(buf, offs, lens, out, q, qn, lane, wave, step, nul, fix, kfull, s1, s2, T);
 }
+
 
 }  // namespace
 namespace kvh { namespace rt { int g_tune_spans = 2; int g_tune_tok = 1; } }
@@ -573,7 +650,7 @@ uint64_t tok_chunks(const void* text, size_t nbytes) {
 extern "C" {
 
 size_t kvh_tokenize_scratch_bytes(size_t nbytes) {
-  return 8 * ((nbytes + 31 + kTok2Chunk - 1) / kTok2Chunk + 1);  // either kernel, any text alignment
+  return 16 * ((nbytes + 31 + kTok2Chunk - 1) / kTok2Chunk + 1);  // counts + prefixes; either kernel, any alignment
 }
 
 int kvh_tokenize(const void* text, size_t nbytes, uint32_t max_token, uint64_t* tok_offs, uint32_t* tok_lens,
@@ -591,16 +668,18 @@ int kvh_tokenize(const void* text, size_t nbytes, uint32_t max_token, uint64_t* 
   const uint8_t* t = (const uint8_t*)text;
   if (g_tune_tok) {
     const uint64_t nc = (G.nseg * kTokSeg + kTok2Chunk - 1) / kTok2Chunk;
+    uint64_t* pre = cc + nc;
     const uint32_t grid = (uint32_t)((nc + 3) / 4);
     hipLaunchKernelGGL(k_tok2<false>, dim3(grid), dim3(256), 0, st, t, G, max_token, cc, nc, (uint64_t*)nullptr,
                        (uint32_t*)nullptr, (uint64_t)0);
     int rc = launch_done();
     if (rc) return rc;
-    hipLaunchKernelGGL(k_tok_scan, dim3(1), dim3(kScanBlock), 0, st, cc, nc, count);
+    hipLaunchKernelGGL(k_tok_scan3, dim3((uint32_t)((nc + kScan3 - 1) / kScan3)), dim3(kScanBlock), 0, st, cc, nc,
+                       pre, count);
     rc = launch_done();
     if (rc) return rc;
     if (cap == 0) return set_err(0);
-    hipLaunchKernelGGL(k_tok2<true>, dim3(grid), dim3(256), 0, st, t, G, max_token, cc, nc, tok_offs, tok_lens,
+    hipLaunchKernelGGL(k_tok2<true>, dim3(grid), dim3(256), 0, st, t, G, max_token, pre, nc, tok_offs, tok_lens,
                        (uint64_t)cap);
     return launch_done();
   }
@@ -627,10 +706,10 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
   if (g_tune_spans)
     if (g_tune_spans == 2)
-      hipLaunchKernelGGL((k_spans<2, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+      hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                          lens, (uint64_t)n, seed1, seed2, out, flags);
     else
-      hipLaunchKernelGGL((k_spans<2, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+      hipLaunchKernelGGL((k_spans<4, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                          lens, (uint64_t)n, seed1, seed2, out, flags);
   else
     hipLaunchKernelGGL((k_keysrc<SRC_SPANS, 4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream,

@@ -56,7 +56,7 @@ constexpr int kNF = 256;  // F-only records for 64 <= L < 64 + kNF
 template <class Tab>
 struct LdsK {
   const MeowConst* full;   // [kLT]
-  const Blk* ftab;         // [kNF][4]
+  const Blk* ftab;         // [kNF][4], or null: folds in-lane
   uint32_t L;
   Blk m;
   const Tab& T;
@@ -67,7 +67,7 @@ struct LdsK {
   __device__ __forceinline__ Blk M() const { return m; }
   __device__ __forceinline__ Blk F(int i) const {
     if (L < (uint32_t)kLT) return full[L].F[i];
-    if (L < (uint32_t)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
+    if (ftab && L < (uint32_t)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
     return aesT(bxor(ramp(i), m), T);
   }
   __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }

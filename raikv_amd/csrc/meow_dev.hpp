@@ -257,7 +257,7 @@ __device__ __forceinline__ Blk meow_ct(const Blk* D, const MeowConst& K, const T
 // dword (no fault at the end of an allocation).
 __device__ __forceinline__ Blk load_bytes(const uint8_t* p, uint32_t n) {
   const uintptr_t a = (uintptr_t)p;
-  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t* q = (const uint32_t*)(p - (a & 3));  // pointer arithmetic keeps the global address space
   const uint32_t sh = (uint32_t)(a & 3);
   const uint32_t nd = (sh + n + 3) >> 2;
   uint32_t d[5];
@@ -281,7 +281,7 @@ __device__ __forceinline__ Blk load_bytes(const uint8_t* p, uint32_t n) {
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ Blk load16_full(const uint8_t* p) {
   const uintptr_t a = (uintptr_t)p;
-  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t* q = (const uint32_t*)(p - (a & 3));  // pointer arithmetic keeps the global address space
   const uint32_t sh = (uint32_t)(a & 3);
   const u32x4_a4 v = *(const u32x4_a4*)q;
   const uint32_t e = sh ? q[4] : 0u;
@@ -302,7 +302,7 @@ struct GlobalLd {
 struct LdsLd {
   static __device__ __forceinline__ Blk full(const uint8_t* p) {
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+    const uint32_t* q = (const uint32_t*)(p - (a & 3));  // pointer arithmetic keeps the global address space
     const uint32_t sh = (uint32_t)(a & 3);
     uint32_t d[5];
 #pragma unroll
