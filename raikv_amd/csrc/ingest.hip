@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <algorithm>
+#include <type_traits>
 #include "kvh_internal.hpp"
 #include "../../include/kvh.h"
 
@@ -509,42 +510,58 @@ __device__ __forceinline__ void spans_long(const uint8_t* __restrict__ buf, cons
 // spans in place and appends the others to its own LDS queue (ballot +
 // mbcnt compaction, no atomics), and runs the runtime-length path only when
 // 64 of them are queued (and once for the remainder at the end): the long
-// path then runs on full, mostly same-shape waves.  Loads run P chunks
-// ahead (a span's text load depends on its offset load).  LDS: all four
+// path then runs on full, mostly same-shape waves.  Loads run ahead of the
+// hashing (a span's text load depends on its offset load).  LDS: all four
 // tables (no rotates in the round), full constant records for L < 64 (the
 // first-absorb folds of longer spans are made in-lane), u32 queue entries.
 // A short span's bytes come from two aligned 16-byte blocks, the one holding
 // its first byte and the one holding its last (the same block when the span
-// does not cross), so no load leaves the span's pages; a funnel shift by
-// p & 15 and a byte mask give the key block.
-__device__ __forceinline__ Blk load_short(const uint8_t* __restrict__ p, uint32_t D) {
-  // pointer arithmetic (not integer masks) keeps these global, not flat, loads
-  const uintptr_t a = (uintptr_t)p;
-  const uint32_t e = D ? D - 1 : 0;
-  const v4u A = *(const v4u*)(p - (a & 15));
-  const v4u B = *(const v4u*)(p + e - ((a + e) & 15));
-  const uint32_t s = (uint32_t)a & 15u;
-  uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-  // rotate the 8 words down by s >> 2 (two mux stages), then funnel by s & 3
-  if (s & 8) {
-#pragma unroll
-    for (int i = 0; i < 6; i++) w[i] = w[i + 2];
-  }
-  if (s & 4) {
-#pragma unroll
-    for (int i = 0; i < 5; i++) w[i] = w[i + 1];
-  }
-  Blk r;
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const uint32_t v = __builtin_amdgcn_alignbyte(w[c + 1], w[c], s & 3u);
-    const int keep = (int)D - 4 * c;
-    r.w[c] = v & (keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u));
+// does not cross), so no load leaves the span's pages.  The blocks stay raw
+// in the load pipeline; when the chunk is hashed, two selects rotate them
+// down by (p & 15) >> 2 words and one v_perm per word does the byte shift
+// and the zero fill past the span, with selectors from an LDS table indexed
+// by (length, p & 3).
+struct ShortRaw {
+  v4u A, B;
+  uint32_t s, D;  // p & 15, span bytes (0: nothing loaded)
+};
+
+__device__ __forceinline__ ShortRaw short_issue(const uint8_t* __restrict__ p, uint32_t D, bool load) {
+  ShortRaw r;
+  const uint32_t a = (uint32_t)(uintptr_t)p & 15u;
+  r.s = a;
+  r.D = load ? D : 0u;
+  if (load) {  // pointer arithmetic (not integer masks) keeps these global loads
+    const uint32_t e = D - 1;
+    r.A = *(const v4u*)(p - a);
+    r.B = *(const v4u*)(p + e - ((a + e) & 15u));
+  } else {
+    r.A = v4u{0, 0, 0, 0};
+    r.B = r.A;
   }
   return r;
 }
 
-template <int NT, int P>
+__device__ __forceinline__ Blk short_key(const ShortRaw& r, const uint32_t* __restrict__ psel) {
+  uint32_t w[8] = {r.A.x, r.A.y, r.A.z, r.A.w, r.B.x, r.B.y, r.B.z, r.B.w};
+  if (r.s & 8) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) w[i] = w[i + 2];
+  }
+  if (r.s & 4) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) w[i] = w[i + 1];
+  }
+  const v4u sel = *(const v4u*)(psel + 4 * (4 * r.D + (r.s & 3u)));
+  Blk k;
+  k.w[0] = __builtin_amdgcn_perm(w[1], w[0], sel.x);
+  k.w[1] = __builtin_amdgcn_perm(w[2], w[1], sel.y);
+  k.w[2] = __builtin_amdgcn_perm(w[3], w[2], sel.z);
+  k.w[3] = __builtin_amdgcn_perm(w[4], w[3], sel.w);
+  return k;
+}
+
+template <int NT>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags) {
@@ -552,7 +569,14 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
   __shared__ MeowConst kfull[kLT];
   __shared__ uint32_t queue[NW][128];
+  __shared__ uint32_t psel[16 * 4 * 4];  // [D][p & 3][word] v_perm selectors
   fill_tables<NT>(lds);
+  for (uint32_t i = threadIdx.x; i < 16u * 4u * 4u; i += blockDim.x) {
+    const uint32_t c = i & 3u, sh = (i >> 2) & 3u, D = i >> 4;
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; k++) v |= (4 * c + k < D ? sh + k : 0x0cu) << (8 * k);
+    psel[i] = v;
+  }
   __syncthreads();
   const LdsTab<NT> T(lds);
   for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) kfull[l] = make_const(s1, s2, l, T);
@@ -565,38 +589,46 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   const uint64_t step = ((uint64_t)gridDim.x * blockDim.x) & ~(uint64_t)63;
   // queue entry e = 64 * (chunk iteration) + lane  ->  span wave*64 + (e>>6)*step + (e&63)
   uint32_t qn = 0;  // wave-uniform queue length
-  uint64_t b = wave * 64, oN;
-  uint32_t it = 0;
-  uint32_t Dq[P + 1], DN;
-  Blk kq[P];
-#pragma unroll
-  for (int s = 0; s < P; s++) {
-    const uint64_t jj = std::min<uint64_t>(b + s * step + lane, n - 1);
-    const uint64_t o = offs[jj];
-    Dq[s] = lens[jj];
-    kq[s] = (b + s * step + lane < n && Dq[s] && Dq[s] + nul - 1u < 15u) ? load_short(buf + o, Dq[s]) : bzero();
-  }
+  auto is_short = [nul](uint32_t D) { return D + nul - 1u < 15u; };
+  // Pipeline, unrolled by two so that no register is renamed while its load
+  // is in flight: iteration c issues the offsets/lengths of chunk c+2 and the
+  // text blocks of chunk c+1 (whose offsets arrived during iteration c-1),
+  // then hashes chunk c from the blocks issued during iteration c-1.
+  uint64_t mo[2];
+  uint32_t mD[2];
+  ShortRaw tr[2];
+  const uint64_t b0 = wave * 64;
   {
-    const uint64_t jj = std::min<uint64_t>(b + P * step + lane, n - 1);
-    oN = offs[jj];
-    DN = lens[jj];
+    const uint64_t j0 = std::min<uint64_t>(b0 + lane, n - 1), j1 = std::min<uint64_t>(b0 + step + lane, n - 1);
+    const uint64_t o0 = offs[j0];
+    const uint32_t D0 = lens[j0];
+    mo[1] = offs[j1];
+    mD[1] = lens[j1];
+    tr[0] = short_issue(buf + o0, D0, b0 + lane < n && D0 && is_short(D0));
+    tr[0].D = D0;  // the length rides with the blocks (0-byte spans load nothing)
   }
-  for (; b < n; b += step, it++) {  // wave-uniform trip count
-    Dq[P] = DN;
-    // a 0-byte span reads nothing: its address may be one past the buffer
-    const Blk kn = (b + P * step + lane < n && DN && DN + nul - 1u < 15u) ? load_short(buf + oN, DN) : bzero();
+  uint32_t it = 0;
+  auto body = [&](uint64_t b, auto uc) {
+    constexpr int u = decltype(uc)::value;  // slot parity, a compile-time constant
+    // offsets of chunk b + 2 step into slot u (chunk b's slot, consumed)
     {
-      const uint64_t jj = std::min<uint64_t>(b + (P + 1) * step + lane, n - 1);
-      oN = offs[jj];
-      DN = lens[jj];
+      const uint64_t jj = std::min<uint64_t>(b + 2 * step + lane, n - 1);
+      mo[u] = offs[jj];
+      mD[u] = lens[jj];
     }
-    const Blk k0 = kq[0];
-    const uint32_t D0 = Dq[0];
+    // text of chunk b + step
+    {
+      const uint32_t D1 = mD[u ^ 1];
+      tr[u ^ 1] = short_issue(buf + mo[u ^ 1], D1, b + step + lane < n && D1 && is_short(D1));
+      tr[u ^ 1].D = D1;
+    }
     const uint64_t j = b + lane;
     const bool valid = j < n;
+    const uint32_t D0 = tr[u].D;
     const uint32_t H = D0 + nul;
-    const bool shrt = H - 1u < 15u;
+    const bool shrt = is_short(D0);
     if (valid && shrt) {
+      const Blk k0 = short_key(tr[u], psel);
       const MeowConst& c = kfull[H];
       const Blk M = c.M;
       Blk S3 = aesdec(bxor(c.F[3], k0), k0, T);
@@ -618,18 +650,19 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
         wave_lds_sync();
       }
     }
-#pragma unroll
-    for (int s = 0; s < P - 1; s++) kq[s] = kq[s + 1];
-    kq[P - 1] = kn;
-#pragma unroll
-    for (int s = 0; s < P; s++) Dq[s] = Dq[s + 1];
+    it++;
+  };
+  for (uint64_t b = b0; b < n; b += 2 * step) {  // wave-uniform trip count
+    body(b, std::integral_constant<int, 0>{});
+    if (b + step >= n) break;
+    body(b + step, std::integral_constant<int, 1>{});
   }
   if (qn) spans_long<NT>(buf, offs, lens, out, q, qn, lane, wave, step, nul, fix, kfull, s1, s2, T);
 }
 
 
 }  // namespace
-namespace kvh { namespace rt { int g_tune_spans = 2; int g_tune_tok = 1; } }
+namespace kvh { namespace rt { int g_tune_spans = 1; int g_tune_tok = 1; } }
 namespace {
 
 TokGeo tok_geo(const void* text, size_t nbytes) {
@@ -705,12 +738,8 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
   if (g_tune_spans)
-    if (g_tune_spans == 2)
-      hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
-                         lens, (uint64_t)n, seed1, seed2, out, flags);
-    else
-      hipLaunchKernelGGL((k_spans<4, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
-                         lens, (uint64_t)n, seed1, seed2, out, flags);
+    hipLaunchKernelGGL((k_spans<4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+                       lens, (uint64_t)n, seed1, seed2, out, flags);
   else
     hipLaunchKernelGGL((k_keysrc<SRC_SPANS, 4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)buf, offs, lens, (uint64_t)n, seed1, seed2, out, flags);
