@@ -484,12 +484,12 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
 template <int NT>
 __device__ __forceinline__ void spans_long(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
                                            const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
-                                           const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t wave, uint64_t step,
-                                           uint32_t nul, bool fix, const MeowConst* kfull, uint64_t s1, uint64_t s2,
-                                           const LdsTab<NT>& T) {
+                                           const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
+                                           uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConst* kfull,
+                                           uint64_t s1, uint64_t s2, const LdsTab<NT>& T) {
   if (lane < cnt) {
     const uint32_t e = q[lane];
-    const uint64_t j = wave * 64 + (uint64_t)(e >> 6) * step + (e & 63u);
+    const uint64_t j = qbase + (uint64_t)(e / CH) * step + (e % CH);
     const uint8_t* p = buf + offs[j];
     const uint32_t D = lens[j], H = D + nul;
     const LdsK<LdsTab<NT>> K(kfull, nullptr, H, s1, s2, T);
@@ -561,14 +561,21 @@ __device__ __forceinline__ Blk short_key(const ShortRaw& r, const uint32_t* __re
   return k;
 }
 
-template <int NT>
+// NH = spans per lane per iteration (NH 64-span halves of a 64*NH-span
+// chunk): their four-round chains are independent, so the LDS latency of one
+// overlaps the other (the kernel is latency-bound at the 4 waves per SIMD its
+// 149 KiB of LDS allow).  The short path is computed for every lane of both
+// halves (zero key for the others) so the chains share one branch.
+template <int NT, int NH>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags) {
   constexpr int NW = 1024 / 64;
+  constexpr uint32_t CH = 64 * NH;  // spans per wave per iteration
+  constexpr uint32_t QCAP = 64 + CH;
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
   __shared__ MeowConst kfull[kLT];
-  __shared__ uint32_t queue[NW][128];
+  __shared__ uint32_t queue[NW][QCAP];
   __shared__ uint32_t psel[16 * 4 * 4];  // [D][p & 3][word] v_perm selectors
   fill_tables<NT>(lds);
   for (uint32_t i = threadIdx.x; i < 16u * 4u * 4u; i += blockDim.x) {
@@ -586,69 +593,89 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   const uint32_t lane = threadIdx.x & 63;
   uint32_t* q = queue[threadIdx.x >> 6];
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t step = ((uint64_t)gridDim.x * blockDim.x) & ~(uint64_t)63;
-  // queue entry e = 64 * (chunk iteration) + lane  ->  span wave*64 + (e>>6)*step + (e&63)
-  uint32_t qn = 0;  // wave-uniform queue length
+  const uint64_t step = (uint64_t)gridDim.x * NW * CH;  // spans per grid iteration
+  // The long-span queue is a stack: entry e = CH * (iteration) + 64 * half + lane
+  // -> span wave*CH + (e / CH) * step + e % CH; full sets of 64 pop off the top.
+  uint32_t qn = 0;  // wave-uniform
+  const uint64_t qbase = wave * CH;
   auto is_short = [nul](uint32_t D) { return D + nul - 1u < 15u; };
   // Pipeline, unrolled by two so that no register is renamed while its load
   // is in flight: iteration c issues the offsets/lengths of chunk c+2 and the
   // text blocks of chunk c+1 (whose offsets arrived during iteration c-1),
   // then hashes chunk c from the blocks issued during iteration c-1.
-  uint64_t mo[2];
-  uint32_t mD[2];
-  ShortRaw tr[2];
-  const uint64_t b0 = wave * 64;
-  {
-    const uint64_t j0 = std::min<uint64_t>(b0 + lane, n - 1), j1 = std::min<uint64_t>(b0 + step + lane, n - 1);
+  uint64_t mo[2][NH];
+  uint32_t mD[2][NH];
+  ShortRaw tr[2][NH];
+  const uint64_t b0 = qbase;
+#pragma unroll
+  for (int h = 0; h < NH; h++) {
+    const uint64_t j0 = std::min<uint64_t>(b0 + 64 * h + lane, n - 1);
+    const uint64_t j1 = std::min<uint64_t>(b0 + step + 64 * h + lane, n - 1);
     const uint64_t o0 = offs[j0];
     const uint32_t D0 = lens[j0];
-    mo[1] = offs[j1];
-    mD[1] = lens[j1];
-    tr[0] = short_issue(buf + o0, D0, b0 + lane < n && D0 && is_short(D0));
-    tr[0].D = D0;  // the length rides with the blocks (0-byte spans load nothing)
+    mo[1][h] = offs[j1];
+    mD[1][h] = lens[j1];
+    tr[0][h] = short_issue(buf + o0, D0, b0 + 64 * h + lane < n && D0 && is_short(D0));
+    tr[0][h].D = D0;  // the length rides with the blocks (0-byte spans load nothing)
   }
   uint32_t it = 0;
   auto body = [&](uint64_t b, auto uc) {
     constexpr int u = decltype(uc)::value;  // slot parity, a compile-time constant
-    // offsets of chunk b + 2 step into slot u (chunk b's slot, consumed)
-    {
-      const uint64_t jj = std::min<uint64_t>(b + 2 * step + lane, n - 1);
-      mo[u] = offs[jj];
-      mD[u] = lens[jj];
+#pragma unroll
+    for (int h = 0; h < NH; h++) {  // offsets of chunk b + 2 step into slot u (chunk b's, consumed)
+      const uint64_t jj = std::min<uint64_t>(b + 2 * step + 64 * h + lane, n - 1);
+      mo[u][h] = offs[jj];
+      mD[u][h] = lens[jj];
     }
-    // text of chunk b + step
-    {
-      const uint32_t D1 = mD[u ^ 1];
-      tr[u ^ 1] = short_issue(buf + mo[u ^ 1], D1, b + step + lane < n && D1 && is_short(D1));
-      tr[u ^ 1].D = D1;
+#pragma unroll
+    for (int h = 0; h < NH; h++) {  // text of chunk b + step
+      const uint32_t D1 = mD[u ^ 1][h];
+      tr[u ^ 1][h] = short_issue(buf + mo[u ^ 1][h], D1, b + step + 64 * h + lane < n && D1 && is_short(D1));
+      tr[u ^ 1][h].D = D1;
     }
-    const uint64_t j = b + lane;
-    const bool valid = j < n;
-    const uint32_t D0 = tr[u].D;
-    const uint32_t H = D0 + nul;
-    const bool shrt = is_short(D0);
-    if (valid && shrt) {
-      const Blk k0 = short_key(tr[u], psel);
-      const MeowConst& c = kfull[H];
-      const Blk M = c.M;
-      Blk S3 = aesdec(bxor(c.F[3], k0), k0, T);
-      S3 = aesdec(S3, M, T);
-      const Blk S2 = aesdec(bxor(c.TG2, S3), M, T);
-      store_h(out, j, aesdec(bxor(c.TCS0a, S2), M, T), fix);
+    bool valid[NH], shrt[NH];
+    Blk hh[NH];
+    uint32_t any = 0;
+#pragma unroll
+    for (int h = 0; h < NH; h++) {
+      valid[h] = b + 64 * h + lane < n;
+      shrt[h] = is_short(tr[u][h].D);
+      any |= (valid[h] && shrt[h]) ? 1u : 0u;
     }
-    const uint64_t lm = __ballot(valid && !shrt);
-    if (lm) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-      if (valid && !shrt) q[qn + below] = 64u * it + lane;
-      qn += (uint32_t)__popcll(lm);
-      wave_lds_sync();
-      if (qn >= 64) {
-        spans_long<NT>(buf, offs, lens, out, q, 64, lane, wave, step, nul, fix, kfull, s1, s2, T);
-        wave_lds_sync();
-        qn -= 64;
-        if (lane < qn) q[lane] = q[64 + lane];  // move the overflow to the front
-        wave_lds_sync();
+    if (any) {
+#pragma unroll
+      for (int h = 0; h < NH; h++) {
+        const uint32_t D0 = shrt[h] ? tr[u][h].D : 0u;  // long / invalid lanes hash a zero key, discarded
+        ShortRaw r = tr[u][h];
+        r.D = D0;
+        const Blk k0 = short_key(r, psel);
+        const MeowConst& c = kfull[D0 + nul];
+        const Blk M = c.M;
+        Blk S3 = aesdec(bxor(c.F[3], k0), k0, T);
+        S3 = aesdec(S3, M, T);
+        const Blk S2 = aesdec(bxor(c.TG2, S3), M, T);
+        hh[h] = aesdec(bxor(c.TCS0a, S2), M, T);
       }
+#pragma unroll
+      for (int h = 0; h < NH; h++)
+        if (valid[h] && shrt[h]) store_h(out, b + 64 * h + lane, hh[h], fix);
+    }
+#pragma unroll
+    for (int h = 0; h < NH; h++) {
+      const uint64_t lm = __ballot(valid[h] && !shrt[h]);
+      if (lm) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
+        if (valid[h] && !shrt[h]) q[qn + below] = CH * it + 64 * h + lane;
+        qn += (uint32_t)__popcll(lm);
+      }
+    }
+    if (qn >= 64) {
+      wave_lds_sync();
+      do {
+        spans_long<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
+        qn -= 64;
+      } while (qn >= 64);
+      wave_lds_sync();
     }
     it++;
   };
@@ -657,12 +684,15 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
     if (b + step >= n) break;
     body(b + step, std::integral_constant<int, 1>{});
   }
-  if (qn) spans_long<NT>(buf, offs, lens, out, q, qn, lane, wave, step, nul, fix, kfull, s1, s2, T);
+  if (qn) {
+    wave_lds_sync();
+    spans_long<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
+  }
 }
 
 
 }  // namespace
-namespace kvh { namespace rt { int g_tune_spans = 1; int g_tune_tok = 1; } }
+namespace kvh { namespace rt { int g_tune_spans = 2; int g_tune_tok = 1; } }
 namespace {
 
 TokGeo tok_geo(const void* text, size_t nbytes) {
@@ -737,8 +767,11 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
-  if (g_tune_spans)
-    hipLaunchKernelGGL((k_spans<4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+  if (g_tune_spans == 2)
+    hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+                       lens, (uint64_t)n, seed1, seed2, out, flags);
+  else if (g_tune_spans == 1)
+    hipLaunchKernelGGL((k_spans<4, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);
   else
     hipLaunchKernelGGL((k_keysrc<SRC_SPANS, 4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream,

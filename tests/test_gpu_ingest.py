@@ -148,7 +148,7 @@ def test_large_text_property(kvh, tok_kernel):
         np.testing.assert_array_equal(l[a], wl[inner])
 
 
-@pytest.mark.parametrize("kernel", [0, 1])
+@pytest.mark.parametrize("kernel", [0, 1, 2])
 @pytest.mark.parametrize("nulterm", [True, False])
 def test_spans_kernels_vs_oracle(kvh, kernel, nulterm):
     """Both span kernels (lane per span; short spans in place with the long

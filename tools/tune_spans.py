@@ -18,9 +18,9 @@ offs, lens = kvh.tokenize(text, 256)
 k = offs.numel()
 out = torch.empty((k, 2), dtype=torch.int64, device="cuda")
 st = torch.cuda.current_stream()
-ref, res = None, {0: [], 1: []}
+ref, res = None, {0: [], 1: [], 2: []}
 for rnd in range(3):
-    for v in (0, 1):
+    for v in (0, 1, 2):
         kvh.lib.kvh_set_tuning(18, v)
         kvh.meow128_spans(text, offs, lens, kvh.STATIC_SEED, out=out)
         torch.cuda.synchronize()
