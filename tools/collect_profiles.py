@@ -10,10 +10,11 @@ dst = os.path.join(root, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 HOT = ("k_fixed", "k_var", "k_generic", "k_fixed_ms", "k_fixed_dma")
 HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",), "f4": ("k_crc_fixed",), "f4v": ("k_crc_var",),
-              "f3": ("k_tok<true>", "k_keysrc"), "c2": ("k_var6",), "c3": ("k_fixed_lanes",)}
+              "c2": ("k_var6",), "c3": ("k_fixed_lanes",)}
 # configs whose unit of work is one call of several kernels: (kernel name parts,
 # calls in the PMC run (run_kernel.py --reps), calls in the traced bench run (W + K))
-MULTI = {"f2": (("k_sort", "onesweep", "radix", "rocprim"), 5, 200)}
+MULTI = {"f2": (("k_sort", "onesweep", "radix", "rocprim"), 5, 200),
+         "f3": (("k_tok", "k_spans"), 5, 200)}
 tpath = os.path.join(root, "profiles", "pmc_traffic.json")
 spath = os.path.join(dst, "summary.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
