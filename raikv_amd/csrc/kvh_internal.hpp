@@ -92,21 +92,39 @@ __device__ __forceinline__ void wave_lds_sync() {
 // r_len (u16, 65535 = "re-read the offsets"), r_idx (u16 index in window).
 // Returns the window's first byte offset.  Used by the length-sorted
 // variable-length kernels (k_crc_var_sorted; k_var6 inlines the same steps).
+// The offsets of a window (raw, as loaded), so that a kernel can load the
+// next window's while it hashes the current one.
 template <int WIN>
-__device__ __forceinline__ uint64_t wave_sort_window(const uint64_t* __restrict__ offs, uint64_t i0, uint32_t k,
-                                                     uint32_t* hist, uint32_t* r_off, uint16_t* r_len,
-                                                     uint16_t* r_idx) {
+struct WinOffs {
+  uint64_t ws, a[WIN / 64], e[WIN / 64];
+};
+
+template <int WIN>
+__device__ __forceinline__ WinOffs<WIN> win_load(const uint64_t* __restrict__ offs, uint64_t i0, uint32_t k) {
+  WinOffs<WIN> w;
+  const uint32_t lane = threadIdx.x & 63;
+  w.ws = offs[i0];
+#pragma unroll
+  for (int m = 0; m < WIN / 64; m++) {
+    const uint32_t j = lane + 64 * m;
+    const uint32_t jj = j < k ? j : k - 1;
+    w.a[m] = offs[i0 + jj];
+    w.e[m] = offs[i0 + jj + 1];
+  }
+  return w;
+}
+
+template <int WIN>
+__device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32_t k, uint32_t* hist,
+                                                   uint32_t* r_off, uint16_t* r_len, uint16_t* r_idx) {
   constexpr int M = WIN / 64;
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t ws = offs[i0];
+  const uint64_t ws = W.ws;
   uint32_t o[M], L[M], r[M];
 #pragma unroll
   for (int m = 0; m < M; m++) {
-    const uint32_t j = lane + 64 * m;
-    const uint32_t jj = j < k ? j : k - 1;
-    const uint64_t a = offs[i0 + jj], e = offs[i0 + jj + 1];
-    o[m] = (uint32_t)(a - ws);
-    L[m] = e - a < 65535 ? (uint32_t)(e - a) : 65535u;
+    o[m] = (uint32_t)(W.a[m] - ws);
+    L[m] = W.e[m] - W.a[m] < 65535 ? (uint32_t)(W.e[m] - W.a[m]) : 65535u;
   }
 #pragma unroll
   for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
@@ -144,6 +162,13 @@ __device__ __forceinline__ uint64_t wave_sort_window(const uint64_t* __restrict_
   }
   wave_lds_sync();
   return ws;
+}
+
+template <int WIN>
+__device__ __forceinline__ uint64_t wave_sort_window(const uint64_t* __restrict__ offs, uint64_t i0, uint32_t k,
+                                                     uint32_t* hist, uint32_t* r_off, uint16_t* r_len,
+                                                     uint16_t* r_idx) {
+  return wave_sort_from<WIN>(win_load<WIN>(offs, i0, k), k, hist, r_off, r_len, r_idx);
 }
 
 namespace rt {
