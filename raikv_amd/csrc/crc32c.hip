@@ -253,7 +253,7 @@ __device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, u
 // go through the wave's LDS slice back to input order and leave as one
 // contiguous run.  NW waves per workgroup: the 128 KiB of replicated tables
 // leave room for NW * 3 KiB of window state.
-template <int WIN, int NW>
+template <int WIN, int NW, int SH = 0>
 __global__ void __launch_bounds__(NW * 64)
 k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
                  const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out
@@ -273,7 +273,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
   for (uint64_t w = (uint64_t)blockIdx.x * NW + wv; w < nwin; w += (uint64_t)gridDim.x * NW) {
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
-    const uint64_t ws = wave_sort_window<WIN>(offs, i0, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
+    const uint64_t ws = wave_sort_window<WIN, SH>(offs, i0, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
     // (running the lane's M keys as interleaved chains was slower: each
     // lane then steps as long as its longest key, chunk M-1's)
     uint32_t crc[M], ix[M];

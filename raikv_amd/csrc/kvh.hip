@@ -884,7 +884,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int NT, int WIN, bool PF = false, int NW = kBlock / 64>
+template <int NT, int WIN, bool PF = false, int NW = kBlock / 64, int SH = 0>
 __global__ void __launch_bounds__(NW * 64)
 k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -942,7 +942,7 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 #pragma unroll
     for (int m = 0; m < M; m++) {
       const uint32_t j = lane + 64 * m;
-      b[m] = L[m] < 255u ? L[m] : 255u;
+      b[m] = (L[m] >> SH) < 255u ? (L[m] >> SH) : 255u;  // SH: see wave_sort_from
       r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
     }
     wave_sync();
@@ -1218,7 +1218,7 @@ int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
 int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
 int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
 int g_tune_var_mode = 0;  // ablation of k_var3: 1 no-hash, 2 no-gather, 3 no-sort
-int g_tune_var = 7;       // var-length kernel: 7 = k_var6 (per-wave sorted windows); 0 = unsorted k_generic; 2-6, 8-12 experiments
+int g_tune_var = 13;      // var-length kernel: 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic; 2-6, 8-12 experiments
 
 uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
   const uint64_t need = (n + kBlock - 1) / kBlock;
@@ -1534,11 +1534,12 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
     return launch_generic(true, (const uint8_t*)keys, offsets, 0, n, s, 1, out, flags, (hipStream_t)stream,
                           cus);
   }
-  if (g_tune_var >= 7 && g_tune_var <= 12) {
+  if (g_tune_var >= 7 && g_tune_var <= 13) {
     const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
     hipStream_t st = (hipStream_t)stream;
     const uint8_t* kp = (const uint8_t*)keys;
     switch (g_tune_var) {
+      case 13: hipLaunchKernelGGL((k_var6<2, 256, false, kBlock / 64, 4>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
       case 11: hipLaunchKernelGGL((k_var6<2, 384, false, 12>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
       case 12: hipLaunchKernelGGL((k_var6<2, 512, false, 10>), dim3(cus), dim3(640), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
       case 7: hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
@@ -1945,7 +1946,7 @@ int kvh_set_tuning(int knob, int value) {
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
     case 9: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_var_mode; g_tune_var_mode = value; return prev;
     case 8: prev = g_tune_ms_lanes; g_tune_ms_lanes = value ? 1 : 0; return prev;
-    case 7: if (value < 0 || value > 12 || value == 1) return KVH_EINVAL;
+    case 7: if (value < 0 || value > 13 || value == 1) return KVH_EINVAL;
             prev = g_tune_var; g_tune_var = value; return prev;
     case 6: if (value != 0 && value != 2 && value != 3 && value != 4 && value != 6) return KVH_EINVAL;
             prev = g_tune_dma; g_tune_dma = value; return prev;

@@ -114,7 +114,11 @@ __device__ __forceinline__ WinOffs<WIN> win_load(const uint64_t* __restrict__ of
   return w;
 }
 
-template <int WIN>
+// SH: bucket = min(len >> SH, 255).  SH = 0 sorts by exact length; SH = 4 by
+// 16-byte class (same full-block count, so the same trip counts), which keeps
+// a class in address order (the counting sort is stable) and so coalesces
+// the chunk's key gathers.
+template <int WIN, int SH = 0>
 __device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32_t k, uint32_t* hist,
                                                    uint32_t* r_off, uint16_t* r_len, uint16_t* r_idx) {
   constexpr int M = WIN / 64;
@@ -132,7 +136,7 @@ __device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32
 #pragma unroll
   for (int m = 0; m < M; m++) {
     const uint32_t j = lane + 64 * m;
-    r[m] = j < k ? atomicAdd(&hist[L[m] < 255u ? L[m] : 255u], 1u) : 0u;
+    r[m] = j < k ? atomicAdd(&hist[(L[m] >> SH) < 255u ? (L[m] >> SH) : 255u], 1u) : 0u;
   }
   wave_lds_sync();
   {
@@ -154,7 +158,7 @@ __device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32
   for (int m = 0; m < M; m++) {
     const uint32_t j = lane + 64 * m;
     if (j < k) {
-      const uint32_t pos = hist[L[m] < 255u ? L[m] : 255u] + r[m];
+      const uint32_t pos = hist[(L[m] >> SH) < 255u ? (L[m] >> SH) : 255u] + r[m];
       r_off[pos] = o[m];
       r_len[pos] = (uint16_t)L[m];
       r_idx[pos] = (uint16_t)j;
@@ -164,11 +168,11 @@ __device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32
   return ws;
 }
 
-template <int WIN>
+template <int WIN, int SH = 0>
 __device__ __forceinline__ uint64_t wave_sort_window(const uint64_t* __restrict__ offs, uint64_t i0, uint32_t k,
                                                      uint32_t* hist, uint32_t* r_off, uint16_t* r_len,
                                                      uint16_t* r_idx) {
-  return wave_sort_from<WIN>(win_load<WIN>(offs, i0, k), k, hist, r_off, r_len, r_idx);
+  return wave_sort_from<WIN, SH>(win_load<WIN>(offs, i0, k), k, hist, r_off, r_len, r_idx);
 }
 
 namespace rt {

@@ -297,3 +297,27 @@ def test_cpp_hash_test_program(kvh):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("variant", [0, 7, 13])
+def test_var_kernel_variants_vs_oracle(kvh, variant):
+    """The variable-length kernels (kvh_set_tuning(7, v): 0 unsorted, 7
+    length-sorted windows, 13 windows sorted by 16-byte length class) against
+    the oracle: zipf 8-256 B plus 0..300-byte and 70 000-byte keys, odd counts
+    for ragged last windows, at an unaligned base."""
+    from raikv_amd.workload import zipf_lengths
+    rng = np.random.default_rng(variant)
+    for n in (1, 255, 257, 4099, 100003):
+        lens = zipf_lengths(n, 8, 256, seed=n).astype(np.int64)
+        if n > 300:
+            lens[rng.integers(0, n, 300)] = rng.integers(0, 301, 300)
+            lens[rng.integers(0, n)] = 70000
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + 3
+        keys = rng.integers(0, 256, int(offs[-1]) + 5, dtype=np.uint8)
+        want = orc_var(ORC, keys, offs, STATIC)
+        prev = kvh.lib.kvh_set_tuning(7, variant)
+        try:
+            got = u64(kvh.meow128_var(dev(keys), dev_u64(offs), STATIC))
+        finally:
+            kvh.lib.kvh_set_tuning(7, prev)
+        np.testing.assert_array_equal(got, want, err_msg=f"n={n}")
