@@ -333,17 +333,17 @@ def main():
         t_lens = torch.empty((cap,), dtype=torch.int32, device="cuda")
         t_cnt = torch.zeros((1,), dtype=torch.int64, device="cuda")
         t_scr = torch.empty((kvh.lib.kvh_tokenize_scratch_bytes(n) // 8 + 1,), dtype=torch.int64, device="cuda")
-        t_out = torch.empty((ntok, 2), dtype=torch.int64, device="cuda")
+        t_out = torch.empty((cap, 2), dtype=torch.int64, device="cuda")
         import ctypes as _C
 
         def run(out):
+            # one asynchronous call: tokenizer, then the span hash reading the
+            # token count on the device (no host round trip in between)
             st = torch.cuda.current_stream().cuda_stream
-            rc = kvh.lib.kvh_tokenize(text.data_ptr(), n, 256, t_offs.data_ptr(), t_lens.data_ptr(), cap,
-                                      t_cnt.data_ptr(), t_scr.data_ptr(), t_scr.numel() * 8, st)
-            assert rc == 0
-            rc = kvh.lib.kvh_meow128_spans(text.data_ptr(), t_offs.data_ptr(), t_lens.data_ptr(), ntok,
-                                           _C.c_uint64(seed[0]), _C.c_uint64(seed[1]), t_out.data_ptr(),
-                                           kvh.KVH_FIXUP | kvh.KVH_NULTERM, st)
+            rc = kvh.lib.kvh_tokenize_hash(text.data_ptr(), n, 256, _C.c_uint64(seed[0]), _C.c_uint64(seed[1]),
+                                           kvh.KVH_FIXUP | kvh.KVH_NULTERM, t_offs.data_ptr(), t_lens.data_ptr(),
+                                           t_out.data_ptr(), cap, t_cnt.data_ptr(), t_scr.data_ptr(),
+                                           t_scr.numel() * 8, st)
             assert rc == 0
         # text read twice (count + emit passes) + spans written/read + key bytes gathered + hashes
         alg_bytes = n + 12 * ntok + 16 * ntok

@@ -288,6 +288,20 @@ int kvh_tokenize(const void *text, size_t nbytes, uint32_t max_token,
                  uint64_t *count, void *scratch, size_t scratch_bytes,
                  void *stream);
 
+/* Tokenize and hash in one asynchronous call: ctest's ingest loop
+ * (ctest.c:202-233, a kv_hash_key_frag of every kept token,
+ * key_ctx.cpp:1774-1783) as kvh_tokenize followed by kvh_meow128_spans over
+ * its tokens, the span hash reading the token count from the device (no
+ * host round trip between the two).  out: cap x 2 u64, hashes of the first
+ * min(count, cap) tokens in text order; flags as kvh_meow128_spans
+ * (KVH_NULTERM | KVH_FIXUP for kv_hash_key_frag).  Same scratch as
+ * kvh_tokenize. */
+int kvh_tokenize_hash(const void *text, size_t nbytes, uint32_t max_token,
+                      uint64_t seed1, uint64_t seed2, uint32_t flags,
+                      uint64_t *tok_offs, uint32_t *tok_lens, uint64_t *out,
+                      size_t cap, uint64_t *count, void *scratch,
+                      size_t scratch_bytes, void *stream);
+
 /* Meow128 of n keys given as (offset, length) spans into buf (device).
  * With KVH_NULTERM the hashed key is the span followed by one 0 byte that
  * need not be in buf: a token becomes the kv_key_frag_t "token\0" of

@@ -13,6 +13,7 @@ from .binding import (  # noqa: F401
     HtGeom,
     crc_c_fixed,
     tokenize,
+    tokenize_hash,
     HtSorter,
     KVH_DEDUP,
     meow128_spans,
@@ -43,5 +44,5 @@ __all__ = [
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "host_empty", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
     "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
-    "tokenize", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP",
+    "tokenize", "tokenize_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP",
 ]

@@ -112,6 +112,7 @@ def _load():
         "kvh_crc_c_key_array": (I, [P, P, P, SZ]),
         "kvh_tokenize_scratch_bytes": (SZ, [SZ]),
         "kvh_tokenize": (I, [P, SZ, U32, P, P, SZ, P, P, SZ, P]),
+        "kvh_tokenize_hash": (I, [P, SZ, U32, U64, U64, U32, P, P, P, SZ, P, P, SZ, P]),
         "kvh_meow128_spans": (I, [P, P, P, SZ, U64, U64, P, U32, P]),
         "kvh_meow128_frags": (I, [P, P, SZ, U64, U64, P, U32, P]),
         "kvh_ht_sort_scratch_bytes": (SZ, [SZ]),
@@ -246,6 +247,28 @@ def tokenize(text, max_token: int = 256, cap: Optional[int] = None, stream=None)
                            _dev_ptr(cnt), _dev_ptr(scratch), scratch.numel() * 8, _stream_ptr(stream)), "kvh_tokenize")
     k = int(cnt.item())
     return offs[:min(k, cap)], lens[:min(k, cap)]
+
+
+def tokenize_hash(text, seed: Tuple[int, int], max_token: int = 256, cap: Optional[int] = None, fixup: bool = True,
+                  nulterm: bool = True, stream=None):
+    """kvh_tokenize + kvh_meow128_spans in one asynchronous call (ctest.c:202-233
+    with a kv_hash_key_frag per token; the count stays on the device) ->
+    (offsets int64 [k], lengths int32 [k], hashes int64 [k, 2])."""
+    n = text.numel()
+    cnt = torch.zeros((1,), dtype=torch.int64, device=text.device)
+    scratch = torch.empty((max(1, lib.kvh_tokenize_scratch_bytes(n) // 8),), dtype=torch.int64, device=text.device)
+    if cap is None:
+        cap = n // 2 + 1
+    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=text.device)
+    lens = torch.empty((max(cap, 1),), dtype=torch.int32, device=text.device)
+    out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=text.device)
+    check(lib.kvh_tokenize_hash(_dev_ptr(text) if n else None, n, max_token, U64(seed[0] & (2**64 - 1)),
+                                U64(seed[1] & (2**64 - 1)),
+                                (KVH_FIXUP if fixup else 0) | (KVH_NULTERM if nulterm else 0), _dev_ptr(offs),
+                                _dev_ptr(lens), _dev_ptr(out), cap, _dev_ptr(cnt), _dev_ptr(scratch),
+                                scratch.numel() * 8, _stream_ptr(stream)), "kvh_tokenize_hash")
+    k = min(int(cnt.item()), cap)
+    return offs[:k], lens[:k], out[:k]
 
 
 def meow128_spans(buf, offs, lens, seed: Tuple[int, int], out=None, fixup: bool = True, nulterm: bool = True,

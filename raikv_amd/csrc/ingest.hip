@@ -569,7 +569,8 @@ __device__ __forceinline__ Blk short_key(const ShortRaw& r, const uint32_t* __re
 template <int NT, int NH>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
-        uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags) {
+        uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
+        const uint64_t* __restrict__ dcount = nullptr) {  // dcount: n = min(n, *dcount), read on the device
   constexpr int NW = 1024 / 64;
   constexpr uint32_t CH = 64 * NH;  // spans per wave per iteration
   constexpr uint32_t QCAP = 64 + CH;
@@ -588,6 +589,11 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   const LdsTab<NT> T(lds);
   for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) kfull[l] = make_const(s1, s2, l, T);
   __syncthreads();
+  if (dcount) {  // no barrier follows
+    const uint64_t dn = *dcount;
+    n = dn < n ? dn : n;
+  }
+  if (n == 0) return;
   const bool fix = (flags & KVH_FIXUP) != 0;
   const uint32_t nul = (flags & KVH_NULTERM) ? 1u : 0u;
   const uint32_t lane = threadIdx.x & 63;
@@ -757,6 +763,22 @@ int kvh_tokenize(const void* text, size_t nbytes, uint32_t max_token, uint64_t* 
   if (cap == 0) return set_err(0);
   hipLaunchKernelGGL(k_tok<true>, dim3((uint32_t)nc), dim3(kTokBlock), 0, st, t, G, max_token, cc, tok_offs,
                      tok_lens, (uint64_t)cap);
+  return launch_done();
+}
+
+int kvh_tokenize_hash(const void* text, size_t nbytes, uint32_t max_token, uint64_t seed1, uint64_t seed2,
+                      uint32_t flags, uint64_t* tok_offs, uint32_t* tok_lens, uint64_t* out, size_t cap,
+                      uint64_t* count, void* scratch, size_t scratch_bytes, void* stream) {
+  if (cap && !out) return set_err(KVH_EINVAL);
+  int rc = kvh_tokenize(text, nbytes, max_token, tok_offs, tok_lens, cap, count, scratch, scratch_bytes, stream);
+  if (rc || cap == 0 || nbytes == 0) return rc;
+  int cus = 0;
+  rc = device_cus(&cus);
+  if (rc) return rc;
+  // the span hash takes its count from the device: no host round trip
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((cap + 1023) / 1024, (uint64_t)cus));
+  hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)text,
+                     tok_offs, tok_lens, (uint64_t)cap, seed1, seed2, out, flags, (const uint64_t*)count);
   return launch_done();
 }
 

@@ -170,3 +170,41 @@ def test_spans_kernels_vs_oracle(kvh, kernel, nulterm):
             np.testing.assert_array_equal(host(h), orc_hash_spans(ORC, buf, offs, lens, SEED, nul=nulterm))
         finally:
             kvh.lib.kvh_set_tuning(18, prev)
+
+
+@pytest.mark.parametrize("max_token", [1, 5, 16, 17, 256, 5000, 40000])
+def test_tokenize_hash_fused_vs_oracle(kvh, max_token):
+    """kvh_tokenize_hash (tokenizer, then the span hash reading the token count
+    on the device) against the oracle's tokens and span hashes, with and
+    without the NUL, at three text misalignments; the golden text against the
+    reference's own kv_hash_key_frag hashes, also with cap below the count."""
+    rng = np.random.default_rng(max_token + 1)
+    for shift, n, nul in ((0, 1 << 20, True), (3, 300001, False), (13, 16384 * 3 + 5, True)):
+        arr = np.concatenate([np.full(shift, 35, np.uint8), _mixed_text(rng, n)])
+        dev = torch.from_numpy(arr).cuda()[shift:]
+        o, l, h = kvh.tokenize_hash(dev, SEED, max_token, nulterm=nul)
+        wo, wl = orc_tokenize(ORC, arr[shift:], max_token)
+        np.testing.assert_array_equal(host(o), wo)
+        np.testing.assert_array_equal(host(l), wl)
+        np.testing.assert_array_equal(host(h), orc_hash_spans(ORC, arr[shift:], wo, wl, SEED, nul=nul))
+    if max_token == 256:
+        o, l, h = kvh.tokenize_hash(torch.from_numpy(G["text"]).cuda(), SEED, 256)
+        np.testing.assert_array_equal(host(h), G["hashes"])
+        _, _, hc = kvh.tokenize_hash(torch.from_numpy(G["text"]).cuda(), SEED, 256, cap=100)
+        np.testing.assert_array_equal(host(hc), G["hashes"][:100])
+
+
+def test_tokenize_hash_large_text(kvh):
+    """1 GiB of f3 text: one-call hashes equal tokenize + span hash, bit for bit."""
+    n = 1 << 30
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(12)
+    r = torch.randint(0, 8, (n,), dtype=torch.uint8, device="cuda", generator=gen)
+    text = torch.where(r == 0, 32, torch.where(r == 1, 10, 97 + r)).to(torch.uint8)
+    del r
+    o, l, h = kvh.tokenize_hash(text, SEED, 256)
+    o2, l2 = kvh.tokenize(text, 256)
+    assert torch.equal(o, o2) and torch.equal(l, l2)
+    del o2
+    h2 = kvh.meow128_spans(text, o, l2, SEED)
+    assert torch.equal(h, h2)
