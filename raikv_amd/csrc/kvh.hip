@@ -1210,10 +1210,10 @@ int g_tune_nt = 0;        // tables per LDS: 2 or 4 (0 = per-length default)
 int g_tune_wgmul = 1;     // workgroups per CU multiplier
 int g_tune_generic = 0;   // force the generic kernel
 int g_tune_kpl = 0;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8; 0 = per-length default)
-int g_tune_pf = 0;
+int g_tune_pf = 0;        // k_fixed: 1 = register prefetch of the next chunk
 int g_tune_bs = 0;        // hybrid kernel: bitsliced share of the keys in per mille (0 = k_fixed)
-int g_tune_bsw = 4;
-int g_tune_prio = 2;      // hybrid kernel: s_setprio of the T-table waves (0, 2, 3)       // hybrid kernel: bitsliced waves per 16-wave workgroup        // k_fixed: 1 = register prefetch of the next chunk
+int g_tune_bsw = 4;       // hybrid kernel: bitsliced waves per 16-wave workgroup
+int g_tune_prio = 2;      // hybrid kernel: s_setprio of the T-table waves (0, 2, 3)
 int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
 int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
 int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
