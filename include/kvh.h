@@ -370,8 +370,9 @@ int         kvh_device_synchronize(void);
  * 11 = bitsliced share of a 16-byte batch in per mille (0 = T-table only),
  * 14 = variable-length CRC32C kernel (1 length-sorted windows, 0 input order),
  * 15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort key bits (0 auto),
- * 18 = span-hash kernel (2 / 1 short spans in place + per-wave long queue,
- *      two / one spans per lane per step; 0 lane per span),
+ * 18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
+ *      long queues, two / one spans per lane per step; 0 lane per span;
+ *      3, 4 ablations whose outputs are NOT hashes: no rounds; no text),
  * 19 = tokenizer (1 wave-chunked, 0 workgroup-chunked).
  * Returns the previous value or KVH_EINVAL. */
 int         kvh_set_tuning(int knob, int value);

@@ -566,20 +566,100 @@ __device__ __forceinline__ Blk short_key(const ShortRaw& r, const uint32_t* __re
 // overlaps the other (the kernel is latency-bound at the 4 waves per SIMD its
 // 149 KiB of LDS allow).  The short path is computed for every lane of both
 // halves (zero key for the others) so the chains share one branch.
-template <int NT, int NH>
+// Medium spans, 16..31 hashed bytes (nb = 0, C = 16, t = H - 16): S0 absorbs
+// bytes [0, 16), S3 the trail [16, H) when t != 0, then Mix / Compress2 /
+// Compress fold to eight table rounds with no branch (the t = 0 case takes
+// CS2b in place of the trail's Compress2).  Bytes from up to three aligned
+// 16-byte blocks, each clamped to the block holding the span's last byte
+// (never past its pages), funnelled like the short key.
+struct MedRaw {
+  v4u A, B, C;
+  uint32_t s;
+};
+__device__ __forceinline__ MedRaw med_issue(const uint8_t* __restrict__ p, uint32_t L) {  // L >= 1
+  MedRaw r;
+  const uint32_t a = (uint32_t)(uintptr_t)p & 15u;
+  r.s = a;
+  const uint8_t* blk = p - a;                                         // block of the first byte
+  const uint32_t lastoff = (a + L - 1) & ~15u;                        // last byte's block, from blk
+  r.A = *(const v4u*)blk;
+  r.B = *(const v4u*)(blk + (16u < lastoff ? 16u : lastoff));
+  r.C = *(const v4u*)(blk + (32u < lastoff ? 32u : lastoff));
+  return r;
+}
+__device__ __forceinline__ Blk funnel(const uint32_t (&w)[8], uint32_t s, uint32_t D, const uint32_t* __restrict__ psel) {
+  uint32_t x[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) x[i] = w[i];
+  if (s & 8) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) x[i] = x[i + 2];
+  }
+  if (s & 4) {
+#pragma unroll
+    for (int i = 0; i < 5; i++) x[i] = x[i + 1];
+  }
+  const v4u sel = *(const v4u*)(psel + 4 * (4 * D + (s & 3u)));
+  Blk k;
+  k.w[0] = __builtin_amdgcn_perm(x[1], x[0], sel.x);
+  k.w[1] = __builtin_amdgcn_perm(x[2], x[1], sel.y);
+  k.w[2] = __builtin_amdgcn_perm(x[3], x[2], sel.z);
+  k.w[3] = __builtin_amdgcn_perm(x[4], x[3], sel.w);
+  return k;
+}
+template <class Tab>
+__device__ __forceinline__ Blk meow_medium(const MedRaw& r, uint32_t L, uint32_t H, const MeowConst& c,
+                                           const uint32_t* __restrict__ psel, const Tab& T) {
+  const uint32_t wAB[8] = {r.A.x, r.A.y, r.A.z, r.A.w, r.B.x, r.B.y, r.B.z, r.B.w};
+  const uint32_t wBC[8] = {r.B.x, r.B.y, r.B.z, r.B.w, r.C.x, r.C.y, r.C.z, r.C.w};
+  const Blk k0 = funnel(wAB, r.s, L < 16 ? L : 16u, psel);
+  const Blk k3 = funnel(wBC, r.s, L > 16 ? L - 16 : 0u, psel);
+  const Blk M = c.M;
+  Blk S0 = aesdec(bxor(c.F[0], k0), k0, T);
+  S0 = aesdec(S0, M, T);
+  Blk S3 = aesdec(bxor(c.F[3], k3), k3, T);
+  S3 = aesdec(S3, M, T);
+  const Blk S2t = aesdec(bxor(c.TG2, S3), M, T);
+  const bool t = H != 16;
+  Blk S2b;
+#pragma unroll
+  for (int i = 0; i < 4; i++) S2b.w[i] = t ? S2t.w[i] : c.CS2b.w[i];
+  const Blk S0b = aesdec(aesdec(S0, c.G[1], T), S2b, T);
+  return aesdec(S0b, M, T);
+}
+
+// hash the queued medium spans q[0 .. cnt) (cnt <= 64), lane per entry
+template <int NT>
+__device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
+                                             const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
+                                             const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
+                                             uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConst* kfull,
+                                             const uint32_t* __restrict__ psel, const LdsTab<NT>& T) {
+  if (lane < cnt) {
+    const uint32_t e = q[lane];
+    const uint64_t j = qbase + (uint64_t)(e / CH) * step + (e % CH);
+    const uint32_t L = lens[j], H = L + nul;
+    const MedRaw r = med_issue(buf + offs[j], L);
+    store_h(out, j, meow_medium(r, L, H, kfull[H], psel, T), fix);
+  }
+}
+
+template <int NT, int NH, int ABL = 0, int PD = 2>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
         const uint64_t* __restrict__ dcount = nullptr) {  // dcount: n = min(n, *dcount), read on the device
   constexpr int NW = 1024 / 64;
   constexpr uint32_t CH = 64 * NH;  // spans per wave per iteration
-  constexpr uint32_t QCAP = 64 + CH;
+  // medium spans stack up from 0, longer ones down from QCAP - 1; each holds
+  // < 64 after a flush and an iteration adds <= CH to the two together
+  constexpr uint32_t QCAP = 2 * 64 + CH;
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
   __shared__ MeowConst kfull[kLT];
   __shared__ uint32_t queue[NW][QCAP];
-  __shared__ uint32_t psel[16 * 4 * 4];  // [D][p & 3][word] v_perm selectors
+  __shared__ uint32_t psel[17 * 4 * 4];  // [D 0..16][p & 3][word] v_perm selectors
   fill_tables<NT>(lds);
-  for (uint32_t i = threadIdx.x; i < 16u * 4u * 4u; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < 17u * 4u * 4u; i += blockDim.x) {
     const uint32_t c = i & 3u, sh = (i >> 2) & 3u, D = i >> 4;
     uint32_t v = 0;
     for (uint32_t k = 0; k < 4; k++) v |= (4 * c + k < D ? sh + k : 0x0cu) << (8 * k);
@@ -602,42 +682,48 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   const uint64_t step = (uint64_t)gridDim.x * NW * CH;  // spans per grid iteration
   // The long-span queue is a stack: entry e = CH * (iteration) + 64 * half + lane
   // -> span wave*CH + (e / CH) * step + e % CH; full sets of 64 pop off the top.
-  uint32_t qn = 0;  // wave-uniform
+  uint32_t qn = 0, ql = 0;  // wave-uniform: medium (16..31 hashed bytes) and long queue depths
   const uint64_t qbase = wave * CH;
   auto is_short = [nul](uint32_t D) { return D + nul - 1u < 15u; };
-  // Pipeline, unrolled by two so that no register is renamed while its load
-  // is in flight: iteration c issues the offsets/lengths of chunk c+2 and the
-  // text blocks of chunk c+1 (whose offsets arrived during iteration c-1),
-  // then hashes chunk c from the blocks issued during iteration c-1.
-  uint64_t mo[2][NH];
-  uint32_t mD[2][NH];
+  // Pipeline, unrolled by PD so that no register is renamed while its load
+  // is in flight: iteration c issues the offsets/lengths of chunk c+PD and the
+  // text blocks of chunk c+1 (whose offsets arrived during iteration c-PD+1),
+  // then hashes chunk c from the blocks issued during iteration c-1.  Offset
+  // slots cycle mod PD, text slots mod 2.
+  static_assert(PD % 2 == 0, "text slots alternate");
+  uint64_t mo[PD][NH];
+  uint32_t mD[PD][NH];
   ShortRaw tr[2][NH];
   const uint64_t b0 = qbase;
 #pragma unroll
   for (int h = 0; h < NH; h++) {
     const uint64_t j0 = std::min<uint64_t>(b0 + 64 * h + lane, n - 1);
-    const uint64_t j1 = std::min<uint64_t>(b0 + step + 64 * h + lane, n - 1);
     const uint64_t o0 = offs[j0];
     const uint32_t D0 = lens[j0];
-    mo[1][h] = offs[j1];
-    mD[1][h] = lens[j1];
+#pragma unroll
+    for (int d = 1; d < PD; d++) {
+      const uint64_t jd = std::min<uint64_t>(b0 + d * step + 64 * h + lane, n - 1);
+      mo[d][h] = offs[jd];
+      mD[d][h] = lens[jd];
+    }
     tr[0][h] = short_issue(buf + o0, D0, b0 + 64 * h + lane < n && D0 && is_short(D0));
     tr[0][h].D = D0;  // the length rides with the blocks (0-byte spans load nothing)
   }
   uint32_t it = 0;
   auto body = [&](uint64_t b, auto uc) {
-    constexpr int u = decltype(uc)::value;  // slot parity, a compile-time constant
+    constexpr int u = decltype(uc)::value;  // offset slot, a compile-time constant
+    constexpr int un = (u + 1) % PD, x = u & 1;  // next chunk's offset slot; this chunk's text slot
 #pragma unroll
-    for (int h = 0; h < NH; h++) {  // offsets of chunk b + 2 step into slot u (chunk b's, consumed)
-      const uint64_t jj = std::min<uint64_t>(b + 2 * step + 64 * h + lane, n - 1);
+    for (int h = 0; h < NH; h++) {  // offsets of chunk b + PD step into slot u (chunk b's, consumed)
+      const uint64_t jj = std::min<uint64_t>(b + PD * step + 64 * h + lane, n - 1);
       mo[u][h] = offs[jj];
       mD[u][h] = lens[jj];
     }
 #pragma unroll
     for (int h = 0; h < NH; h++) {  // text of chunk b + step
-      const uint32_t D1 = mD[u ^ 1][h];
-      tr[u ^ 1][h] = short_issue(buf + mo[u ^ 1][h], D1, b + step + 64 * h + lane < n && D1 && is_short(D1));
-      tr[u ^ 1][h].D = D1;
+      const uint32_t D1 = mD[un][h];
+      tr[x ^ 1][h] = short_issue(buf + mo[un][h], D1, ABL < 2 && b + step + 64 * h + lane < n && D1 && is_short(D1));
+      tr[x ^ 1][h].D = D1;
     }
     bool valid[NH], shrt[NH];
     Blk hh[NH];
@@ -645,22 +731,26 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
 #pragma unroll
     for (int h = 0; h < NH; h++) {
       valid[h] = b + 64 * h + lane < n;
-      shrt[h] = is_short(tr[u][h].D);
+      shrt[h] = is_short(tr[x][h].D);
       any |= (valid[h] && shrt[h]) ? 1u : 0u;
     }
     if (any) {
 #pragma unroll
       for (int h = 0; h < NH; h++) {
-        const uint32_t D0 = shrt[h] ? tr[u][h].D : 0u;  // long / invalid lanes hash a zero key, discarded
-        ShortRaw r = tr[u][h];
+        const uint32_t D0 = shrt[h] ? tr[x][h].D : 0u;  // long / invalid lanes hash a zero key, discarded
+        ShortRaw r = tr[x][h];
         r.D = D0;
         const Blk k0 = short_key(r, psel);
+        if constexpr (ABL != 0) {  // ablation: loads and stores only (2: no text loads either)
+          hh[h] = bxor(k0, kfull[D0 + nul].M);
+        } else {
         const MeowConst& c = kfull[D0 + nul];
         const Blk M = c.M;
         Blk S3 = aesdec(bxor(c.F[3], k0), k0, T);
         S3 = aesdec(S3, M, T);
         const Blk S2 = aesdec(bxor(c.TG2, S3), M, T);
         hh[h] = aesdec(bxor(c.TCS0a, S2), M, T);
+        }
       }
 #pragma unroll
       for (int h = 0; h < NH; h++)
@@ -668,31 +758,51 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
     }
 #pragma unroll
     for (int h = 0; h < NH; h++) {
-      const uint64_t lm = __ballot(valid[h] && !shrt[h]);
-      if (lm) {
+      const uint32_t H = tr[x][h].D + nul;
+      const bool med = valid[h] && !shrt[h] && H - 16u < 16u, lng = valid[h] && !shrt[h] && !med;
+      const uint64_t mm = __ballot(med), lm = __ballot(lng);
+      const uint32_t e = CH * it + 64 * h + lane;
+      if (mm) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+        if (med) q[qn + below] = e;
+        qn += (uint32_t)__popcll(mm);
+      }
+      if (lm) {  // the long stack grows down from q[QCAP - 1]
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-        if (valid[h] && !shrt[h]) q[qn + below] = CH * it + 64 * h + lane;
-        qn += (uint32_t)__popcll(lm);
+        if (lng) q[QCAP - 1 - (ql + below)] = e;
+        ql += (uint32_t)__popcll(lm);
       }
     }
-    if (qn >= 64) {
+    if (ABL == 3) qn = ql = 0;  // ablation: no medium / long path
+    if (qn >= 64 || ql >= 64) {
       wave_lds_sync();
-      do {
-        spans_long<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
+      while (qn >= 64) {
+        spans_medium<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CH, nul, fix, kfull, psel, T);
         qn -= 64;
-      } while (qn >= 64);
+      }
+      while (ql >= 64) {  // its newest 64 entries: q[QCAP - ql .. QCAP - ql + 64)
+        spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, 64, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
+        ql -= 64;
+      }
       wave_lds_sync();
     }
     it++;
   };
-  for (uint64_t b = b0; b < n; b += 2 * step) {  // wave-uniform trip count
+  for (uint64_t b = b0; b < n; b += PD * step) {  // wave-uniform trip count
     body(b, std::integral_constant<int, 0>{});
     if (b + step >= n) break;
     body(b + step, std::integral_constant<int, 1>{});
+    if constexpr (PD >= 4) {
+      if (b + 2 * step >= n) break;
+      body(b + 2 * step, std::integral_constant<int, 2 % PD>{});
+      if (b + 3 * step >= n) break;
+      body(b + 3 * step, std::integral_constant<int, 3 % PD>{});
+    }
   }
-  if (qn) {
+  if (qn || ql) {
     wave_lds_sync();
-    spans_long<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
+    if (qn) spans_medium<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CH, nul, fix, kfull, psel, T);
+    if (ql) spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, ql, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
   }
 }
 
@@ -789,7 +899,13 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
-  if (g_tune_spans == 2)
+  if (g_tune_spans == 3)  // ablation: loads and stores, no table rounds (outputs are not hashes)
+    hipLaunchKernelGGL((k_spans<4, 2, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+                       lens, (uint64_t)n, seed1, seed2, out, flags);
+  else if (g_tune_spans == 4)  // ablation: offsets/lengths in, hashes out only (no text, no medium/long path)
+    hipLaunchKernelGGL((k_spans<4, 2, 3>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
+                       lens, (uint64_t)n, seed1, seed2, out, flags);
+  else if (g_tune_spans == 2)
     hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);
   else if (g_tune_spans == 1)

@@ -1941,7 +1941,7 @@ int kvh_set_tuning(int knob, int value) {
     case 15: if (value < 1 || value > 1024) return KVH_EINVAL; prev = g_tune_pipe_mib; g_tune_pipe_mib = value; return prev;
     case 17: if (value < 0 || value > 64) return KVH_EINVAL; prev = g_tune_sort_bits; g_tune_sort_bits = value; return prev;
     case 19: if (value < 0 || value > 1) return KVH_EINVAL; prev = g_tune_tok; g_tune_tok = value; return prev;
-    case 18: if (value < 0 || value > 2) return KVH_EINVAL; prev = g_tune_spans; g_tune_spans = value; return prev;
+    case 18: if (value < 0 || value > 4) return KVH_EINVAL; prev = g_tune_spans; g_tune_spans = value; return prev;
     case 10: prev = g_tune_pf; g_tune_pf = value ? 1 : 0; return prev;
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
     case 9: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_var_mode; g_tune_var_mode = value; return prev;
