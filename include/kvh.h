@@ -368,7 +368,8 @@ int         kvh_device_synchronize(void);
  *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3),
  * 10 = register prefetch of the next chunk in the fixed-length kernel (0/1),
  * 11 = bitsliced share of a 16-byte batch in per mille (0 = T-table only),
- * 14 = variable-length CRC32C kernel (1 length-sorted windows, 0 input order),
+ * 14 = variable-length CRC32C kernel (3 length-sorted windows, 16 waves on
+ *      16-copy tables; 1 the same with 10 waves on 32-copy tables; 0 input order),
  * 15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort key bits (0 auto),
  * 18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
  *      long queues, two / one spans per lane per step; 0 lane per span;

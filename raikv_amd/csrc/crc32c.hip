@@ -61,23 +61,31 @@ constexpr int kBlock = 1024;
 constexpr int kWords = 4 * 8192;  // 4 tables x 256 entries x 32 copies
 
 // LDS slot s holds table T_{3-s}, so slot s is indexed by byte s of x.
-// Byte address of (slot s, value v, lane copy c):
+// R = 32 copies (conflict-free), byte address of (slot s, value v, copy c):
 //   (s >> 1) << 16 | v << 8 | (s & 1) << 7 | c << 2
+// R = 16 copies (64 KiB, lanes 16 apart share a bank: 2-way), all four
+// slots in one 256-byte row per value:
+//   v << 8 | s << 6 | c << 2
+template <int R = 32>
 __device__ __forceinline__ void fill_crc(uint32_t* lds) {
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kWords; i += blockDim.x) {
-    const uint32_t s = (((i >> 14) & 1u) << 1) | ((i >> 5) & 1u);
+  constexpr uint32_t words = R == 32 ? (uint32_t)kWords : (uint32_t)kWords / 2;
+  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+    const uint32_t s = R == 32 ? ((((i >> 14) & 1u) << 1) | ((i >> 5) & 1u)) : ((i >> 4) & 3u);
     const uint32_t v = (i >> 6) & 255u;
     lds[i] = c_crc.t[3 - s][v];
   }
 }
 
-struct CrcLds {
+template <int R = 32>
+struct CrcLdsT {
+  static_assert(R == 32 || R == 16, "table copies");
   const uint32_t* lds;
   uint32_t lw[4];
-  __device__ __forceinline__ explicit CrcLds(const uint32_t* p) : lds(p) {
-    const uint32_t lane = (threadIdx.x & 31u) << 2;
+  __device__ __forceinline__ explicit CrcLdsT(const uint32_t* p) : lds(p) {
+    const uint32_t lane = (threadIdx.x & (uint32_t)(R - 1)) << 2;
 #pragma unroll
-    for (int s = 0; s < 4; s++) lw[s] = ((uint32_t)(s >> 1) << 16) | ((uint32_t)(s & 1) << 7) | lane;
+    for (int s = 0; s < 4; s++)
+      lw[s] = R == 32 ? (((uint32_t)(s >> 1) << 16) | ((uint32_t)(s & 1) << 7) | lane) : (((uint32_t)s << 6) | lane);
   }
   __device__ __forceinline__ uint32_t ld(uint32_t a) const { return *(const uint32_t*)((const char*)lds + a); }
   template <int K> static constexpr uint32_t sel() { return 0x03020000u | ((4u + K) << 8); }
@@ -96,12 +104,15 @@ struct CrcLds {
     uint32_t o = r >> (8 * n);
     for (uint32_t i = 0; i < n; i++) {
       const uint32_t s = 4 - n + i;
-      const uint32_t a = ((s >> 1) << 16) | (((x >> (8 * i)) & 255u) << 8) | ((s & 1) << 7) | ((threadIdx.x & 31u) << 2);
+      const uint32_t v = (x >> (8 * i)) & 255u, c = (threadIdx.x & (uint32_t)(R - 1)) << 2;
+      const uint32_t a = R == 32 ? (((s >> 1) << 16) | (v << 8) | ((s & 1) << 7) | c) : ((v << 8) | (s << 6) | c);
       o ^= ld(a);
     }
     return o;
   }
 };
+
+using CrcLds = CrcLdsT<32>;
 
 // kv_crc_c over one key of len bytes; 16-byte pieces through the
 // dword-aligned loaders (no over-read past the key).
@@ -218,7 +229,8 @@ k_crc_var(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, u
 
 // kv_crc_c over one key with the next 16-byte piece in flight while the
 // current one steps through the tables.
-__device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, uint32_t r, const CrcLds& T) {
+template <class Tab>
+__device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, uint32_t r, const Tab& T) {
   uint64_t o = 0;
   if (len >= 16) {
     Blk cur = load16_full(p);
@@ -253,20 +265,20 @@ __device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, u
 // go through the wave's LDS slice back to input order and leave as one
 // contiguous run.  NW waves per workgroup: the 128 KiB of replicated tables
 // leave room for NW * 3 KiB of window state.
-template <int WIN, int NW, int SH = 0>
+template <int WIN, int NW, int SH = 0, int R = 32>
 __global__ void __launch_bounds__(NW * 64)
 k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
                  const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out
   constexpr int M = WIN / 64;
   static_assert(WIN <= 256 * 4, "hist slice doubles as the CRC staging area");
-  __shared__ uint32_t lds[kWords];
+  __shared__ uint32_t lds[R == 32 ? kWords : kWords / 2];
   __shared__ uint32_t hist_s[NW][WIN > 256 ? WIN : 256];
   __shared__ uint32_t roff_s[NW][WIN];
   __shared__ uint16_t rlen_s[NW][WIN];
   __shared__ uint16_t ridx_s[NW][WIN];
-  fill_crc(lds);
+  fill_crc<R>(lds);
   __syncthreads();
-  const CrcLds T(lds);
+  const CrcLdsT<R> T(lds);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* hist = hist_s[wv];
   const uint64_t nwin = (n + WIN - 1) / WIN;
@@ -304,7 +316,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
 }
 
 }  // namespace
-namespace kvh { namespace rt { int g_tune_crc_var = 1; } }
+namespace kvh { namespace rt { int g_tune_crc_var = 3; } }
 namespace {
 
 uint32_t grid_crc(uint64_t n, int cus) {
@@ -409,6 +421,9 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
   if (rc) return rc;
   if (g_tune_crc_var == 1)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 10>), dim3(cus), dim3(640), 0, (hipStream_t)stream,
+                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  else if (g_tune_crc_var == 3)  // tables with 16 copies (64 KiB): 16 waves per CU
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (g_tune_crc_var == 2)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 8>), dim3(cus), dim3(512), 0, (hipStream_t)stream,

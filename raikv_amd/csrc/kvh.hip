@@ -1936,7 +1936,7 @@ int kvh_set_tuning(int knob, int value) {
     case 11: if (value < 0 || value > 1000) return KVH_EINVAL; prev = g_tune_bs; g_tune_bs = value; return prev;
     case 12: if (value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_bsw; g_tune_bsw = value; return prev;
     case 13: if (value != 0 && value != 2 && value != 3) return KVH_EINVAL; prev = g_tune_prio; g_tune_prio = value; return prev;
-    case 14: if (value < 0 || value > 2) return KVH_EINVAL; prev = g_tune_crc_var; g_tune_crc_var = value; return prev;
+    case 14: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_crc_var; g_tune_crc_var = value; return prev;
     case 16: if (value < 2 || value > 16) return KVH_EINVAL; prev = g_tune_pipe_slots; g_tune_pipe_slots = value; return prev;
     case 15: if (value < 1 || value > 1024) return KVH_EINVAL; prev = g_tune_pipe_mib; g_tune_pipe_mib = value; return prev;
     case 17: if (value < 0 || value > 64) return KVH_EINVAL; prev = g_tune_sort_bits; g_tune_sort_bits = value; return prev;

@@ -184,7 +184,8 @@ int hip_err(hipError_t e);
 int device_cus(int* cus);
 // hipGetLastError after a launch -> 0 or the recorded error
 int launch_done();
-// variable-length CRC32C kernel: 1 = length-sorted windows (default), 0 = lane per key in input order
+// variable-length CRC32C kernel: 3 = length-sorted windows on 16-copy tables (default), 1 = on 32-copy
+// tables, 0 = lane per key in input order
 extern int g_tune_crc_var;
 // table-order sort: h1 bits sorted below the slot bits (0 = by batch size; 64 = the full key)
 extern int g_tune_sort_bits;
