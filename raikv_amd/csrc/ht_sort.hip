@@ -12,12 +12,14 @@
 // the reference's order, so every adjacent-equal pair the reference could
 // find is adjacent here, and all duplicates of a key are contiguous.
 //   1. k_sort_keys   key64 = slot << (64 - sbits) | (h1 << 1) >> sbits,
-//                    kept: that prefix; idx = i (u32)
-//   2. radix sort of (key64, idx) pairs over a prefix of key64 only: the
-//      slot bits and max(1, log2(n) + 5 - sbits) bits of h1 (100M keys, 64 GiB
-//      table: 4 onesweep passes instead of 8): rocPRIM's
-//      rocprim::radix_sort_pairs (the library primitive; ROCm's own), stable
-//   3. k_sort_pack   (with items) (h1, h2, item) -> 32-byte records
+//                    kept: that prefix, as u32 when it fits 31 bits; idx = i
+//                    (u32); with items, (h1, h2, item) -> 32-byte records in
+//                    the same pass over the hashes
+//   2. radix sort of (key, idx) pairs over a prefix of key64 only: the
+//      slot bits and max(1, log2(n) + 5 - sbits) bits of h1, at most 31 with
+//      u32 keys (100M keys, 64 GiB table: 31 bits in 4 onesweep passes of
+//      u32 keys instead of 8 of u64): rocPRIM's rocprim::radix_sort_pairs
+//      (the library primitive; ROCm's own), stable
 //   4. k_sort_place  hashes_out / items_out[j] = record idx[j] (one random
 //                    read per element)
 //   5. k_sort_fixup  runs of equal sorted prefix (equal slot and equal top
@@ -60,29 +62,25 @@ __device__ __forceinline__ bool rec_less(uint64_t a1, uint64_t a2, uint64_t b1, 
 // shifted down to bit 0: the radix sort then runs over bits [0, 64 - lo).
 // (Not [lo, 64) in place: rocPRIM's merge-sort path, taken for n <= 1M,
 // builds its mask as (1 << (begin_bit + bits)) - 1, undefined at 64.)
+template <class K, bool PACK>
 __global__ void __launch_bounds__(kSB)
-k_sort_keys(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sbits, uint32_t lo,
-            uint64_t* __restrict__ key, uint32_t* __restrict__ idx) {
+k_sort_keys(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, HtGeom g,
+            uint32_t sbits, uint32_t lo, K* __restrict__ key, uint32_t* __restrict__ idx, Rec* __restrict__ rec) {
   const uint64_t i = (uint64_t)blockIdx.x * kSB + threadIdx.x;
   if (i >= n) return;
   const uint64_t h1 = h[2 * i];
   const uint64_t slot = ht_mod(g, h1);
   const uint64_t k64 = sbits >= 64 ? slot : (slot << (64 - sbits)) | ((h1 << 1) >> sbits);
-  key[i] = k64 >> lo;
+  key[i] = (K)(k64 >> lo);
   idx[i] = (uint32_t)i;
-}
-
-// input order: (h1, h2, item) -> 32-byte records (coalesced both ways)
-__global__ void __launch_bounds__(kSB)
-k_sort_pack(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, Rec* __restrict__ rec) {
-  const uint64_t i = (uint64_t)blockIdx.x * kSB + threadIdx.x;
-  if (i >= n) return;
-  Rec r;
-  r.h1 = h[2 * i];
-  r.h2 = h[2 * i + 1];
-  r.item = items[i];
-  r.pad = 0;
-  rec[i] = r;
+  if constexpr (PACK) {  // (h1, h2, item) -> 32-byte record, in the same pass over the hashes
+    Rec r;
+    r.h1 = h1;
+    r.h2 = h[2 * i + 1];
+    r.item = items[i];
+    r.pad = 0;
+    rec[i] = r;
+  }
 }
 
 // sorted position j <- record idx[j]: one random read (a packed record, or
@@ -110,8 +108,9 @@ k_sort_place(const uint64_t* __restrict__ h, const Rec* __restrict__ rec, const 
 // run -- and, with dedup, every element equal (h1, h2) to its successor gets
 // h1 = 0 (ctest.c:96-104).  Equal pairs share a prefix, so runs are the only
 // place duplicates occur.  Grid-stride; one atomic per workgroup.
+template <class K>
 __global__ void __launch_bounds__(kSB)
-k_sort_fixup(const uint64_t* __restrict__ key, uint64_t n, uint64_t* __restrict__ h, uint64_t* __restrict__ items,
+k_sort_fixup(const K* __restrict__ key, uint64_t n, uint64_t* __restrict__ h, uint64_t* __restrict__ items,
              uint32_t dedup, unsigned long long* __restrict__ dups) {
   __shared__ uint32_t wsum[kSB / 64];
   uint32_t d = 0;
@@ -159,11 +158,15 @@ struct SortLayout {
 };
 
 int sort_layout(size_t n, SortLayout* L) {
-  size_t tmp = 0;
+  size_t tmp = 0, tmp32 = 0;  // either key width (sort_impl picks one)
   hipError_t e = rocprim::radix_sort_pairs((void*)nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                                            (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u, 64u,
                                            (hipStream_t)0);
   if (e != hipSuccess) return hip_err(e);
+  e = rocprim::radix_sort_pairs((void*)nullptr, tmp32, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                (const uint32_t*)nullptr, (uint32_t*)nullptr, n, 0u, 31u, (hipStream_t)0);
+  if (e != hipSuccess) return hip_err(e);
+  tmp = std::max(tmp, tmp32);
   size_t o = 0;
   L->key_in = o; o += al256(8 * n);
   L->key_out = o; o += al256(8 * n);
@@ -221,27 +224,51 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   while (lg < 63 && (1ull << lg) < (uint64_t)n) lg++;
   uint32_t nb = g_tune_sort_bits ? sb + (uint32_t)g_tune_sort_bits : std::max(sb + 1, lg + 5);
   if (nb > 64) nb = 64;
+  // u32 keys halve the key bytes every radix pass moves (16 instead of 24 per
+  // element with the index): used when the prefix fits 31 bits -- all slot
+  // bits and as many h1 bits as fit (rocPRIM's merge path, taken for small n,
+  // builds its mask as (T(1) << end_bit) - 1: undefined at the type's width)
+  const bool k32 = !g_tune_sort_bits && sb <= 31;
+  if (k32) nb = std::min(nb, 31u);
   const uint32_t lo = 64u - nb;
-  hipLaunchKernelGGL(k_sort_keys, dim3(grid), dim3(kSB), 0, st, hashes, (uint64_t)n, g, sb, lo, kin, iin);
-  rc = launch_done();
-  if (rc) return rc;
-  if (items) {  // carried items: packed with their hashes for a single random read per record
-    hipLaunchKernelGGL(k_sort_pack, dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, rec);
-    rc = launch_done();
-    if (rc) return rc;
-  }
-  size_t tb = L.tmp_bytes;
-  hipError_t e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, kin, kout, iin, iout, n, 0u, 64u - lo, st);
-  if (e != hipSuccess) return hip_err(e);
-  hipLaunchKernelGGL(k_sort_place, dim3(grid), dim3(kSB), 0, st, hashes, items ? rec : (const Rec*)nullptr, iout,
-                     (uint64_t)n, h_out, items_out);
-  rc = launch_done();
-  if (rc) return rc;
   int cus = 0;
   if ((rc = device_cus(&cus))) return rc;
   const uint32_t fgrid = (uint32_t)std::min<uint64_t>(grid, (uint64_t)cus * 8);
-  hipLaunchKernelGGL(k_sort_fixup, dim3(fgrid), dim3(kSB), 0, st, kout, (uint64_t)n, h_out, items_out,
-                     dedup ? 1u : 0u, (unsigned long long*)dup_count);
+  size_t tb = L.tmp_bytes;
+  hipError_t e;
+  if (k32) {
+    uint32_t* k32in = (uint32_t*)kin;
+    uint32_t* k32out = (uint32_t*)kout;
+    if (items)
+      hipLaunchKernelGGL((k_sort_keys<uint32_t, true>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
+                         sb, lo, k32in, iin, rec);
+    else
+      hipLaunchKernelGGL((k_sort_keys<uint32_t, false>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
+                         sb, lo, k32in, iin, rec);
+    if ((rc = launch_done())) return rc;
+    e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, k32in, k32out, iin, iout, n, 0u, nb, st);
+    if (e != hipSuccess) return hip_err(e);
+    hipLaunchKernelGGL(k_sort_place, dim3(grid), dim3(kSB), 0, st, hashes, items ? rec : (const Rec*)nullptr, iout,
+                       (uint64_t)n, h_out, items_out);
+    if ((rc = launch_done())) return rc;
+    hipLaunchKernelGGL((k_sort_fixup<uint32_t>), dim3(fgrid), dim3(kSB), 0, st, (const uint32_t*)k32out, (uint64_t)n,
+                       h_out, items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count);
+    return launch_done();
+  }
+  if (items)
+    hipLaunchKernelGGL((k_sort_keys<uint64_t, true>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
+                       sb, lo, kin, iin, rec);
+  else
+    hipLaunchKernelGGL((k_sort_keys<uint64_t, false>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
+                       sb, lo, kin, iin, rec);
+  if ((rc = launch_done())) return rc;
+  e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, kin, kout, iin, iout, n, 0u, 64u - lo, st);
+  if (e != hipSuccess) return hip_err(e);
+  hipLaunchKernelGGL(k_sort_place, dim3(grid), dim3(kSB), 0, st, hashes, items ? rec : (const Rec*)nullptr, iout,
+                     (uint64_t)n, h_out, items_out);
+  if ((rc = launch_done())) return rc;
+  hipLaunchKernelGGL((k_sort_fixup<uint64_t>), dim3(fgrid), dim3(kSB), 0, st, (const uint64_t*)kout, (uint64_t)n,
+                     h_out, items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count);
   return launch_done();
 }
 

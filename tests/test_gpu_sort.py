@@ -34,8 +34,19 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
 
 
+@pytest.mark.parametrize("sort_bits", [0, 33], ids=["auto_u32", "u64_33"])
 @pytest.mark.parametrize("f", FIX, ids=[f["name"] for f in FIX])
-def test_sort_golden(kvh, f):
+def test_sort_golden(kvh, f, sort_bits):
+    """Golden sets, both key widths: knob 17 = 0 sorts u32 keys when the
+    prefix fits 31 bits; 33 forces u64 keys over slot + 33 h1 bits."""
+    prev = kvh.lib.kvh_set_tuning(17, sort_bits)
+    try:
+        _sort_golden(kvh, f)
+    finally:
+        kvh.lib.kvh_set_tuning(17, prev)
+
+
+def _sort_golden(kvh, f):
     g = kvh.HtGeom.from_map(f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
     og = orc_geom(ORC, f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
     h = f["hashes"]
