@@ -703,8 +703,8 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
 #pragma unroll
     for (int d = 1; d < PD; d++) {
       const uint64_t jd = std::min<uint64_t>(b0 + d * step + 64 * h + lane, n - 1);
-      mo[d][h] = offs[jd];
-      mD[d][h] = lens[jd];
+      mo[d][h] = __builtin_nontemporal_load(offs + jd);  // read once: streaming
+      mD[d][h] = __builtin_nontemporal_load(lens + jd);
     }
     tr[0][h] = short_issue(buf + o0, D0, b0 + 64 * h + lane < n && D0 && is_short(D0));
     tr[0][h].D = D0;  // the length rides with the blocks (0-byte spans load nothing)
@@ -716,8 +716,8 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
 #pragma unroll
     for (int h = 0; h < NH; h++) {  // offsets of chunk b + PD step into slot u (chunk b's, consumed)
       const uint64_t jj = std::min<uint64_t>(b + PD * step + 64 * h + lane, n - 1);
-      mo[u][h] = offs[jj];
-      mD[u][h] = lens[jj];
+      mo[u][h] = __builtin_nontemporal_load(offs + jj);
+      mD[u][h] = __builtin_nontemporal_load(lens + jj);
     }
 #pragma unroll
     for (int h = 0; h < NH; h++) {  // text of chunk b + step
@@ -754,7 +754,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
       }
 #pragma unroll
       for (int h = 0; h < NH; h++)
-        if (valid[h] && shrt[h]) store_h(out, b + 64 * h + lane, hh[h], fix);
+        if (valid[h] && shrt[h]) store_h<true>(out, b + 64 * h + lane, hh[h], fix);  // streaming
     }
 #pragma unroll
     for (int h = 0; h < NH; h++) {
