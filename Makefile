@@ -12,7 +12,7 @@ HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/
             raikv_amd/csrc/ht_pos.hpp raikv_amd/csrc/bs_prelude.hpp raikv_amd/csrc/bs_aes.hpp \
             raikv_amd/csrc/bs_meow.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
-CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host
+CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/paths_gpu
 
 all: $(LIB) oracle cpptests
 
@@ -29,6 +29,12 @@ oracle:
 cpptests: $(CPP_TESTS)
 
 tests/cpp/hash_test_gpu: tests/cpp/hash_test_gpu.cpp $(LIB) include/raikv_amd/key_hash.hpp include/kvh.h
+	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
+
+# the C++ API of the f1-f4 paths (key_hash.hpp) on the GPU
+tests/cpp/paths_gpu: tests/cpp/paths_gpu.cpp $(LIB) include/raikv_amd/key_hash.hpp include/kvh.h
 	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
 	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib

@@ -13,6 +13,7 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
+#include <hip/hip_runtime_api.h>  // device scratch for the f2 / f3 helpers
 #include "../kvh.h"
 
 namespace kvh {
@@ -122,6 +123,77 @@ inline void hash_multiseed(const void* keys, uint32_t key_len, size_t n, const s
   check(kvh_meow128_multiseed(keys, key_len, n, s.data(), (uint32_t)seeds.size(), out,
                               fixup ? KVH_FIXUP : 0u, stream),
         "kvh::hash_multiseed");
+}
+
+// ---- the calls either side of the hash, same shape
+
+// Table geometry from the map's header fields (shm_ht.h:143-157, ht_init.cpp:117-156).
+inline kvh_ht_geom_t ht_geom(uint64_t map_size, uint32_t hash_entry_size, float hash_value_ratio,
+                             uint16_t cuckoo_buckets, uint8_t cuckoo_arity) {
+  kvh_ht_geom_t g;
+  check(kvh_ht_geom_init(map_size, hash_entry_size, hash_value_ratio, cuckoo_buckets, cuckoo_arity, &g),
+        "kvh::ht_geom");
+  return g;
+}
+// f1: hash pairs -> ht_mod(h1) and the cuckoo alternates, positions_per_key(g) per key.
+inline uint32_t positions_per_key(const kvh_ht_geom_t& g) { return kvh_positions_per_key(&g); }
+inline void ht_positions(const uint64_t* hashes, size_t n, const kvh_ht_geom_t& g, uint64_t* pos,
+                         void* stream = nullptr) {
+  check(kvh_ht_positions(hashes, n, &g, pos, 0u, stream), "kvh::ht_positions");
+}
+// f1 fused: fixed-length keys -> fixed-up hash pairs + positions in one pass.
+inline void hash_fixed_positions(const void* keys, uint32_t key_len, size_t n, const HashSeed& hs,
+                                 const kvh_ht_geom_t& g, uint64_t* hashes, uint64_t* pos, void* stream = nullptr) {
+  check(kvh_meow128_fixed_positions(keys, key_len, n, hs.hash1, hs.hash2, &g, hashes, pos, 0u, stream),
+        "kvh::hash_fixed_positions");
+}
+
+// Device scratch owned by the caller-side helpers below (grown on demand,
+// reused across calls; not thread-safe, one per stream).
+struct Scratch {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void* need(size_t b) {
+    if (b > bytes) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      bytes = 0;
+      if (hipMalloc(&p, b) != hipSuccess) throw Error("kvh::Scratch", KVH_ENOMEM);
+      bytes = b;
+    }
+    return p;
+  }
+  ~Scratch() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// f2: kv_ht_radix_sort + ctest's duplicate loop (ctest.c:89-104) on the device:
+// hash pairs (+ items, or nullptr to carry the input index) -> table order.
+inline void ht_sort(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh_ht_geom_t& g,
+                    uint64_t* hashes_out, uint64_t* items_out, uint64_t* dup_count, bool dedup, Scratch& sc,
+                    void* stream = nullptr) {
+  const size_t b = kvh_ht_sort_scratch_bytes(n);
+  check(kvh_ht_sort(hashes, items, n, &g, hashes_out, items_out, dup_count, dedup ? KVH_DEDUP : 0u, sc.need(b), b,
+                    stream),
+        "kvh::ht_sort");
+}
+
+// f3: ctest's ingest loop (tokenize + kv_hash_key_frag of "token\0") in one
+// asynchronous call; *count (device) receives the kept token count.
+inline void ingest_text(const void* text, size_t nbytes, const HashSeed& hs, uint64_t* tok_offs, uint32_t* tok_lens,
+                        uint64_t* hashes, size_t cap, uint64_t* count, Scratch& sc, uint32_t max_token = 256,
+                        void* stream = nullptr) {
+  const size_t b = kvh_tokenize_scratch_bytes(nbytes);
+  check(kvh_tokenize_hash(text, nbytes, max_token, hs.hash1, hs.hash2, KVH_FIXUP | KVH_NULTERM, tok_offs, tok_lens,
+                          hashes, cap, count, sc.need(b), b, stream),
+        "kvh::ingest_text");
+}
+
+// f4: kv_crc_c of n packed variable-length keys (seeds nullptr: one seed for all).
+inline void crc_var(const void* keys, const uint64_t* offsets, size_t n, const uint32_t* seeds, uint32_t seed,
+                    uint32_t* out, void* stream = nullptr) {
+  check(kvh_crc_c_var(keys, offsets, n, seeds, seed, out, stream), "kvh::crc_var");
 }
 
 }  // namespace kvh

@@ -321,3 +321,13 @@ def test_var_kernel_variants_vs_oracle(kvh, variant):
         finally:
             kvh.lib.kvh_set_tuning(7, prev)
         np.testing.assert_array_equal(got, want, err_msg=f"n={n}")
+
+
+def test_cpp_paths_program(kvh):
+    """The C++ API of the f1-f4 paths (include/raikv_amd/key_hash.hpp) on the GPU."""
+    exe = os.path.join(ROOT, "tests", "cpp", "paths_gpu")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "cpptests"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
