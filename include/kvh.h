@@ -99,6 +99,11 @@ int kvh_meow128_fixed_host(const void *keys, uint32_t key_len, size_t n,
  * GPU side; 0 or a negative error.  Free with kvh_host_free. */
 int kvh_host_alloc(void **p, size_t bytes);
 int kvh_host_free(void *p);
+/* Device memory on the current GPU (scratch for kvh_ht_sort / kvh_tokenize
+ * from hosts that do not link the HIP runtime themselves); 0 or a negative
+ * error.  Free with kvh_device_free. */
+int kvh_device_alloc(void **p, size_t bytes);
+int kvh_device_free(void *p);
 
 /* ---------------------------------------------------------------------
  * Drop-ins for include/raikv/key_hash.h (host pointers, synchronous).  They

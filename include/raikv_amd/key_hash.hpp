@@ -13,7 +13,6 @@
 #include <stdexcept>
 #include <string>
 #include <vector>
-#include <hip/hip_runtime_api.h>  // device scratch for the f2 / f3 helpers
 #include "../kvh.h"
 
 namespace kvh {
@@ -155,17 +154,18 @@ struct Scratch {
   size_t bytes = 0;
   void* need(size_t b) {
     if (b > bytes) {
-      if (p) (void)hipFree(p);
+      check(kvh_device_free(p), "kvh::Scratch");
       p = nullptr;
       bytes = 0;
-      if (hipMalloc(&p, b) != hipSuccess) throw Error("kvh::Scratch", KVH_ENOMEM);
+      check(kvh_device_alloc(&p, b), "kvh::Scratch");
       bytes = b;
     }
     return p;
   }
-  ~Scratch() {
-    if (p) (void)hipFree(p);
-  }
+  Scratch() = default;
+  Scratch(const Scratch&) = delete;
+  Scratch& operator=(const Scratch&) = delete;
+  ~Scratch() { (void)kvh_device_free(p); }
 };
 
 // f2: kv_ht_radix_sort + ctest's duplicate loop (ctest.c:89-104) on the device:

@@ -80,6 +80,8 @@ def _load():
         "kvh_meow128_fixed_host": (I, [P, U32, SZ, U64, U64, P, U32]),
         "kvh_host_alloc": (I, [C.POINTER(P), SZ]),
         "kvh_host_free": (I, [P]),
+        "kvh_device_alloc": (I, [C.POINTER(P), SZ]),
+        "kvh_device_free": (I, [P]),
         "kvh_hash_meow128": (I, [P, SZ, C.POINTER(U64), C.POINTER(U64)]),
         "kvh_hash_meow64": (U64, [P, SZ, U64]),
         "kvh_hash_meow128_2_same_length": (I, [P, P, SZ, P]),

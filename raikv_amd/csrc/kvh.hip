@@ -1725,6 +1725,19 @@ int kvh_host_free(void* p) {
   return e == hipSuccess ? set_err(0) : hip_err(e);
 }
 
+int kvh_device_alloc(void** p, size_t bytes) {
+  if (!p) return set_err(KVH_EINVAL);
+  *p = nullptr;
+  const hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+  return e == hipSuccess ? set_err(0) : hip_err(e);
+}
+
+int kvh_device_free(void* p) {
+  if (!p) return set_err(0);
+  const hipError_t e = hipFree(p);
+  return e == hipSuccess ? set_err(0) : hip_err(e);
+}
+
 int kvh_hash_meow128(const void* p, size_t sz, uint64_t* h1, uint64_t* h2) {
   if (!h1 || !h2) return set_err(KVH_EINVAL);
   uint64_t s[2] = {*h1, *h2}, o[2];
