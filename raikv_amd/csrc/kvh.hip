@@ -169,7 +169,9 @@ k_fixed_lanes(const uint8_t* __restrict__ keys, uint64_t n, uint64_t* __restrict
 }
 
 // ---------------------------------------------------------------------
-// LDS-DMA streaming (the C1/C4 hot path).  One 1024-thread workgroup per CU:
+// LDS-DMA streaming (opt-in, knob 6; the register path k_fixed is C1/C4's
+// default: 153.9 vs 130-139 G hash/s at ring depths 2-6, tools/tune.py).
+// One 1024-thread workgroup per CU:
 // NT replicated tables plus, per wave, a ring of R chunk slots in the SAME
 // __shared__ array (one LDS object: no compiler-inserted vmcnt(0) before the
 // ring reads).  A chunk is 64 consecutive keys (64*L contiguous bytes); the
