@@ -317,6 +317,25 @@ int kvh_meow128_spans(const void *buf, const uint64_t *offs,
                       uint64_t seed2, uint64_t *out, uint32_t flags,
                       void *stream);
 
+/* Record offsets of a packed kv_key_frag_t stream: buf
+ * holds records {u16 keylen, keylen bytes, pad to 2} back to back from byte
+ * 0 (kv_make_key_frag, key_ctx.cpp:1737-1745, ctest.c:223); writes the byte
+ * offsets of the first min(count, cap) records and the record count to
+ * *count (device), found on the device by list ranking.  A record running
+ * past nbytes ends the stream.  nbytes < 8 GiB.  scratch: device buffer of
+ * kvh_frag_offsets_scratch_bytes(nbytes). */
+size_t kvh_frag_offsets_scratch_bytes(size_t nbytes);
+int kvh_frag_offsets(const void *buf, size_t nbytes, uint64_t *rec_offs,
+                     size_t cap, uint64_t *count, void *scratch,
+                     size_t scratch_bytes, void *stream);
+/* kvh_frag_offsets, then kvh_meow128_frags over those records reading the
+ * count on the device (one asynchronous call): the hashes of a packed frag
+ * stream, out cap x 2 u64. */
+int kvh_frags_hash(const void *buf, size_t nbytes, uint64_t seed1,
+                   uint64_t seed2, uint32_t flags, uint64_t *rec_offs,
+                   uint64_t *out, size_t cap, uint64_t *count, void *scratch,
+                   size_t scratch_bytes, void *stream);
+
 /* Meow128 of n packed kv_key_frag_t records {u16 keylen, keylen bytes,
  * pad to 2} (hash_entry.h:28-36, kv_make_key_frag key_ctx.cpp:1737-1745):
  * rec_offs[i] is the byte offset of record i in buf (ctest.c's xh[].frag

@@ -14,6 +14,8 @@ from .binding import (  # noqa: F401
     crc_c_fixed,
     tokenize,
     tokenize_hash,
+    frag_offsets,
+    frags_hash,
     HtSorter,
     KVH_DEDUP,
     meow128_spans,
@@ -44,5 +46,5 @@ __all__ = [
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "host_empty", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
     "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
-    "tokenize", "tokenize_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP",
+    "tokenize", "tokenize_hash", "frag_offsets", "frags_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP",
 ]

@@ -117,6 +117,9 @@ def _load():
         "kvh_tokenize_hash": (I, [P, SZ, U32, U64, U64, U32, P, P, P, SZ, P, P, SZ, P]),
         "kvh_meow128_spans": (I, [P, P, P, SZ, U64, U64, P, U32, P]),
         "kvh_meow128_frags": (I, [P, P, SZ, U64, U64, P, U32, P]),
+        "kvh_frag_offsets_scratch_bytes": (SZ, [SZ]),
+        "kvh_frag_offsets": (I, [P, SZ, P, SZ, P, P, SZ, P]),
+        "kvh_frags_hash": (I, [P, SZ, U64, U64, U32, P, P, SZ, P, P, SZ, P]),
         "kvh_ht_sort_scratch_bytes": (SZ, [SZ]),
         "kvh_ht_sort": (I, [P, P, SZ, P, P, P, P, U32, P, SZ, P]),
         "kvh_ht_radix_sort": (I, [P, U32, P]),
@@ -285,6 +288,39 @@ def meow128_spans(buf, offs, lens, seed: Tuple[int, int], out=None, fixup: bool 
                                 (KVH_FIXUP if fixup else 0) | (KVH_NULTERM if nulterm else 0), _stream_ptr(stream)),
           "kvh_meow128_spans")
     return out
+
+
+def frag_offsets(buf, cap: Optional[int] = None, stream=None):
+    """Record offsets of a packed kv_key_frag_t stream, found on the device
+    (list ranking) -> int64 [count]."""
+    n = buf.numel()
+    cnt = torch.zeros((1,), dtype=torch.int64, device=buf.device)
+    scratch = torch.empty((max(1, lib.kvh_frag_offsets_scratch_bytes(n) // 8 + 1),), dtype=torch.int64,
+                          device=buf.device)
+    if cap is None:
+        cap = n // 2 + 1
+    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=buf.device)
+    check(lib.kvh_frag_offsets(_dev_ptr(buf) if n else None, n, _dev_ptr(offs), cap, _dev_ptr(cnt), _dev_ptr(scratch),
+                               scratch.numel() * 8, _stream_ptr(stream)), "kvh_frag_offsets")
+    return offs[:min(int(cnt.item()), cap)]
+
+
+def frags_hash(buf, seed: Tuple[int, int], cap: Optional[int] = None, fixup: bool = True, stream=None):
+    """Hashes of every record of a packed kv_key_frag_t stream in one call
+    (offsets found on the device) -> (offsets int64 [k], hashes int64 [k, 2])."""
+    n = buf.numel()
+    cnt = torch.zeros((1,), dtype=torch.int64, device=buf.device)
+    scratch = torch.empty((max(1, lib.kvh_frag_offsets_scratch_bytes(n) // 8 + 1),), dtype=torch.int64,
+                          device=buf.device)
+    if cap is None:
+        cap = n // 2 + 1
+    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=buf.device)
+    out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=buf.device)
+    check(lib.kvh_frags_hash(_dev_ptr(buf) if n else None, n, U64(seed[0] & (2**64 - 1)), U64(seed[1] & (2**64 - 1)),
+                             KVH_FIXUP if fixup else 0, _dev_ptr(offs), _dev_ptr(out), cap, _dev_ptr(cnt),
+                             _dev_ptr(scratch), scratch.numel() * 8, _stream_ptr(stream)), "kvh_frags_hash")
+    k = min(int(cnt.item()), cap)
+    return offs[:k], out[:k]
 
 
 def meow128_frags(buf, rec_offs, seed: Tuple[int, int], out=None, fixup: bool = True, stream=None):

@@ -441,7 +441,8 @@ enum { SRC_SPANS = 0, SRC_FRAGS = 1 };
 template <int SRC, int NT>
 __global__ void __launch_bounds__(1024)
 k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
-         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags) {
+         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
+         const uint64_t* __restrict__ dcount = nullptr) {  // dcount: n = min(n, *dcount), read on the device
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
   __shared__ MeowConst kfull[kLT];
   __shared__ Blk kf[kNF * 4];
@@ -458,6 +459,10 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
     }
   }
   __syncthreads();
+  if (dcount) {  // no barrier follows
+    const uint64_t dn = *dcount;
+    n = dn < n ? dn : n;
+  }
   const bool fix = (flags & KVH_FIXUP) != 0;
   const uint32_t nul = (flags & KVH_NULTERM) ? 1u : 0u;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -807,6 +812,82 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
 }
 
 
+// ---------------------------------------------------------------------
+// Packed kv_key_frag_t stream -> record offsets: records
+// {u16 keylen, keylen bytes, pad to 2} back to back (kv_make_key_frag,
+// key_ctx.cpp:1737-1745, as ctest packs them), so record starts are 2-byte
+// positions and each one names the next: a linked list.  List ranking on the
+// device: every position i gets next(i) = i + 1 + (keylen + 1) / 2 (in 2-byte
+// units); ceil(log2 M) + 1 pointer-jumping launches mark every position
+// reachable from 0 (after step k every record fewer than 2^(k+1) hops from
+// the start is marked, which needs the previous step's marks complete: one
+// launch per step); a count / scan / emit compacts the marks into offsets.
+// A record running past the buffer ends the chain (jump sentinel M + 1).
+constexpr uint32_t kFragChunk = 1024;
+
+__global__ void __launch_bounds__(256)
+k_frag_next(const uint8_t* __restrict__ b, uint64_t nbytes, uint32_t M, uint32_t* __restrict__ jump,
+            uint8_t* __restrict__ mark) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += stride) {
+    const uint64_t o = 2 * i;
+    const uint32_t len = (uint32_t)b[o] | ((uint32_t)b[o + 1] << 8);  // o + 2 <= nbytes: i < M = nbytes / 2
+    const uint64_t end = o + 2 + len;                                // the record's last byte + 1
+    const bool valid = end <= nbytes;
+    const uint64_t nx = (end + 1) >> 1;                              // past the pad byte, in positions
+    jump[i] = valid ? (uint32_t)(nx < M ? nx : M) : M + 1;
+    mark[i] = (i == 0 && valid) ? 1 : 0;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+k_frag_jump(const uint32_t* __restrict__ jin, uint32_t* __restrict__ jout, uint8_t* __restrict__ mark, uint32_t M) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M; i += stride) {
+    const uint32_t j = jin[i];
+    if (j < M) {
+      const uint32_t jj = jin[j];
+      if (jj != M + 1 && mark[i]) mark[j] = 1;  // j is a valid record reachable from 0
+      jout[i] = jj == M + 1 ? M : jj;
+    } else {
+      jout[i] = j;
+    }
+  }
+}
+
+// marks per chunk of kFragChunk positions
+__global__ void __launch_bounds__(kFragChunk)
+k_frag_count(const uint8_t* __restrict__ mark, uint32_t M, uint64_t* __restrict__ cnt) {
+  __shared__ uint32_t ws[kFragChunk / 64];
+  const uint64_t i = (uint64_t)blockIdx.x * kFragChunk + threadIdx.x;
+  const uint64_t bm = __ballot(i < M && mark[i]);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = (uint32_t)__popcll(bm);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kFragChunk / 64; w++) t += ws[w];
+    cnt[blockIdx.x] = t;
+  }
+}
+
+// marked positions -> byte offsets, in order, at the chunk's scanned base
+__global__ void __launch_bounds__(kFragChunk)
+k_frag_emit(const uint8_t* __restrict__ mark, uint32_t M, const uint64_t* __restrict__ pre,
+            uint64_t* __restrict__ rec_offs, uint64_t cap) {
+  __shared__ uint32_t ws[kFragChunk / 64];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t i = (uint64_t)blockIdx.x * kFragChunk + threadIdx.x;
+  const bool m = i < M && mark[i];
+  const uint64_t bm = __ballot(m);
+  if (lane == 0) ws[wv] = (uint32_t)__popcll(bm);
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < wv; w++) before += ws[w];
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+  const uint64_t k = pre[blockIdx.x] + before + below;
+  if (m && k < cap) rec_offs[k] = 2 * i;
+}
+
 }  // namespace
 namespace kvh { namespace rt { int g_tune_spans = 2; int g_tune_tok = 1; } }
 namespace {
@@ -889,6 +970,70 @@ int kvh_tokenize_hash(const void* text, size_t nbytes, uint32_t max_token, uint6
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((cap + 1023) / 1024, (uint64_t)cus));
   hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)text,
                      tok_offs, tok_lens, (uint64_t)cap, seed1, seed2, out, flags, (const uint64_t*)count);
+  return launch_done();
+}
+
+size_t kvh_frag_offsets_scratch_bytes(size_t nbytes) {
+  const uint64_t M = nbytes / 2, nc = (M + kFragChunk - 1) / kFragChunk + 1;
+  return 2 * 4 * (M + 64) + (M + 64) + 2 * 8 * nc + 256;
+}
+
+int kvh_frag_offsets(const void* buf, size_t nbytes, uint64_t* rec_offs, size_t cap, uint64_t* count, void* scratch,
+                     size_t scratch_bytes, void* stream) {
+  if (!count) return set_err(KVH_EINVAL);
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t M = nbytes / 2;
+  if (M == 0) {
+    hipError_t e = hipMemsetAsync(count, 0, 8, st);
+    return e == hipSuccess ? set_err(0) : hip_err(e);
+  }
+  if (!buf || M >= 0xfffffff0ull || !scratch || scratch_bytes < kvh_frag_offsets_scratch_bytes(nbytes) ||
+      (cap && !rec_offs))
+    return set_err(KVH_EINVAL);
+  int cus = 0, rc = device_cus(&cus);
+  if (rc) return rc;
+  const uint64_t nc = (M + kFragChunk - 1) / kFragChunk;
+  uint8_t* sp = (uint8_t*)scratch;
+  uint32_t* ja = (uint32_t*)sp;
+  uint32_t* jb = ja + (M + 64);
+  uint64_t* cnt = (uint64_t*)(((uintptr_t)(jb + (M + 64)) + 15) & ~(uintptr_t)15);
+  uint64_t* pre = cnt + nc;
+  uint8_t* mark = (uint8_t*)(pre + nc);
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((M + 255) / 256, (uint64_t)cus * 8));
+  hipLaunchKernelGGL(k_frag_next, dim3(grid), dim3(256), 0, st, (const uint8_t*)buf, (uint64_t)nbytes, (uint32_t)M,
+                     ja, mark);
+  if ((rc = launch_done())) return rc;
+  uint32_t steps = 1;
+  while ((1ull << steps) <= M) steps++;
+  for (uint32_t k = 0; k <= steps; k++) {
+    hipLaunchKernelGGL(k_frag_jump, dim3(grid), dim3(256), 0, st, (const uint32_t*)ja, jb, mark, (uint32_t)M);
+    if ((rc = launch_done())) return rc;
+    std::swap(ja, jb);
+  }
+  hipLaunchKernelGGL(k_frag_count, dim3((uint32_t)nc), dim3(kFragChunk), 0, st, (const uint8_t*)mark, (uint32_t)M,
+                     cnt);
+  if ((rc = launch_done())) return rc;
+  hipLaunchKernelGGL(k_tok_scan3, dim3((uint32_t)((nc + kScan3 - 1) / kScan3)), dim3(kScanBlock), 0, st,
+                     (const uint64_t*)cnt, nc, pre, count);
+  if ((rc = launch_done())) return rc;
+  if (cap == 0) return set_err(0);
+  hipLaunchKernelGGL(k_frag_emit, dim3((uint32_t)nc), dim3(kFragChunk), 0, st, (const uint8_t*)mark, (uint32_t)M,
+                     (const uint64_t*)pre, rec_offs, (uint64_t)cap);
+  return launch_done();
+}
+
+int kvh_frags_hash(const void* buf, size_t nbytes, uint64_t seed1, uint64_t seed2, uint32_t flags,
+                   uint64_t* rec_offs, uint64_t* out, size_t cap, uint64_t* count, void* scratch,
+                   size_t scratch_bytes, void* stream) {
+  if (cap && !out) return set_err(KVH_EINVAL);
+  int rc = kvh_frag_offsets(buf, nbytes, rec_offs, cap, count, scratch, scratch_bytes, stream);
+  if (rc || cap == 0 || nbytes < 2) return rc;
+  int cus = 0;
+  if ((rc = device_cus(&cus))) return rc;
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((cap + 1023) / 1024, (uint64_t)cus));
+  hipLaunchKernelGGL((k_keysrc<SRC_FRAGS, 4>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf,
+                     rec_offs, (const uint32_t*)nullptr, (uint64_t)cap, seed1, seed2, out, flags & ~KVH_NULTERM,
+                     (const uint64_t*)count);
   return launch_done();
 }
 

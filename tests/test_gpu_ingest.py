@@ -208,3 +208,60 @@ def test_tokenize_hash_large_text(kvh):
     del o2
     h2 = kvh.meow128_spans(text, o, l2, SEED)
     assert torch.equal(h, h2)
+
+
+def _pack_frags(rng, lens, truncate=0):
+    """kv_key_frag_t records {u16 keylen, bytes, pad to 2} back to back."""
+    parts, offs, o = [], [], 0
+    for L in lens:
+        rec = int(L).to_bytes(2, "little") + bytes(rng.integers(0, 256, int(L), dtype=np.uint8))
+        if len(rec) & 1:
+            rec += b"\0"
+        parts.append(rec)
+        offs.append(o)
+        o += len(rec)
+    buf = b"".join(parts)
+    if truncate:
+        buf = buf[:-truncate]
+    return np.frombuffer(buf, dtype=np.uint8).copy(), np.array(offs, dtype=np.uint64)
+
+
+def test_frag_stream_golden(kvh):
+    """The reference's own packed frag records (ctest's buffer) parse on the
+    device to its record offsets and hash to its kv_hash_key_frag hashes."""
+    frags = torch.from_numpy(G["frags"]).cuda()
+    np.testing.assert_array_equal(host(kvh.frag_offsets(frags)), G["rec_offs"].astype(np.uint64))
+    o, h = kvh.frags_hash(frags, SEED)
+    np.testing.assert_array_equal(host(o), G["rec_offs"].astype(np.uint64))
+    np.testing.assert_array_equal(host(h), G["hashes"])
+    _, h100 = kvh.frags_hash(frags, SEED, cap=100)
+    np.testing.assert_array_equal(host(h100), G["hashes"][:100])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1000, 100003])
+def test_frag_stream_random(kvh, n):
+    """Random streams (keylen 0..300, odd and even), the last record cut
+    short (it must end the stream), against the host packer's offsets and
+    the oracle's hash of each record's bytes."""
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 301, n)
+    lens[rng.integers(0, n, max(1, n // 10))] = rng.integers(0, 3, max(1, n // 10))
+    buf, offs = _pack_frags(rng, lens)
+    np.testing.assert_array_equal(host(kvh.frag_offsets(torch.from_numpy(buf).cuda())), offs)
+    o, h = kvh.frags_hash(torch.from_numpy(buf).cuda(), SEED)
+    np.testing.assert_array_equal(host(o), offs)
+    sp_off = offs + 2
+    want = orc_hash_spans(ORC, buf, sp_off, lens.astype(np.uint32), SEED, nul=False)
+    np.testing.assert_array_equal(host(h), want)
+    if n > 1 and lens[-1] > 1:
+        bt, _ = _pack_frags(np.random.default_rng(n), lens, truncate=1 + (lens[-1] & 1))
+        np.testing.assert_array_equal(host(kvh.frag_offsets(torch.from_numpy(bt).cuda())), offs[:-1])
+
+
+def test_frag_stream_tiny(kvh):
+    for b in (b"", b"\x00", b"\x00\x00", b"\x01\x00a", b"\x01\x00a\x00", b"\x05\x00ab"):
+        arr = np.frombuffer(b, dtype=np.uint8).copy()
+        dev = torch.from_numpy(arr).cuda() if arr.size else torch.zeros(0, dtype=torch.uint8, device="cuda")
+        got = host(kvh.frag_offsets(dev))
+        want = {b"": [], b"\x00": [], b"\x00\x00": [0], b"\x01\x00a": [0], b"\x01\x00a\x00": [0], b"\x05\x00ab": []}[b]
+        np.testing.assert_array_equal(got, np.array(want, dtype=np.uint64), err_msg=repr(b))
