@@ -115,6 +115,34 @@ def test_spans_without_nul_match_var(kvh):
     np.testing.assert_array_equal(host(h), orc_hash_spans(ORC, buf, offs, lens, SEED, nul=False, fix=False))
 
 
+def test_evkey_nul_format(kvh):
+    """EvKeyCtx keys (ev_key.h:105-114 copy_key): the string then a '\\0',
+    keylen = strlen + 1, hashed by HashSeed::hash.  The expected values come
+    from explicit "string\\0" buffers hashed with no appended NUL.  The device
+    hashes (offset, strlen) spans inside unterminated text with KVH_NULTERM."""
+    rng = np.random.default_rng(11)
+    n = 5000
+    strl = rng.integers(0, 300, n).astype(np.uint32)
+    strl[:40] = np.arange(40)                          # every short length, strlen 0 included
+    parts, offs, kb, kb_offs = [], [], [], []
+    pos = kpos = 0
+    for L in strl:
+        s = bytes(rng.integers(1, 256, int(L), dtype=np.uint8))    # no NUL inside a key string
+        gap = bytes(rng.integers(1, 256, int(rng.integers(0, 5)), dtype=np.uint8))
+        offs.append(pos)
+        parts += [s, gap]
+        pos += len(s) + len(gap)
+        kb_offs.append(kpos)
+        kb.append(s + b"\0")
+        kpos += len(s) + 1
+    text = np.frombuffer(b"".join(parts) + b"x", dtype=np.uint8).copy()
+    kbuf = np.frombuffer(b"".join(kb), dtype=np.uint8).copy()
+    want = orc_hash_spans(ORC, kbuf, np.array(kb_offs, np.uint64), strl + 1, SEED, nul=False, fix=True)
+    h = kvh.meow128_spans(torch.from_numpy(text).cuda(), torch.from_numpy(np.array(offs, np.int64)).cuda(),
+                          torch.from_numpy(strl.view(np.int32)).cuda(), SEED)
+    np.testing.assert_array_equal(host(h), want)
+
+
 def test_cap_truncates_but_counts(kvh, tok_kernel):
     text = torch.from_numpy(G["text"]).cuda()
     offs, lens = kvh.tokenize(text, 256, cap=100)
