@@ -23,6 +23,19 @@ raikv_amd/csrc/%.o: raikv_amd/csrc/%.hip $(HDRS)
 $(LIB): $(OBJS) raikv_amd/csrc/kvh.map
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(OBJS)
 
+# Research build (NOT the product): the same sources with -DKVH_EXPERIMENTS,
+# which adds the superseded kernels and the ablation builds (outputs that are
+# not hashes) behind extra kvh_set_tuning knobs.  Used by tools/*.py through
+# KVH_LIB=tools/libkvh_exp.so; never loaded by the tests of the product path.
+EXP_LIB  := tools/libkvh_exp.so
+EXP_OBJS := $(SRCS:raikv_amd/csrc/%.hip=tools/exp/%.o)
+tools/exp/%.o: raikv_amd/csrc/%.hip $(HDRS)
+	@mkdir -p tools/exp
+	$(HIPCC) $(HIPFLAGS) -DKVH_EXPERIMENTS $(INC) -c -o $@ $<
+$(EXP_LIB): $(EXP_OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(EXP_OBJS)
+experiments: $(EXP_LIB)
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -50,7 +63,7 @@ tests/cpp/bs_host_test: tests/cpp/bs_host_test.cpp raikv_amd/csrc/bs_aes.hpp rai
 	g++ -O2 -std=c++17 -o $@ $< -Loracle -loracle -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 clean:
-	rm -f $(LIB) $(OBJS) $(CPP_TESTS)
+	rm -f $(LIB) $(OBJS) $(CPP_TESTS) $(EXP_LIB) $(EXP_OBJS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle cpptests clean
+.PHONY: all oracle cpptests clean experiments

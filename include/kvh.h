@@ -385,24 +385,26 @@ const char *kvh_strerror(int err);
 const char *kvh_version(void);
 /* synchronise the current device (host wall-clock timing helpers) */
 int         kvh_device_synchronize(void);
-/* expert tuning knobs (bench/ablation): 0 = tables-per-LDS (2 or 4),
- * 1 = workgroups per CU multiplier, 2 = force generic kernel (0/1),
- * 3 = keys per lane per step in the fixed-length kernel (1, 2 or 4),
- * 5 = ablation mode of the 16/32-byte kernel (0 product, 1 copy-only,
- *     2 no-load, 3 no-store; outputs are NOT hashes for modes 1-3),
- * 10 = register prefetch of the next chunk in the fixed-length kernel (0/1),
- * 11 = bitsliced share of a 16-byte batch in per mille (0 = T-table only),
- * 14 = variable-length CRC32C kernel (3 length-sorted windows, 16 waves on
- *      16-copy tables; 1 the same with 10 waves on 32-copy tables; 0 input order),
- * 15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort key bits (0 auto),
- * 18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
- *      long queues, two / one spans per lane per step; 0 lane per span;
- *      3, 4 ablations whose outputs are NOT hashes: no rounds; no text),
- * 19 = tokenizer (1 wave-chunked, 0 workgroup-chunked).
- * Returns the previous value or KVH_EINVAL. */
+/* Tuning knobs: each selects among kernels that return the same hashes, or
+ * sizes the host pipeline.  Process-wide; atomic (a call already running
+ * keeps the value it read).
+ *   0 = tables per LDS (0 per-length default, 2 or 4),
+ *   1 = workgroups per CU multiplier (1-8), 2 = force the generic kernel (0/1),
+ *   3 = keys per lane per step in the fixed-length kernel (0 default, 1, 2, 4, 8),
+ *   7 = variable-length kernel (13 default: per-wave windows sorted by 16-byte
+ *       length class; 7 by exact length; 0 lane per key in input order),
+ *   8 = multi-seed kernel (1 lanes per key, 0 one lane per key),
+ *  14 = variable-length CRC32C kernel (3 length-sorted windows, 16 waves on
+ *       16-copy tables; 1 the same with 10 waves on 32-copy tables; 2 with 8
+ *       waves; 0 input order),
+ *  15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort key bits (0 auto),
+ *  18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
+ *       long queues, two / one spans per lane per step; 0 lane per span),
+ *  19 = tokenizer (1 wave-chunked, 0 workgroup-chunked).
+ * Returns the previous value or KVH_EINVAL.  (Research kernels and ablation
+ * builds whose outputs are not hashes exist only in the experiments build,
+ * tools/libkvh_exp.so, never in libkvh.so.) */
 int         kvh_set_tuning(int knob, int value);
-/* diagnostics: per-wave phase cycle stamps of the last stamped launch */
-int         kvh_debug_stamps(uint64_t *host, size_t count);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,9 @@ KVH_DEDUP = 0x8
 KVH_MAX_ARITY = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-lib_path = os.path.join(_HERE, "libkvh.so")
+# KVH_LIB: research tools (tools/*.py) point this at the experiments build
+# tools/libkvh_exp.so; the product path and its tests load libkvh.so.
+lib_path = os.environ.get("KVH_LIB") or os.path.join(_HERE, "libkvh.so")
 
 U64 = C.c_uint64
 U32 = C.c_uint32

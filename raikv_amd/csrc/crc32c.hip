@@ -285,6 +285,19 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
   for (uint64_t w = (uint64_t)blockIdx.x * NW + wv; w < nwin; w += (uint64_t)gridDim.x * NW) {
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    if (offs[i0 + k] - offs[i0] >= (1ull << 32)) {
+      // a window spanning 4 GiB or more: its records would hold u32 window
+      // offsets, so it runs in input order with u64 offsets (wave-uniform)
+#pragma unroll 1
+      for (int c = 0; c < M; c++) {
+        const uint32_t j = 64 * c + lane;
+        if (j < k) {
+          const uint64_t a = offs[i0 + j], e = offs[i0 + j + 1];
+          out[i0 + j] = crc_key_pf(keys + a, e - a, seeds ? seeds[i0 + j] : seed, T);
+        }
+      }
+      continue;
+    }
     const uint64_t ws = wave_sort_window<WIN, SH>(offs, i0, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
     // (running the lane's M keys as interleaved chains was slower: each
     // lane then steps as long as its longest key, chunk M-1's)
@@ -316,7 +329,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
 }
 
 }  // namespace
-namespace kvh { namespace rt { int g_tune_crc_var = 3; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_crc_var{3}; } }
 namespace {
 
 uint32_t grid_crc(uint64_t n, int cus) {
@@ -419,13 +432,14 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
   if (!out || !offsets || !keys) return set_err(KVH_EINVAL);
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
-  if (g_tune_crc_var == 1)
+  const int v = g_tune_crc_var.load(std::memory_order_relaxed);
+  if (v == 1)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 10>), dim3(cus), dim3(640), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
-  else if (g_tune_crc_var == 3)  // tables with 16 copies (64 KiB): 16 waves per CU
+  else if (v == 3)  // tables with 16 copies (64 KiB): 16 waves per CU
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
-  else if (g_tune_crc_var == 2)
+  else if (v == 2)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 8>), dim3(cus), dim3(512), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else

@@ -222,13 +222,14 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   const uint32_t sb = slot_bits(geom->ht_size);
   uint32_t lg = 0;
   while (lg < 63 && (1ull << lg) < (uint64_t)n) lg++;
-  uint32_t nb = g_tune_sort_bits ? sb + (uint32_t)g_tune_sort_bits : std::max(sb + 1, lg + 5);
+  const int tsb = g_tune_sort_bits.load(std::memory_order_relaxed);
+  uint32_t nb = tsb ? sb + (uint32_t)tsb : std::max(sb + 1, lg + 5);
   if (nb > 64) nb = 64;
   // u32 keys halve the key bytes every radix pass moves (16 instead of 24 per
   // element with the index): used when the prefix fits 31 bits -- all slot
   // bits and as many h1 bits as fit (rocPRIM's merge path, taken for small n,
   // builds its mask as (T(1) << end_bit) - 1: undefined at the type's width)
-  const bool k32 = !g_tune_sort_bits && sb <= 31;
+  const bool k32 = !tsb && sb <= 31;
   if (k32) nb = std::min(nb, 31u);
   const uint32_t lo = 64u - nb;
   int cus = 0;
@@ -274,7 +275,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
 
 }  // namespace
 
-namespace kvh { namespace rt { int g_tune_sort_bits = 0; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; } }
 
 extern "C" {
 

@@ -889,7 +889,7 @@ k_frag_emit(const uint8_t* __restrict__ mark, uint32_t M, const uint64_t* __rest
 }
 
 }  // namespace
-namespace kvh { namespace rt { int g_tune_spans = 2; int g_tune_tok = 1; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_spans{2}; std::atomic<int> g_tune_tok{1}; } }
 namespace {
 
 TokGeo tok_geo(const void* text, size_t nbytes) {
@@ -926,7 +926,7 @@ int kvh_tokenize(const void* text, size_t nbytes, uint32_t max_token, uint64_t* 
   const TokGeo G = tok_geo(text, nbytes);
   uint64_t* cc = (uint64_t*)scratch;
   const uint8_t* t = (const uint8_t*)text;
-  if (g_tune_tok) {
+  if (g_tune_tok.load(std::memory_order_relaxed)) {
     const uint64_t nc = (G.nseg * kTokSeg + kTok2Chunk - 1) / kTok2Chunk;
     uint64_t* pre = cc + nc;
     const uint32_t grid = (uint32_t)((nc + 3) / 4);
@@ -1044,16 +1044,20 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
-  if (g_tune_spans == 3)  // ablation: loads and stores, no table rounds (outputs are not hashes)
+  const int sk = g_tune_spans.load(std::memory_order_relaxed);
+#ifdef KVH_EXPERIMENTS
+  if (sk == 3)  // ablation: loads and stores, no table rounds (outputs are not hashes)
     hipLaunchKernelGGL((k_spans<4, 2, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);
-  else if (g_tune_spans == 4)  // ablation: offsets/lengths in, hashes out only (no text, no medium/long path)
+  else if (sk == 4)  // ablation: offsets/lengths in, hashes out only (no text, no medium/long path)
     hipLaunchKernelGGL((k_spans<4, 2, 3>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);
-  else if (g_tune_spans == 2)
+  else
+#endif
+  if (sk == 2)
     hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);
-  else if (g_tune_spans == 1)
+  else if (sk == 1)
     hipLaunchKernelGGL((k_spans<4, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);
   else

@@ -10,15 +10,25 @@
 //   k_seeded              straight-line restatement, per-key seeds, constant
 //                         memory tables (drop-ins, x2/x4/x8 variants)
 //   k_stream_*            streaming init/update/final state transitions
+//
+// Research kernels that lost their A/B (k_var, k_var3, k_var5,
+// k_fixed_dma, k_hybrid, the ablation builds of k_fixed whose outputs are
+// not hashes) compile only with -DKVH_EXPERIMENTS, into
+// tools/libkvh_exp.so (`make experiments`); libkvh.so, the product, holds
+// none of them and no exported call of it returns anything but hashes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
+#include <atomic>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <algorithm>
 #include "meow_dev.hpp"
+#ifdef KVH_EXPERIMENTS
 #include "bs_prelude.hpp"
+#endif
 #include "kvh_internal.hpp"
 #include "../../include/kvh.h"
 
@@ -168,6 +178,7 @@ k_fixed_lanes(const uint8_t* __restrict__ keys, uint64_t n, uint64_t* __restrict
   }
 }
 
+#ifdef KVH_EXPERIMENTS
 // ---------------------------------------------------------------------
 // LDS-DMA streaming (opt-in, knob 6; the register path k_fixed is C1/C4's
 // default: 153.9 vs 130-139 G hash/s at ring depths 2-6, tools/tune.py).
@@ -280,6 +291,7 @@ k_fixed_dma(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t 
     }
   }
 }
+#endif  // KVH_EXPERIMENTS
 
 template <int L, int NT, bool A16>
 __global__ void __launch_bounds__(kBlock)
@@ -351,8 +363,8 @@ k_generic(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, u
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     if constexpr (VAR) {
       const uint64_t o0 = offs[i], o1 = offs[i + 1];
-      const uint32_t L = (uint32_t)(o1 - o0);
-      const LdsK<LdsTab<NT>> K(kfull, kf, L, a0, b0, T);
+      const uint64_t L = o1 - o0;  // any size_t length, as kv_hash_meow128 (key_hash.c:1413)
+      const LdsK<LdsTab<NT>, uint64_t> K(kfull, kf, L, a0, b0, T);
       store_h(out, i, meow_rt(keys + o0, L, K, T), fix);
     } else {
       const uint8_t* p = keys + i * (uint64_t)fixed_len;
@@ -365,6 +377,7 @@ k_generic(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, u
   }
 }
 
+#ifdef KVH_EXPERIMENTS
 // ---------------------------------------------------------------------
 // Variable-length batches (config C2).  One lane per key, but NOT in input
 // order: each workgroup takes a window of 1024 consecutive keys, counting-
@@ -622,6 +635,7 @@ k_var3(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     __syncthreads();  // staging area reuse
   }
 }
+#endif  // KVH_EXPERIMENTS
 
 // k_var5: windows of 1024 keys; the window's contiguous key bytes are
 // streamed into an LDS staging buffer by LDS-DMA (coalesced 1 KiB pieces)
@@ -640,21 +654,21 @@ struct VConst {  // MeowConst minus the Mixer (recomputed in-lane)
   Blk F[4], G[4], TG2, CS2b, TCS0a;
 };
 
-template <class Tab>
+template <class Tab, class LenT = uint32_t>
 struct LdsKV5 {
   const VConst* full;
-  uint32_t L;
+  LenT L;
   Blk m;
   const Tab& T;
   const Blk* ftab;  // first-absorb folds F[0..3] for kLT <= L < kLT + kNF, or null
-  __device__ __forceinline__ LdsKV5(const VConst* f, uint32_t len, uint64_t s1, uint64_t s2, const Tab& t,
+  __device__ __forceinline__ LdsKV5(const VConst* f, LenT len, uint64_t s1, uint64_t s2, const Tab& t,
                                     const Blk* ft = nullptr)
       : full(f), L(len), m(mixer(s1, s2, len)), T(t), ftab(ft) {}
-  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ uint32_t li() const { return L < (LenT)kLT ? (uint32_t)L : (uint32_t)kLT - 1; }
   __device__ __forceinline__ Blk M() const { return m; }
   __device__ __forceinline__ Blk F(int i) const {
-    if (L < (uint32_t)kLT) return full[L].F[i];
-    if (ftab && L < (uint32_t)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
+    if (L < (LenT)kLT) return full[L].F[i];
+    if (ftab && L < (LenT)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
     return aesT(bxor(ramp(i), m), T);
   }
   __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
@@ -663,6 +677,7 @@ struct LdsKV5 {
   __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
 };
 
+#ifdef KVH_EXPERIMENTS
 template <int NT>
 struct Var5Cfg {
   static constexpr int kTab = NT * 8192 * 4;
@@ -858,6 +873,7 @@ k_var5(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       for (int q = 0; q < 6; q++) g_dbg[gw * 8 + q] = acc[q];
   }
 }
+#endif  // KVH_EXPERIMENTS
 
 // ---------------------------------------------------------------------
 // k_var6: per-WAVE windows, no workgroup barriers after the prologue.
@@ -929,6 +945,22 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
     const uint64_t ws = offs[i0];
+    if (offs[i0 + k] - ws >= (1ull << 32)) {
+      // A window spanning 4 GiB or more (some key of >= 16 MiB; a key of
+      // >= 4 GiB): the records below hold u32 window offsets and lengths, so
+      // this window is hashed in input order with u64 offsets and lengths
+      // instead (wave-uniform branch).
+#pragma unroll 1
+      for (int c = 0; c < M; c++) {
+        const uint32_t j = 64 * c + lane;
+        if (j < k) {
+          const uint64_t a = offs[i0 + j], len = offs[i0 + j + 1] - a;
+          const LdsKV5<LdsTab<NT>, uint64_t> K(kfull, len, s1, s2, T, ftab);
+          store_h(out, i0 + j, meow_rt(keys + a, len, K, T), fix);
+        }
+      }
+      continue;
+    }
     uint64_t o[M];
     uint32_t L[M], b[M], r[M];
 #pragma unroll
@@ -1036,6 +1068,7 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
   }
 }
 
+#ifdef KVH_EXPERIMENTS
 // ---------------------------------------------------------------------
 // k_hybrid: the LDS T-table round and the bitsliced VALU round (bs_meow.hpp)
 // side by side in one workgroup per CU.  The T-table keys are bound by the
@@ -1126,6 +1159,7 @@ k_hybrid(const uint8_t* __restrict__ keys, uint64_t n, uint64_t nB, uint64_t s1,
     }
   }
 }
+#endif  // KVH_EXPERIMENTS
 
 // straight-line restatement, one thread per key, per-key seeds
 __global__ void __launch_bounds__(256)
@@ -1208,23 +1242,30 @@ int launch_done() {
 namespace {
 
 // ------------------------------------------------------------ host side
-int g_tune_nt = 0;        // tables per LDS: 2 or 4 (0 = per-length default)
-int g_tune_wgmul = 1;     // workgroups per CU multiplier
-int g_tune_generic = 0;   // force the generic kernel
-int g_tune_kpl = 0;       // keys per lane per chunk in k_fixed (1, 2, 4 or 8; 0 = per-length default)
-int g_tune_pf = 0;        // k_fixed: 1 = register prefetch of the next chunk
-int g_tune_bs = 0;        // hybrid kernel: bitsliced share of the keys in per mille (0 = k_fixed)
-int g_tune_bsw = 4;       // hybrid kernel: bitsliced waves per 16-wave workgroup
-int g_tune_prio = 2;      // hybrid kernel: s_setprio of the T-table waves (0, 2, 3)
-int g_tune_ablate = 0;    // ablation build of k_fixed (0 = product path)
-int g_tune_dma = 0;       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
-int g_tune_ms_lanes = 1;  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
-int g_tune_var_mode = 0;  // ablation of k_var3: 1 no-hash, 2 no-gather, 3 no-sort
-int g_tune_var = 13;      // var-length kernel: 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic; 2-6, 8-12 experiments
+// Tuning knobs (kvh_set_tuning): process-wide, read once per call with
+// relaxed atomic loads, so a knob set on one thread never races a launch on
+// another (a call in flight keeps the value it read).
+using Knob = std::atomic<int>;
+Knob g_tune_nt{0};        // tables per LDS: 2 or 4 (0 = per-length default)
+Knob g_tune_wgmul{1};     // workgroups per CU multiplier
+Knob g_tune_generic{0};   // force the generic kernel
+Knob g_tune_kpl{0};       // keys per lane per chunk in k_fixed (1, 2, 4 or 8; 0 = per-length default)
+Knob g_tune_ms_lanes{1};  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
+Knob g_tune_var{13};      // var-length kernel: 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic
+#ifdef KVH_EXPERIMENTS
+Knob g_tune_pf{0};        // k_fixed: 1 = register prefetch of the next chunk
+Knob g_tune_bs{0};        // hybrid kernel: bitsliced share of the keys in per mille (0 = k_fixed)
+Knob g_tune_bsw{4};       // hybrid kernel: bitsliced waves per 16-wave workgroup
+Knob g_tune_prio{2};      // hybrid kernel: s_setprio of the T-table waves (0, 2, 3)
+Knob g_tune_ablate{0};    // ablation build of k_fixed (0 = product path)
+Knob g_tune_dma{0};       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
+Knob g_tune_var_mode{0};  // ablation of k_var3: 1 no-hash, 2 no-gather, 3 no-sort
+#endif
+inline int knob(const Knob& k) { return k.load(std::memory_order_relaxed); }
 
 uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
   const uint64_t need = (n + kBlock - 1) / kBlock;
-  uint64_t g = (uint64_t)cus * (uint64_t)std::max(1, wg_per_cu * g_tune_wgmul);
+  uint64_t g = (uint64_t)cus * (uint64_t)std::max(1, wg_per_cu * knob(g_tune_wgmul));
   if (need < g) g = need;
   return (uint32_t)std::max<uint64_t>(g, 1);
 }
@@ -1250,18 +1291,20 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
   if constexpr (L == 16 || L == 32) {
     // per-length defaults from tools/tune.py: Td0..Td3 in LDS
     // (no rotations), 4 keys per lane at 16 B, 2 at 32 B
-    const int nt = g_tune_nt ? g_tune_nt : 4;
-    const int kpl = g_tune_kpl ? g_tune_kpl : (L == 16 ? 4 : 2);
-    if (g_tune_ablate) {
-      switch (g_tune_ablate) {
+    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
+    const int nt = tnt ? tnt : 4;
+    const int kpl = tkpl ? tkpl : (L == 16 ? 4 : 2);
+#ifdef KVH_EXPERIMENTS
+    if (const int ab = knob(g_tune_ablate)) {
+      switch (ab) {
         case 1: return launch_k<L, 2, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
         case 2: return launch_k<L, 2, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
         case 3: return launch_k<L, 2, 4, 3>(keys, n, s1, s2, out, flags, st, cus);
         default: return set_err(KVH_EINVAL);
       }
     }
-    if (g_tune_dma && ((uintptr_t)keys & 15) == 0) {
-      const int dk = (g_tune_nt ? g_tune_nt : 2) * 10 + g_tune_dma;
+    if (knob(g_tune_dma) && ((uintptr_t)keys & 15) == 0) {
+      const int dk = (tnt ? tnt : 2) * 10 + knob(g_tune_dma);
       const uint32_t grid = grid_for(n, cus, 1);
       switch (dk) {
 #define KVH_DMA(NTv, Rv)                                                                              \
@@ -1277,10 +1320,10 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
         default: break;
       }
     }
-    if (L == 16 && g_tune_bs > 0 && ((uintptr_t)keys & 15) == 0) {
-      const uint64_t nB = (uint64_t)((double)n * g_tune_bs / 1000.0) / 512 * 512;
+    if (L == 16 && knob(g_tune_bs) > 0 && ((uintptr_t)keys & 15) == 0) {
+      const uint64_t nB = (uint64_t)((double)n * knob(g_tune_bs) / 1000.0) / 512 * 512;
       const uint32_t grid = grid_for(n, cus, 1);
-      const int hk = g_tune_prio * 1000 + nt * 100 + kpl * 10 + g_tune_bsw;
+      const int hk = knob(g_tune_prio) * 1000 + nt * 100 + kpl * 10 + knob(g_tune_bsw);
       switch (hk) {
 #define KVH_HY(Pv, NTv, Uv, Wv)                                                                               \
   case Pv * 1000 + NTv * 100 + Uv * 10 + Wv:                                                                 \
@@ -1292,12 +1335,17 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
         default: return set_err(KVH_EINVAL);
       }
     }
-    const int key = g_tune_pf * 1000 + nt * 100 + kpl;
-    switch (key) {
-      case 1201: return launch_k<L, 2, 1, 0, true>(keys, n, s1, s2, out, flags, st, cus);
-      case 1202: return launch_k<L, 2, 2, 0, true>(keys, n, s1, s2, out, flags, st, cus);
-      case 1204: return launch_k<L, 2, 4, 0, true>(keys, n, s1, s2, out, flags, st, cus);
-      case 1402: return launch_k<L, 4, 2, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+    if (knob(g_tune_pf)) {
+      switch (nt * 100 + kpl) {
+        case 201: return launch_k<L, 2, 1, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+        case 202: return launch_k<L, 2, 2, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+        case 204: return launch_k<L, 2, 4, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+        case 402: return launch_k<L, 4, 2, 0, true>(keys, n, s1, s2, out, flags, st, cus);
+        default: return set_err(KVH_EINVAL);
+      }
+    }
+#endif  // KVH_EXPERIMENTS
+    switch (nt * 100 + kpl) {
       case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
       case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
       case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
@@ -1447,8 +1495,8 @@ int same_len_host(const void* const* ptrs, size_t cnt, size_t sz, const uint64_t
 // demand, kept for the process lifetime).
 constexpr int kPipeSlots = 16;  // buffer slots allocated; g_tune_pipe_slots of them used
 constexpr int kMaxDev = 64;
-int g_tune_pipe_mib = 16;   // key bytes per pipeline chunk, MiB (knob 15)
-int g_tune_pipe_slots = 4;  // chunks in flight (knob 16)
+Knob g_tune_pipe_mib{16};   // key bytes per pipeline chunk, MiB (knob 15)
+Knob g_tune_pipe_slots{4};  // chunks in flight (knob 16)
 struct HostPipe {
   std::mutex mu;
   hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
@@ -1508,7 +1556,7 @@ int kvh_meow128_fixed(const void* keys, uint32_t key_len, size_t n, uint64_t see
   const uint8_t* k = (const uint8_t*)keys;
   hipStream_t st = (hipStream_t)stream;
   const bool a8 = ((uintptr_t)k & 7) == 0;
-  if (!g_tune_generic && a8) {
+  if (!knob(g_tune_generic) && a8) {
     switch (key_len) {
       case 8: return launch_fixed_nt<8>(k, n, seed1, seed2, out, flags, st, cus);
       case 16: return launch_fixed_nt<16>(k, n, seed1, seed2, out, flags, st, cus);
@@ -1531,62 +1579,70 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
   if (!keys || !offsets || !out) return set_err(KVH_EINVAL);
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
-  if (g_tune_var == 0) {
-    uint64_t s[16] = {seed1, seed2};
-    return launch_generic(true, (const uint8_t*)keys, offsets, 0, n, s, 1, out, flags, (hipStream_t)stream,
-                          cus);
-  }
-  if (g_tune_var >= 7 && g_tune_var <= 13) {
-    const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
-    hipStream_t st = (hipStream_t)stream;
-    const uint8_t* kp = (const uint8_t*)keys;
-    switch (g_tune_var) {
-      case 13: hipLaunchKernelGGL((k_var6<2, 256, false, kBlock / 64, 4>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-      case 11: hipLaunchKernelGGL((k_var6<2, 384, false, 12>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-      case 12: hipLaunchKernelGGL((k_var6<2, 512, false, 10>), dim3(cus), dim3(640), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-      case 7: hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-      case 8: hipLaunchKernelGGL((k_var6<2, 128>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-      case 9: hipLaunchKernelGGL((k_var6<2, 256, true>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-      default: hipLaunchKernelGGL((k_var6<2, 128, true>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
+  hipStream_t st = (hipStream_t)stream;
+  const uint8_t* kp = (const uint8_t*)keys;
+  const int var = knob(g_tune_var);
+  const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
+  switch (var) {
+    case 0: {
+      uint64_t s[16] = {seed1, seed2};
+      return launch_generic(true, kp, offsets, 0, n, s, 1, out, flags, st, cus);
     }
-    return launch_done();
+    case 13:
+      hipLaunchKernelGGL((k_var6<2, 256, false, kBlock / 64, 4>), dim3(grid), dim3(kBlock), 0, st, kp, offsets,
+                         (uint64_t)n, seed1, seed2, out, flags);
+      return launch_done();
+    case 7:
+      hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
+                         out, flags);
+      return launch_done();
+    default:
+      break;
   }
-  if (g_tune_var == 6) {
-    const uint32_t grid = grid_for(n, cus, 1);
-    if (g_tune_var_mode == 1)
-      hipLaunchKernelGGL((k_var5<2, true>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
-                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+#ifdef KVH_EXPERIMENTS
+  switch (var) {
+    case 11: hipLaunchKernelGGL((k_var6<2, 384, false, 12>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 12: hipLaunchKernelGGL((k_var6<2, 512, false, 10>), dim3(cus), dim3(640), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 8: hipLaunchKernelGGL((k_var6<2, 128>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 9: hipLaunchKernelGGL((k_var6<2, 256, true>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 10: hipLaunchKernelGGL((k_var6<2, 128, true>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    default: break;
+  }
+  const int vm = knob(g_tune_var_mode);
+  if (var == 6) {
+    const uint32_t g1 = grid_for(n, cus, 1);
+    if (vm == 1)
+      hipLaunchKernelGGL((k_var5<2, true>), dim3(g1), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags);
     else
-      hipLaunchKernelGGL((k_var5<2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
-                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+      hipLaunchKernelGGL((k_var5<2>), dim3(g1), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags);
     return launch_done();
   }
-  if (g_tune_var == 3 || g_tune_var == 5) {
-    const uint32_t grid = grid_for((n + 3) / 4, cus, 1);
-    if (g_tune_var_mode) {
-      switch (g_tune_var_mode) {
-        case 1: hipLaunchKernelGGL((k_var3<2, 4, 1>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-        case 2: hipLaunchKernelGGL((k_var3<2, 4, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
-        default: hipLaunchKernelGGL((k_var3<2, 4, 3>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
+  if (var == 3 || var == 5) {
+    const uint32_t g4 = grid_for((n + 3) / 4, cus, 1);
+    if (vm) {
+      switch (vm) {
+        case 1: hipLaunchKernelGGL((k_var3<2, 4, 1>), dim3(g4), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
+        case 2: hipLaunchKernelGGL((k_var3<2, 4, 2>), dim3(g4), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
+        default: hipLaunchKernelGGL((k_var3<2, 4, 3>), dim3(g4), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); break;
       }
       return launch_done();
     }
-    if (g_tune_var == 5)
-      hipLaunchKernelGGL((k_var3<2, 4>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
-                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+    if (var == 5)
+      hipLaunchKernelGGL((k_var3<2, 4>), dim3(g4), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags);
     else
-      hipLaunchKernelGGL((k_var3<2, 2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
-                         offsets, (uint64_t)n, seed1, seed2, out, flags);
+      hipLaunchKernelGGL((k_var3<2, 2>), dim3(g4), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags);
     return launch_done();
   }
-  const uint32_t grid = grid_for(n, cus, 1);
-  if (g_tune_var == 4)
-    hipLaunchKernelGGL((k_var<4>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
-                       offsets, (uint64_t)n, seed1, seed2, out, flags);
-  else
-    hipLaunchKernelGGL((k_var<2>), dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, (const uint8_t*)keys,
-                       offsets, (uint64_t)n, seed1, seed2, out, flags);
-  return launch_done();
+  if (var == 2 || var == 4) {
+    const uint32_t g1 = grid_for(n, cus, 1);
+    if (var == 4)
+      hipLaunchKernelGGL((k_var<4>), dim3(g1), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags);
+    else
+      hipLaunchKernelGGL((k_var<2>), dim3(g1), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags);
+    return launch_done();
+  }
+#endif
+  return set_err(KVH_EINVAL);
 }
 
 int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const uint64_t* seeds,
@@ -1601,7 +1657,7 @@ int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const ui
   const uint8_t* k = (const uint8_t*)keys;
   hipStream_t st = (hipStream_t)stream;
   const bool a8 = ((uintptr_t)k & 7) == 0;
-  if (!g_tune_generic && a8 && g_tune_ms_lanes && (arity == 2 || arity == 4 || arity == 8)) {
+  if (!knob(g_tune_generic) && a8 && knob(g_tune_ms_lanes) && (arity == 2 || arity == 4 || arity == 8)) {
     switch (key_len) {
       case 8: return launch_lanes_L<8>(k, n, s, arity, out, flags, st, cus);
       case 16: return launch_lanes_L<16>(k, n, s, arity, out, flags, st, cus);
@@ -1614,7 +1670,7 @@ int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const ui
       default: break;
     }
   }
-  if (!g_tune_generic && a8) {
+  if (!knob(g_tune_generic) && a8) {
     switch (key_len) {
       case 16: return launch_ms_L<16>(k, n, s, arity, out, flags, st, cus);
       case 32: return launch_ms_L<32>(k, n, s, arity, out, flags, st, cus);
@@ -1665,12 +1721,12 @@ int kvh_meow128_fixed_host(const void* keys, uint32_t key_len, size_t n, uint64_
   if (dev < 0 || dev >= kMaxDev) return set_err(KVH_EINVAL);
   HostPipe& P = g_pipe[dev];
   std::lock_guard<std::mutex> lk(P.mu);
-  const size_t chunk = std::max<size_t>(1, ((size_t)g_tune_pipe_mib << 20) / key_len);
+  const size_t chunk = std::max<size_t>(1, ((size_t)knob(g_tune_pipe_mib) << 20) / key_len);
   hipPointerAttribute_t ak, ao;
   const bool pin_k = hipPointerGetAttributes(&ak, keys) == hipSuccess && ak.type == hipMemoryTypeHost;
   const bool pin_o = hipPointerGetAttributes(&ao, out) == hipSuccess && ao.type == hipMemoryTypeHost;
   (void)hipGetLastError();
-  const int slots = std::min(std::max(g_tune_pipe_slots, 2), kPipeSlots);
+  const int slots = std::min(std::max(knob(g_tune_pipe_slots), 2), kPipeSlots);
   int rc = P.reserve(slots, chunk * key_len, chunk * 16, !pin_k, !pin_o);
   if (rc) return rc;
   size_t pend_lo[kPipeSlots] = {}, pend_cnt[kPipeSlots] = {};
@@ -1916,12 +1972,14 @@ int kvh_hash_key_frags(const uint64_t seed[2], const kvh_key_frag_t* const* frag
   return seeded_host(ps.data(), ls.data(), n, seeds.data(), out, KVH_FIXUP);
 }
 
+#ifdef KVH_EXPERIMENTS
 // diagnostics: copy the per-wave phase stamps of the last STAMP launch
 int kvh_debug_stamps(uint64_t* host, size_t count) {
   if (count > 4096 * 8) count = 4096 * 8;
   hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg), count * 8, 0, hipMemcpyDeviceToHost);
   return e == hipSuccess ? set_err(0) : hip_err(e);
 }
+#endif
 
 int kvh_last_error(void) { return t_last_err; }
 
@@ -1941,30 +1999,48 @@ int kvh_device_synchronize(void) {
   return e == hipSuccess ? set_err(0) : hip_err(e);
 }
 
-int kvh_set_tuning(int knob, int value) {
-  int prev;
-  switch (knob) {
-    case 0: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL; prev = g_tune_nt; g_tune_nt = value; return prev;
-    case 1: if (value < 1 || value > 8) return KVH_EINVAL; prev = g_tune_wgmul; g_tune_wgmul = value; return prev;
-    case 2: prev = g_tune_generic; g_tune_generic = value ? 1 : 0; return prev;
-    case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_kpl; g_tune_kpl = value; return prev;
-    case 11: if (value < 0 || value > 1000) return KVH_EINVAL; prev = g_tune_bs; g_tune_bs = value; return prev;
-    case 12: if (value != 2 && value != 4 && value != 8) return KVH_EINVAL; prev = g_tune_bsw; g_tune_bsw = value; return prev;
-    case 13: if (value != 0 && value != 2 && value != 3) return KVH_EINVAL; prev = g_tune_prio; g_tune_prio = value; return prev;
-    case 14: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_crc_var; g_tune_crc_var = value; return prev;
-    case 16: if (value < 2 || value > 16) return KVH_EINVAL; prev = g_tune_pipe_slots; g_tune_pipe_slots = value; return prev;
-    case 15: if (value < 1 || value > 1024) return KVH_EINVAL; prev = g_tune_pipe_mib; g_tune_pipe_mib = value; return prev;
-    case 17: if (value < 0 || value > 64) return KVH_EINVAL; prev = g_tune_sort_bits; g_tune_sort_bits = value; return prev;
-    case 19: if (value < 0 || value > 1) return KVH_EINVAL; prev = g_tune_tok; g_tune_tok = value; return prev;
-    case 18: if (value < 0 || value > 4) return KVH_EINVAL; prev = g_tune_spans; g_tune_spans = value; return prev;
-    case 10: prev = g_tune_pf; g_tune_pf = value ? 1 : 0; return prev;
-    case 5: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_ablate; g_tune_ablate = value; return prev;
-    case 9: if (value < 0 || value > 3) return KVH_EINVAL; prev = g_tune_var_mode; g_tune_var_mode = value; return prev;
-    case 8: prev = g_tune_ms_lanes; g_tune_ms_lanes = value ? 1 : 0; return prev;
-    case 7: if (value < 0 || value > 13 || value == 1) return KVH_EINVAL;
-            prev = g_tune_var; g_tune_var = value; return prev;
+// Every knob selects among kernels whose outputs are the same hashes (or
+// sizes the host pipeline); the ablation and research knobs exist only in
+// the experiments build.  Atomic exchange: safe against concurrent calls.
+int kvh_set_tuning(int k, int value) {
+  auto set = [](Knob& g, int v) { return g.exchange(v, std::memory_order_relaxed); };
+  switch (k) {
+    case 0: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL; return set(g_tune_nt, value);
+    case 1: if (value < 1 || value > 8) return KVH_EINVAL; return set(g_tune_wgmul, value);
+    case 2: return set(g_tune_generic, value ? 1 : 0);
+    case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL;
+            return set(g_tune_kpl, value);
+    case 7: if (value != 0 && value != 7 && value != 13) {
+#ifdef KVH_EXPERIMENTS
+              if (value < 2 || value > 12) return KVH_EINVAL;
+#else
+              return KVH_EINVAL;
+#endif
+            }
+            return set(g_tune_var, value);
+    case 8: return set(g_tune_ms_lanes, value ? 1 : 0);
+    case 14: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_crc_var, value);
+    case 15: if (value < 1 || value > 1024) return KVH_EINVAL; return set(g_tune_pipe_mib, value);
+    case 16: if (value < 2 || value > 16) return KVH_EINVAL; return set(g_tune_pipe_slots, value);
+    case 17: if (value < 0 || value > 64) return KVH_EINVAL; return set(g_tune_sort_bits, value);
+    case 18:
+#ifdef KVH_EXPERIMENTS
+      if (value < 0 || value > 4) return KVH_EINVAL;
+#else
+      if (value < 0 || value > 2) return KVH_EINVAL;
+#endif
+      return set(g_tune_spans, value);
+    case 19: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_tok, value);
+#ifdef KVH_EXPERIMENTS
+    case 5: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_ablate, value);
     case 6: if (value != 0 && value != 2 && value != 3 && value != 4 && value != 6) return KVH_EINVAL;
-            prev = g_tune_dma; g_tune_dma = value; return prev;
+            return set(g_tune_dma, value);
+    case 9: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_var_mode, value);
+    case 10: return set(g_tune_pf, value ? 1 : 0);
+    case 11: if (value < 0 || value > 1000) return KVH_EINVAL; return set(g_tune_bs, value);
+    case 12: if (value != 2 && value != 4 && value != 8) return KVH_EINVAL; return set(g_tune_bsw, value);
+    case 13: if (value != 0 && value != 2 && value != 3) return KVH_EINVAL; return set(g_tune_prio, value);
+#endif
     default: return KVH_EINVAL;
   }
 }

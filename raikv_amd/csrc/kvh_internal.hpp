@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <atomic>
 #include "meow_dev.hpp"
 
 namespace kvh {
@@ -52,22 +53,23 @@ constexpr int kNF = 256;  // F-only records for 64 <= L < 64 + kNF
 
 // Per-length folding constants of a variable-length batch from LDS tables
 // (k_generic, k_keysrc): full records for L < kLT, first-absorb folds for
-// kLT <= L < kLT + kNF, in-lane folds beyond.
-template <class Tab>
+// kLT <= L < kLT + kNF, in-lane folds beyond.  LenT = uint64_t for keys of
+// 4 GiB and more (the Mixer takes the full length, key_hash.c:1418).
+template <class Tab, class LenT = uint32_t>
 struct LdsK {
   const MeowConst* full;   // [kLT]
   const Blk* ftab;         // [kNF][4], or null: folds in-lane
-  uint32_t L;
+  LenT L;
   Blk m;
   const Tab& T;
-  __device__ __forceinline__ LdsK(const MeowConst* f, const Blk* ft, uint32_t len, uint64_t s1,
+  __device__ __forceinline__ LdsK(const MeowConst* f, const Blk* ft, LenT len, uint64_t s1,
                                   uint64_t s2, const Tab& t)
       : full(f), ftab(ft), L(len), m(mixer(s1, s2, len)), T(t) {}
-  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ uint32_t li() const { return L < (LenT)kLT ? (uint32_t)L : (uint32_t)kLT - 1; }
   __device__ __forceinline__ Blk M() const { return m; }
   __device__ __forceinline__ Blk F(int i) const {
-    if (L < (uint32_t)kLT) return full[L].F[i];
-    if (ftab && L < (uint32_t)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
+    if (L < (LenT)kLT) return full[L].F[i];
+    if (ftab && L < (LenT)(kLT + kNF)) return ftab[(L - kLT) * 4 + i];
     return aesT(bxor(ramp(i), m), T);
   }
   __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
@@ -186,12 +188,15 @@ int device_cus(int* cus);
 int launch_done();
 // variable-length CRC32C kernel: 3 = length-sorted windows on 16-copy tables (default), 1 = on 32-copy
 // tables, 0 = lane per key in input order
-extern int g_tune_crc_var;
+// (tuning knobs are atomics: kvh_set_tuning may run concurrently with launches)
+extern std::atomic<int> g_tune_crc_var;
 // table-order sort: h1 bits sorted below the slot bits (0 = by batch size; 64 = the full key)
-extern int g_tune_sort_bits;
-// span hashing: 1 = wave-chunked kernel with the short-key path (default), 0 = lane per span
-extern int g_tune_spans;
-extern int g_tune_tok;
+extern std::atomic<int> g_tune_sort_bits;
+// span hashing: 2 / 1 = wave-chunked kernel with the short-key path, two / one spans per lane
+// (default 2), 0 = lane per span
+extern std::atomic<int> g_tune_spans;
+// tokenizer: 1 = wave-chunked (default), 0 = workgroup-chunked
+extern std::atomic<int> g_tune_tok;
 }  // namespace rt
 
 }  // namespace kvh

@@ -346,19 +346,22 @@ struct ConstRef {
 
 // Runtime-length Meow over key bytes at p (global memory).  Branches are
 // wave-uniform when every lane has the same length (generic fixed-length
-// kernel) and lane-divergent (masked) for variable-length batches.
-template <class Tab, class KGet, class Ld = GlobalLd>
-__device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet& K, const Tab& T,
+// kernel) and lane-divergent (masked) for variable-length batches.  LenT is
+// uint32_t on the hot paths; uint64_t for keys (or window spans) of 4 GiB
+// and more (kv_hash_meow128 takes a size_t length, key_hash.c:1413).
+template <class Tab, class KGet, class Ld = GlobalLd, class LenT = uint32_t>
+__device__ __forceinline__ Blk meow_rt(const uint8_t* p, LenT L, const KGet& K, const Tab& T,
                                        const Ld& ld = Ld{}) {
-  const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
+  const LenT nb = L >> 6;
+  const uint32_t C = (uint32_t)L & 48, t = (uint32_t)L & 15;
   Blk S0, S1, S2, S3;
   if (nb > 0) {
     Blk k0 = ld.full(p), k1 = ld.full(p + 16), k2 = ld.full(p + 32),
         k3 = ld.full(p + 48);
     S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
     S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
-    for (uint32_t b = 1; b < nb; b++) {
-      const uint8_t* q = p + 64 * b;
+    for (LenT b = 1; b < nb; b++) {
+      const uint8_t* q = p + (LenT)64 * b;
       k0 = ld.full(q); k1 = ld.full(q + 16);
       k2 = ld.full(q + 32); k3 = ld.full(q + 48);
       S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
@@ -366,7 +369,7 @@ __device__ __forceinline__ Blk meow_rt(const uint8_t* p, uint32_t L, const KGet&
     }
   }
   const bool first = nb == 0;
-  const uint8_t* q = p + 64 * nb;
+  const uint8_t* q = p + (LenT)64 * nb;
   // trail (key_hash.c:1200-1210); a state's first absorb is folded
   if (t) {
     const Blk k = ld.part(q + C, t);

@@ -8,7 +8,8 @@ reference's own functions (kv_hash_meow128 and its batched / streaming /
 vec variants, key_hash.c:1413-2020); the inputs are our own seeded random
 data.  The fixtures are data only (inputs + expected outputs).
 
-    python tests/golden/make_golden.py [--only-cuckoo | --only-crc | --only-ingest | --only-sort]
+    python tests/golden/make_golden.py [--only-cuckoo | --only-crc | --only-ingest | --only-sort |
+                                        --only-partition4]
 
 The table-position fixtures (cuckoo_*.npz) come from the reference's
 ht_init.cpp + ht_cuckoo.cpp compiled where they lie into
@@ -390,6 +391,54 @@ def make_sort():
         print("sort", name, n, "ref dups", int(dups[0]))
 
 
+def partition_digest(d: np.ndarray) -> int:
+    """Order-dependent digest of u64 words: sum of w_i * (2i + 1) mod 2^64."""
+    w = d.reshape(-1).astype(np.uint64)
+    k = (2 * np.arange(w.size, dtype=np.uint64) + np.uint64(1))
+    with np.errstate(over="ignore"):
+        return int(np.sum(w * k, dtype=np.uint64))
+
+
+def make_partition4():
+    """hash_test.cpp:418-442: bytes 0..127 cut at every n <= m <= o < 128
+    into four keys hashed by the reference's kv_hash_meow128_4_diff_length
+    (seed 10101, 20202).  Every key is a substring buf[a:b], so the fixture
+    is the reference's kv_hash_meow128 of all 8385 substrings (the table the
+    device paths are checked against) plus the digest of the reference's own
+    357,760 x 4-diff outputs in loop order; the generator asserts that each
+    4-diff output equals the four substring hashes, which is the reference
+    test's own assertion."""
+    lib = load_ref()
+    buf = bytes(range(128))
+    cb = C.create_string_buffer(buf, 128)
+    idx = np.full((129, 129), -1, dtype=np.int64)
+    subs = []
+    for a in range(129):
+        for b in range(a, 129):
+            idx[a, b] = len(subs)
+            subs.append((a, b))
+    sub = np.array(subs, dtype=np.uint32)
+    h = np.zeros((len(subs), 2), dtype=np.uint64)
+    for i, (a, b) in enumerate(subs):
+        h[i] = meow(lib, buf[a:b], 10101, 20202)
+    trip = [(n, m, o) for n in range(128) for m in range(n, 128) for o in range(m, 128)]
+    d = np.zeros((len(trip), 8), dtype=np.uint64)
+    x = (U64 * 8)()
+    for t, (n, m, o) in enumerate(trip):
+        for q in range(0, 8, 2):
+            x[q], x[q + 1] = 10101, 20202
+        lib.kv_hash_meow128_4_diff_length(cb, C.c_size_t(n), addr(cb, n), C.c_size_t(m - n), addr(cb, m),
+                                          C.c_size_t(o - m), addr(cb, o), C.c_size_t(128 - o), x)
+        d[t] = list(x)
+    tr = np.array(trip, dtype=np.int64)
+    want = np.concatenate([h[idx[0, tr[:, 0]]], h[idx[tr[:, 0], tr[:, 1]]], h[idx[tr[:, 1], tr[:, 2]]],
+                           h[idx[tr[:, 2], 128]]], axis=1)
+    assert np.array_equal(d, want), "reference 4-diff != single hashes"
+    np.savez_compressed(os.path.join(HERE, "partition4.npz"), sub=sub, out=h, ntrip=np.array([len(trip)]),
+                        digest4=np.array([partition_digest(d)], dtype=np.uint64))
+    print("partition4.npz:", len(subs), "substrings,", len(trip), "triples")
+
+
 if __name__ == "__main__":
     only = [a for a in sys.argv[1:] if a.startswith("--only-")]
     if not only:
@@ -402,3 +451,5 @@ if __name__ == "__main__":
         make_ingest()
     if not only or "--only-sort" in only:
         make_sort()
+    if not only or "--only-partition4" in only:
+        make_partition4()

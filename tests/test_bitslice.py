@@ -5,8 +5,9 @@ checks every circuit bit-exactly against a direct AESDEC before writing), and
 the bitsliced Meow chain, run on the host with the gfx950 primitives emulated
 (tests/cpp/bs_host_test.cpp), equals the oracle's kv_hash_meow128
 (key_hash.c:1413-1429) for 16/32/48-byte keys under random and edge seeds.
-GPU: the hybrid kernel (T-table + bitsliced waves, kvh_set_tuning knob 11)
-is bit-exact against the oracle, tails included.
+The hybrid kernel that runs this chain beside the T-table waves (+1-2 % on
+C1) lost its A/B and lives only in the experiments build
+(tools/libkvh_exp.so); tools/check_hybrid.py checks it on a GPU.
 """
 import os
 import subprocess
@@ -34,25 +35,3 @@ def test_bitsliced_chain_matches_oracle_on_host():
     r = subprocess.run([exe, "48"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("bs_host_test ok 1152")
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("n", [512, 1000, 4099, 1 << 20])
-@pytest.mark.parametrize("share", [200, 1000])
-def test_hybrid_kernel_bit_exact(n, share):
-    import torch
-    import raikv_amd as kvh
-    from oracle_lib import load_oracle, orc_fixed
-    orc = load_oracle()
-    rng = np.random.default_rng(n + share)
-    kb = rng.integers(0, 256, n * 16, dtype=np.uint8)
-    seed = (int(rng.integers(0, 2**63)), int(rng.integers(0, 2**63)))
-    dk = torch.from_numpy(kb).cuda()
-    prev = kvh.lib.kvh_set_tuning(11, share)
-    try:
-        for fix in (False, True):
-            got = kvh.meow128_fixed(dk, 16, seed, fixup=fix)
-            torch.cuda.synchronize()
-            np.testing.assert_array_equal(got.cpu().numpy().view(np.uint64), orc_fixed(orc, kb, 16, seed, fixup=fix))
-    finally:
-        kvh.lib.kvh_set_tuning(11, prev)

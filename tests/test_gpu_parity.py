@@ -331,3 +331,71 @@ def test_cpp_paths_program(kvh):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def _digest(d: np.ndarray) -> int:
+    """tests/golden/make_golden.py partition_digest: sum w_i * (2i + 1) mod 2^64."""
+    w = d.reshape(-1).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        return int(np.sum(w * (2 * np.arange(w.size, dtype=np.uint64) + np.uint64(1)), dtype=np.uint64))
+
+
+@pytest.mark.parametrize("variant", [13, 7, 0])
+def test_partition_vectors_against_reference(kvh, variant):
+    """hash_test.cpp:404-442 on the device, pinned to the REFERENCE's outputs
+    (tests/golden/partition2.npz, partition4.npz; make_golden.py): bytes
+    0..127 cut at every n (part2) and at every n <= m <= o < 128 (part4,
+    357,760 cuts).  Every piece is a substring buf[a:b]; all 8385 substrings
+    are hashed by the device kernels and must equal the reference's
+    kv_hash_meow128; the part4 cuts composed from them must reproduce the
+    digest of the reference's own kv_hash_meow128_4_diff_length outputs."""
+    seed = (10101, 20202)
+    buf = np.arange(128, dtype=np.uint8)
+    p2 = golden("partition2.npz")["out"]
+    g4 = golden("partition4.npz")
+    sub, want = g4["sub"].astype(np.int64), g4["out"]
+    lens = sub[:, 1] - sub[:, 0]
+    offs = np.zeros(len(sub) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    flat = np.concatenate([buf[a:b] for a, b in sub])
+    prev = kvh.lib.kvh_set_tuning(7, variant)
+    try:
+        h = u64(kvh.meow128_var(dev(flat), dev_u64(offs), seed))
+        # part2 as 258 keys in cut order
+        k2 = [buf[:n] if j == 0 else buf[n:] for n in range(129) for j in (0, 1)]
+        o2 = np.zeros(259, dtype=np.uint64)
+        o2[1:] = np.cumsum([len(k) for k in k2])
+        h2 = u64(kvh.meow128_var(dev(np.concatenate(k2)), dev_u64(o2), seed))
+    finally:
+        kvh.lib.kvh_set_tuning(7, prev)
+    np.testing.assert_array_equal(h, want)
+    np.testing.assert_array_equal(h2.reshape(129, 4), p2)
+    if variant != 13:
+        return
+    # the other device paths over the same substrings: straight-line kernel,
+    # (offset, length) spans, and the synchronous drop-ins
+    sd = dev_u64(np.tile(np.array(seed, dtype=np.uint64), (len(sub), 1)))
+    np.testing.assert_array_equal(u64(kvh.meow128_var_seeded(dev(flat), dev_u64(offs), sd)), want)
+    sp = kvh.meow128_spans(dev(buf), dev_u64(sub[:, 0].astype(np.uint64)),
+                           torch.from_numpy(lens.astype(np.int32)).cuda(), seed, fixup=False, nulterm=False)
+    np.testing.assert_array_equal(u64(sp), want)
+    idx = np.full((129, 129), -1, dtype=np.int64)
+    idx[sub[:, 0], sub[:, 1]] = np.arange(len(sub))
+    tr = np.array([(n, m, o) for n in range(128) for m in range(n, 128) for o in range(m, 128)], dtype=np.int64)
+    assert len(tr) == int(g4["ntrip"][0])
+    d = np.concatenate([h[idx[0, tr[:, 0]]], h[idx[tr[:, 0], tr[:, 1]]], h[idx[tr[:, 1], tr[:, 2]]],
+                        h[idx[tr[:, 2], 128]]], axis=1)
+    assert _digest(d) == int(g4["digest4"][0])
+    cb = C.create_string_buffer(buf.tobytes(), 128)
+    base = C.addressof(cb)
+    lib = kvh.lib
+    for n in range(129):
+        x = (C.c_uint64 * 4)(*seed, *seed)
+        assert lib.kvh_hash_meow128_2_diff_length(cb, n, C.c_void_p(base + n), 128 - n, x) == 0
+        assert list(x) == [int(v) for v in p2[n]], n
+    for t in np.random.default_rng(9).choice(len(tr), 200, replace=False):
+        n, m, o = (int(v) for v in tr[t])
+        x = (C.c_uint64 * 8)(*(seed * 4))
+        assert lib.kvh_hash_meow128_4_diff_length(cb, n, C.c_void_p(base + n), m - n, C.c_void_p(base + m), o - m,
+                                                  C.c_void_p(base + o), 128 - o, x) == 0
+        assert list(x) == [int(v) for v in d[t]], (n, m, o)

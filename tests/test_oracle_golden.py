@@ -71,6 +71,15 @@ def test_partition2():
         assert (a + b) == tuple(int(v) for v in out[n])
 
 
+def test_partition4_substrings():
+    """partition4.npz (the reference's kv_hash_meow128 of every substring of
+    bytes 0..127, hash_test.cpp:418-442) against the oracle."""
+    g = golden("partition4.npz")
+    buf = bytes(range(128))
+    for (a, b), h in zip(g["sub"], g["out"]):
+        assert orc_meow(ORC, buf[a:b], 10101, 20202) == (int(h[0]), int(h[1])), (a, b)
+
+
 def test_variants_and_streaming():
     r = VEC["variants"]["results"]
     keys = [k.encode() for k in VEC["variants"]["keys"]]

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Ablation of the fixed-length kernel (kvh_set_tuning(5, mode)): product,
 copy-only, no-load, no-store; interleaved rounds in one process."""
+import os as _os  # research knobs live in the experiments build (make experiments)
+_os.environ.setdefault("KVH_LIB", _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "libkvh_exp.so"))
 import json, os, sys
 import numpy as np
 import torch

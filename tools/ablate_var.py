@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
 """Ablation of k_var3 (KPT=4) on config C2: product / no-hash / no-gather / no-sort."""
+import os as _os  # research knobs live in the experiments build (make experiments)
+_os.environ.setdefault("KVH_LIB", _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "libkvh_exp.so"))
 import json, os, sys
 import numpy as np
 import torch

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase wave cycles of k_var5 (stamped diagnostic build) on config C2."""
+import os as _os  # research knobs live in the experiments build (make experiments)
+_os.environ.setdefault("KVH_LIB", _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "libkvh_exp.so"))
 import ctypes as C, json, os, sys
 import numpy as np
 import torch

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """A/B the fixed-length kernel variants in ONE process, interleaved rounds
 (guide §5.4 rule 24).  Prints per-variant median/min kernel ms and GB/s."""
+import os as _os  # research knobs live in the experiments build (make experiments)
+_os.environ.setdefault("KVH_LIB", _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "libkvh_exp.so"))
 import argparse
 import itertools
 import json
