@@ -12,7 +12,7 @@ HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/
             raikv_amd/csrc/ht_pos.hpp raikv_amd/csrc/bs_prelude.hpp raikv_amd/csrc/bs_aes.hpp \
             raikv_amd/csrc/bs_meow.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
-CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/paths_gpu
+CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/paths_gpu tools/copy_peak
 
 all: $(LIB) oracle cpptests
 
@@ -57,6 +57,10 @@ tests/cpp/e2e_host: tests/cpp/e2e_host.cpp $(LIB) include/kvh.h
 	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
 	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
+
+# measurement: the box's achievable streaming rate for bench.py's roofline
+tools/copy_peak: tools/copy_peak.hip
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
 # TEST ONLY: the bitsliced Meow chain run on the host against the oracle
 tests/cpp/bs_host_test: tests/cpp/bs_host_test.cpp raikv_amd/csrc/bs_aes.hpp raikv_amd/csrc/bs_meow.hpp oracle

@@ -81,43 +81,118 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cpu_threads():
+    """Host threads for the all-core CPU leg: the CPUs this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when the box sets it (the
+    GPU box gives one GPU's job 16 CPUs and exports OMP_NUM_THREADS=16)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    t = int(env) if env.isdigit() and int(env) > 0 else aff
+    return max(1, min(t, aff)), aff
+
+
+def host_model():
+    try:
+        return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:
+        return "unknown"
+
+
+def c0_hash_test():
+    """Config C0: the reference's own test/hash_test.cpp (compiled from its
+    sources by oracle/Makefile into oracle/_ref/hash_test), `hash_test int
+    meow 16`, one host thread; its 1,048,576-key line (10M timed calls, seeds
+    (0,0), hash_test.cpp:730-760)."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "hash_test")
+    if not os.path.exists(exe):
+        return {"value": None, "error": "oracle/_ref/hash_test not built"}
+    r = subprocess.run([exe, "int", "meow", "16"], capture_output=True, text=True, timeout=120)
+    line = [l for l in r.stdout.splitlines() if l.startswith("1048576 keys")]
+    if r.returncode != 0 or not line:
+        return {"value": None, "error": f"rc={r.returncode}", "tail": r.stdout[-300:]}
+    ns = float(line[-1].split("hash =")[1].split("ns")[0])
+    return {"value": 1e9 / ns, "unit": "hash/s", "ns_per_hash": ns, "cores": 1, "kind": "reference",
+            "line": line[-1].strip(), "cmd": "oracle/_ref/hash_test int meow 16 (1M IntContent keys, 10M calls)"}
+
+
 def cpu_baseline(cfg, seed, seconds: float):
-    """Reference kv_hash_meow128 on host threads over a bounded sample."""
+    """The reference CPU path (oracle/_ref/libkvref.so: the unmodified
+    src/key_hash.c) on this box's host cores, on a bounded sample of the same
+    workload shape: all available threads (value) and one thread; plus the C0
+    hash_test line."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import load_ref, load_oracle  # test infrastructure: the checker only
+    from raikv_amd.workload import C3_SEEDS, zipf_lengths, offsets_from_lengths
     import ctypes as C
-    threads = max(1, min(16, os.cpu_count() or 1))
-    L = cfg["key_len"] or 16
-    n = 8_000_000
+    threads, aff = cpu_threads()
     rng = np.random.default_rng(42)
-    keys = rng.integers(0, 256, n * L, dtype=np.uint8)
-    out = np.zeros(2 * n, dtype=np.uint64)
+    arity = cfg["arity"]
+    if cfg["var"]:
+        n = 4_000_000
+        offs = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=42))
+        keys = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+        shape = f"{n} zipf 8-256 B keys ({int(offs[-1]) / n:.1f} B mean) + u64 offsets"
+        L = 0
+    else:
+        L = cfg["key_len"]
+        n = 8_000_000 if arity == 1 else 2_000_000
+        keys = rng.integers(0, 256, n * L, dtype=np.uint8)
+        shape = f"{n} packed {L}-byte keys" + (f" x {arity} seeds" if arity > 1 else "")
+    out = np.zeros(2 * n * arity, dtype=np.uint64)
+    seeds4 = np.array(C3_SEEDS, dtype=np.uint64).reshape(-1)
     ref = load_ref()
     if ref is not None:
         kind = "reference"
-        run = lambda: ref.ref_bench_fixed(keys.ctypes.data, L, n, C.c_uint64(seed[0]), C.c_uint64(seed[1]),
-                                          out.ctypes.data, threads)
+        ref.ref_bench_var.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
+        ref.ref_bench_var.restype = C.c_double
+        ref.ref_bench_4seed.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p, C.c_void_p, C.c_int]
+        ref.ref_bench_4seed.restype = C.c_double
+        what = ("kv_hash_meow128_4_same_length_4_seed (key in all 4 slots)" if arity == 4 else "kv_hash_meow128")
+
+        def run(t):
+            if cfg["var"]:
+                return ref.ref_bench_var(keys.ctypes.data, offs.ctypes.data, n, C.c_uint64(seed[0]),
+                                         C.c_uint64(seed[1]), out.ctypes.data, t)
+            if arity == 4:
+                return ref.ref_bench_4seed(keys.ctypes.data, L, n, seeds4.ctypes.data, out.ctypes.data, t)
+            return ref.ref_bench_fixed(keys.ctypes.data, L, n, C.c_uint64(seed[0]), C.c_uint64(seed[1]),
+                                       out.ctypes.data, t)
     else:  # clean-room port (single thread, scalar C)
-        kind = "port"
-        threads = 1
+        kind, threads, what = "port", 1, "oracle port of kv_hash_meow128"
         orc = load_oracle()
 
-        def run():
-            t = time.perf_counter()
-            orc.orc_batch_fixed(keys.ctypes.data, L, n, C.c_uint64(seed[0]), C.c_uint64(seed[1]),
-                                out.ctypes.data, 0)
-            return time.perf_counter() - t
-    total_t, total_n = 0.0, 0
-    while total_t < seconds:
-        total_t += float(run())
-        total_n += n
-    try:
-        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
-    except Exception:
-        model = "unknown"
-    return {"value": total_n / total_t, "unit": "hash/s", "cores": threads, "kind": kind,
-            "sample": f"{total_n} packed {L}-byte keys ({n} distinct, {total_n // n} passes) x "
-                      f"kv_hash_meow128 (src/key_hash.c), {threads} threads on {model}, {total_t:.1f} s"}
+        def run(t):
+            t0 = time.perf_counter()
+            if cfg["var"]:
+                orc.orc_batch_var(keys.ctypes.data, offs.ctypes.data, n, C.c_uint64(seed[0]), C.c_uint64(seed[1]),
+                                  out.ctypes.data, 0)
+            else:
+                orc.orc_batch_fixed(keys.ctypes.data, L, n, C.c_uint64(seed[0]), C.c_uint64(seed[1]),
+                                    out.ctypes.data, 0)
+            return time.perf_counter() - t0
+
+    def timed(t, budget):
+        tt, nn = 0.0, 0
+        while tt < budget:
+            tt += float(run(t))
+            nn += n
+        return nn * arity / tt, nn, tt
+
+    v, nn, tt = timed(threads, seconds * 0.6)
+    res = {"value": v, "unit": "hash/s", "cores": threads, "kind": kind,
+           "sample": f"{nn} keys ({shape}, {nn // n} passes) x {what} (src/key_hash.c), "
+                     f"{threads} threads on {host_model()}, {tt:.1f} s",
+           "cores_available": aff}
+    if threads > 1:
+        v1, nn1, tt1 = timed(1, seconds * 0.4)
+        res["one_thread"] = {"value": v1, "unit": "hash/s", "cores": 1, "sample": f"{nn1} keys, {tt1:.1f} s"}
+    if not cfg["var"] and arity == 1 and L == 16:
+        res["c0_hash_test"] = c0_hash_test()
+    return res
 
 
 def cpu_baseline_positions(cfg, seed, seconds: float, geom):
@@ -128,7 +203,7 @@ def cpu_baseline_positions(cfg, seed, seconds: float, geom):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_lib import load_ref_ht, load_oracle, orc_geom, orc_positions  # checker only
     import ctypes as C
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, _aff = cpu_threads()
     L, n = cfg["key_len"], 4_000_000
     rng = np.random.default_rng(42)
     keys = rng.integers(0, 256, n * L, dtype=np.uint8)
@@ -203,7 +278,7 @@ def cpu_baseline_crc(cfg, seconds: float):
     if ref is None:
         return {"value": None, "error": "oracle/_ref/libkvref.so not built"}
     ref.kv_crc_c_array.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, _aff = cpu_threads()
     n = 2_000_000
     L = cfg["key_len"]
     lens = zipf_lengths(n, 8, 256, seed=3) if cfg["var"] else np.full(n, L, np.int64)
@@ -301,8 +376,16 @@ def main():
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--e2e", action="store_true", help="also time the PCIe-inclusive host pipeline")
+    ap.add_argument("--e2e", dest="e2e", action="store_true", default=None,
+                    help="time the PCIe-inclusive host pipeline (default: on for c1/c2 at N=1)")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false")
+    ap.add_argument("--settle-ms", type=float, default=500.0,
+                    help="untimed launches before the warmup, until the engine clock has left its post-idle "
+                         "power transient (DESIGN.md §4.5); 0 disables")
+    ap.add_argument("--no-copy-peak", action="store_true", help="skip the achievable-peak copy probe")
     args = ap.parse_args()
+    if args.e2e is None:
+        args.e2e = args.config in ("c1", "c2")
 
     import torch
 
@@ -412,6 +495,14 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
+    # settle: a GPU leaving idle boosts, then its power controller overshoots
+    # (engine clock 2.1 -> 1.4 GHz by launch 6) and recovers over ~100 launches
+    # (profiles/r02/driver_protocol/); steady-state throughput is the metric
+    settle_n, t_s = 0, time.perf_counter()
+    while (time.perf_counter() - t_s) * 1e3 < args.settle_ms:
+        run(out)
+        torch.cuda.synchronize()
+        settle_n += 1
     for _ in range(args.warmup):
         run(out)
     torch.cuda.synchronize()
@@ -460,10 +551,17 @@ def main():
                      "traffic": traffic,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
                      "traffic_source": tsrc},
+        "settle": {"ms": args.settle_ms, "launches": settle_n},
         "hashes_per_s_per_gpu": n * arity / (kern_ms * 1e-3),
         "lds_roofline": lds_line(args.config, units, kern_ms),
     }
-    if args.e2e and rank == 0:
+    if rank == 0 and world == 1 and not args.no_copy_peak:
+        cp = copy_peak(alg_bytes)
+        if cp.get("copy_GBps"):
+            res["roofline"]["achievable_peak"] = cp["copy_GBps"]
+            res["roofline"]["frac_vs_achievable"] = achieved / cp["copy_GBps"]
+        res["roofline"]["achievable_source"] = cp
+    if args.e2e and rank == 0 and world == 1:
         res["e2e_pcie"] = e2e(kvh, cfg, seed)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -485,36 +583,79 @@ def main():
         print(json.dumps(res), flush=True)
 
 
+def copy_peak(alg_bytes):
+    """The box's achievable streaming rate for this traffic (tools/copy_peak:
+    16 B read + 16 B written per item, k_fixed's wave-chunked non-temporal
+    access pattern, same byte count, after the same settle), run as a child
+    process after the timed region."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "copy_peak")
+    if not os.path.exists(exe):
+        return {"error": "tools/copy_peak not built"}
+    try:
+        r = subprocess.run([exe, str(max(1, int(alg_bytes) // 32)), "500", "50"], capture_output=True, text=True,
+                           timeout=120)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as ex:  # reported, never hidden
+        return {"error": repr(ex)[:200]}
+
+
 def e2e(kvh, cfg, seed):
-    """PCIe-inclusive host pipeline: pinned host keys -> H2D -> kernel -> D2H
-    -> pinned host hashes (kvh_meow128_fixed_host).  Measured twice: from a
-    C++ host on the system HIP runtime (tests/cpp/e2e_host, how raikv's C/C++
-    calls the C-ABI; this is the number DESIGN.md quotes), and in this Python
-    process, which runs torch's bundled HIP runtime."""
+    """PCIe-inclusive host pipeline: pinned host keys (+ offsets) -> H2D ->
+    kernel -> D2H -> pinned host hashes (kvh_meow128_fixed_host for c1,
+    kvh_meow128_var_host for c2).  Measured from a C++ host on the system HIP
+    runtime (tests/cpp/e2e_host, how raikv's C/C++ calls the C-ABI; the
+    number DESIGN.md §4.4 quotes), in this Python process (torch's bundled
+    HIP runtime), and, when this process sees more than one GPU, through
+    kvh_meow128_*_host_multi over 2/4/8 of them (one host thread each)."""
     import subprocess
     import torch
-    L = cfg["key_len"] or 16
+    var = cfg["var"]
+    L = 0 if var else (cfg["key_len"] or 16)
     n = 50_000_000
-    res = {"keys": n, "key_len": L}
+    res = {"keys": n, "key_len": "zipf 8-256" if var else L}
     exe = os.path.join(ROOT, "tests", "cpp", "e2e_host")
-    try:
-        r = subprocess.run([exe, str(n), str(L), "5"], capture_output=True, text=True, timeout=300)
-        res["cpp_host"] = json.loads(r.stdout.strip().splitlines()[-1])
-    except Exception as ex:  # the figure is reported, not required
-        res["cpp_host"] = {"error": repr(ex)[:200]}
-    hk = kvh.host_empty((n * L,), np.uint8)
-    hk[:] = np.random.default_rng(7).integers(0, 256, n * L, dtype=np.uint8)
-    ho = kvh.host_empty((n, 2), np.uint64)
-    kvh.meow128_fixed_host(hk, L, seed, out=ho)
-    ref = kvh.meow128_fixed(torch.from_numpy(hk).cuda(), L, seed).cpu().numpy().view(np.uint64)
-    assert np.array_equal(ho, ref), "host pipeline differs from the device-resident kernel"
+
+    def cpp(devs=None):
+        try:
+            cmd = [exe, str(n), str(L), "5"] + ([",".join(map(str, devs))] if devs else [])
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            return json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception as ex:  # the figure is reported, not required
+            return {"error": repr(ex)[:200]}
+    res["cpp_host"] = cpp()
+    ndev = torch.cuda.device_count()
+    if ndev > 1:
+        res["cpp_host_multi"] = {str(k): cpp(list(range(k))) for k in (2, 4, 8) if k <= ndev}
+    rng = np.random.default_rng(7)
+    if var:
+        from raikv_amd.workload import zipf_lengths, offsets_from_lengths
+        offs = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=7))
+        hf = kvh.host_empty(offs.shape, np.uint64)
+        hf[:] = offs
+        hk = kvh.host_empty((int(offs[-1]),), np.uint8)
+        hk[:] = rng.integers(0, 256, hk.size, dtype=np.uint8)
+        ho = kvh.host_empty((n, 2), np.uint64)
+        call = lambda: kvh.meow128_var_host(hk, hf, seed, out=ho)
+        ref = kvh.meow128_var(torch.from_numpy(hk).cuda(), torch.from_numpy(offs.view(np.int64)).cuda(), seed)
+        moved = hk.size + 8 * (n + 1) + 16 * n
+    else:
+        hk = kvh.host_empty((n * L,), np.uint8)
+        hk[:] = rng.integers(0, 256, n * L, dtype=np.uint8)
+        ho = kvh.host_empty((n, 2), np.uint64)
+        call = lambda: kvh.meow128_fixed_host(hk, L, seed, out=ho)
+        ref = kvh.meow128_fixed(torch.from_numpy(hk).cuda(), L, seed)
+        moved = n * (L + 16)
+    call()
+    assert np.array_equal(ho, ref.cpu().numpy().view(np.uint64)), "host pipeline differs from the device kernel"
+    del ref
     ts = []
     for _ in range(5):
         t = time.perf_counter()
-        kvh.meow128_fixed_host(hk, L, seed, out=ho)
+        call()
         ts.append(time.perf_counter() - t)
     dt = float(np.median(ts))
-    res["python_torch_runtime"] = {"hash_per_s": n / dt, "GB_per_s_h2d_plus_d2h": n * (L + 16) / dt / 1e9}
+    res["python_torch_runtime"] = {"hash_per_s": n / dt, "GB_per_s_h2d_plus_d2h": moved / dt / 1e9}
     res["note"] = ("pinned host buffers (kvh_host_alloc), 16 MiB chunks, H2D / kernel / D2H on three streams; "
                    "median of 5 calls; outputs checked against the device kernel")
     return res

@@ -94,6 +94,41 @@ int kvh_meow128_var_seeded(const void *keys, const uint64_t *offsets,
 int kvh_meow128_fixed_host(const void *keys, uint32_t key_len, size_t n,
                            uint64_t seed1, uint64_t seed2, uint64_t *out,
                            uint32_t flags);
+/* Variable-length keys in host memory (socket / shm-segment keys: EvKeyCtx
+ * key buffers, include/raikv/ev_key.h:83-114; ctest's frag stream,
+ * test/ctest.c:202-233): key i = keys[offsets[i] .. offsets[i+1]), n+1 host
+ * u64 offsets (offsets[0] need not be 0).  Chunks of at most 16 MiB of key
+ * bytes (knob 15; a longer key is a chunk of its own), offsets and hashes
+ * DMA'd with them; out[2n] receives the hashes (global layout).  Same
+ * result as kvh_meow128_var on device copies of the buffers. */
+int kvh_meow128_var_host(const void *keys, const uint64_t *offsets, size_t n,
+                         uint64_t seed1, uint64_t seed2, uint64_t *out,
+                         uint32_t flags);
+/* The two above sharded over ndev GPUs of this process, one host thread
+ * per entry of devices[] (a device may be listed more than once): equal
+ * index ranges (fixed) or ranges of equal key bytes (variable), each
+ * device writing its disjoint slice of out.  Keys are independent: no
+ * device-to-device traffic (the one-process shape of raikv's threads,
+ * test/test.cpp:682, test/ctest.c:395).  Synchronous; 0 or the first
+ * error of any shard. */
+int kvh_meow128_fixed_host_multi(const void *keys, uint32_t key_len, size_t n,
+                                 uint64_t seed1, uint64_t seed2, uint64_t *out,
+                                 uint32_t flags, const int *devices, int ndev);
+int kvh_meow128_var_host_multi(const void *keys, const uint64_t *offsets,
+                               size_t n, uint64_t seed1, uint64_t seed2,
+                               uint64_t *out, uint32_t flags,
+                               const int *devices, int ndev);
+/* The shard arithmetic of the _multi entries (host only, no device call):
+ * bounds[0..nshards], shard d = keys [bounds[d], bounds[d+1]).  offsets ==
+ * NULL: equal index ranges; else n+1 offsets and ranges of equal key bytes
+ * (each shard starts at the first key whose offset is >= offsets[0] +
+ * total * d / nshards).  For callers that drive their own devices. */
+int kvh_shard_bounds(const uint64_t *offsets, size_t n, int nshards,
+                     size_t *bounds);
+/* Page-lock an existing host range (e.g. raikv's shared-memory segment,
+ * include/raikv/shm_ht.h:23-29) so the pipelines above DMA it directly. */
+int kvh_host_register(void *p, size_t bytes);
+int kvh_host_unregister(void *p);
 /* pinned (page-locked, DMA-able) host memory for kvh_meow128_fixed_host's
  * key and hash buffers -- the role of raikv's shared-memory segment on the
  * GPU side; 0 or a negative error.  Free with kvh_host_free. */

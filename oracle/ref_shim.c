@@ -56,27 +56,41 @@ void ref_batch_4seed(const uint8_t *keys, size_t len, size_t n,
   }
 }
 
-/* ---- multi-threaded CPU baseline over packed fixed-length keys ---- */
+/* ---- multi-threaded CPU baselines (the reference's own entry points) ----
+ * kind 0: packed fixed-length keys, kv_hash_meow128 per key;
+ * kind 1: packed keys + u64 offsets (C2 shape), kv_hash_meow128 per key;
+ * kind 2: packed fixed-length keys, kv_hash_meow128_4_same_length_4_seed
+ *         with the key in all four slots (C3 shape), out 8 words per key. */
 typedef struct {
-  const uint8_t *keys; size_t len, lo, hi; uint64_t s1, s2; uint64_t *out;
+  int kind;
+  const uint8_t *keys; const uint64_t *offs; size_t len, lo, hi;
+  uint64_t s1, s2; const uint64_t *seeds; uint64_t *out;
 } ref_job;
 
 static void *ref_worker(void *arg)
 {
   ref_job *j = (ref_job *)arg;
   for (size_t i = j->lo; i < j->hi; i++) {
+    if (j->kind == 2) {
+      uint64_t *x = j->out + 8 * i;
+      const uint8_t *p = j->keys + i * j->len;
+      memcpy(x, j->seeds, 8 * sizeof(uint64_t));
+      kv_hash_meow128_4_same_length_4_seed(p, p, p, p, j->len, x);
+      continue;
+    }
     uint64_t h1 = j->s1, h2 = j->s2;
-    kv_hash_meow128(j->keys + i * j->len, j->len, &h1, &h2);
+    if (j->kind == 1)
+      kv_hash_meow128(j->keys + j->offs[i], (size_t)(j->offs[i + 1] - j->offs[i]), &h1, &h2);
+    else
+      kv_hash_meow128(j->keys + i * j->len, j->len, &h1, &h2);
     j->out[2 * i] = h1;
     j->out[2 * i + 1] = h2;
   }
   return NULL;
 }
 
-/* returns elapsed seconds (monotonic) for hashing n keys on `threads`
- * POSIX threads */
-double ref_bench_fixed(const uint8_t *keys, size_t len, size_t n, uint64_t s1,
-                       uint64_t s2, uint64_t *out, int threads)
+static double ref_bench(int kind, const uint8_t *keys, const uint64_t *offs, size_t len, size_t n,
+                        uint64_t s1, uint64_t s2, const uint64_t *seeds, uint64_t *out, int threads)
 {
   if (threads < 1) threads = 1;
   if (threads > 256) threads = 256;
@@ -85,8 +99,8 @@ double ref_bench_fixed(const uint8_t *keys, size_t len, size_t n, uint64_t s1,
   struct timespec a, b;
   clock_gettime(CLOCK_MONOTONIC, &a);
   for (int t = 0; t < threads; t++) {
-    job[t].keys = keys; job[t].len = len; job[t].s1 = s1; job[t].s2 = s2;
-    job[t].out = out;
+    job[t].kind = kind; job[t].keys = keys; job[t].offs = offs; job[t].len = len;
+    job[t].s1 = s1; job[t].s2 = s2; job[t].seeds = seeds; job[t].out = out;
     job[t].lo = n * (size_t)t / (size_t)threads;
     job[t].hi = n * (size_t)(t + 1) / (size_t)threads;
     pthread_create(&tid[t], NULL, ref_worker, &job[t]);
@@ -94,6 +108,26 @@ double ref_bench_fixed(const uint8_t *keys, size_t len, size_t n, uint64_t s1,
   for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
   clock_gettime(CLOCK_MONOTONIC, &b);
   return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+/* returns elapsed seconds (monotonic) for hashing n keys on `threads`
+ * POSIX threads */
+double ref_bench_fixed(const uint8_t *keys, size_t len, size_t n, uint64_t s1,
+                       uint64_t s2, uint64_t *out, int threads)
+{
+  return ref_bench(0, keys, NULL, len, n, s1, s2, NULL, out, threads);
+}
+
+double ref_bench_var(const uint8_t *keys, const uint64_t *offs, size_t n, uint64_t s1,
+                     uint64_t s2, uint64_t *out, int threads)
+{
+  return ref_bench(1, keys, offs, 0, n, s1, s2, NULL, out, threads);
+}
+
+double ref_bench_4seed(const uint8_t *keys, size_t len, size_t n, const uint64_t *seeds,
+                       uint64_t *out, int threads)
+{
+  return ref_bench(2, keys, NULL, len, n, 0, 0, seeds, out, threads);
 }
 
 /* hash_test "int meow <keylen>" protocol (test/hash_test.cpp:447-460,

@@ -33,6 +33,9 @@ from .binding import (  # noqa: F401
     meow128_multiseed,
     meow128_var_seeded,
     meow128_fixed_host,
+    meow128_var_host,
+    meow128_host_multi,
+    shard_bounds,
     host_empty,
     kv_hash_meow128,
     kv_hash_meow64,
@@ -43,7 +46,7 @@ from .workload import STATIC_SEED  # noqa: F401
 
 __all__ = [
     "KVH_FIXUP", "KvhError", "lib", "lib_path", "meow128_fixed", "meow128_var",
-    "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "host_empty", "kv_hash_meow128",
+    "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "meow128_var_host", "meow128_host_multi", "shard_bounds", "host_empty", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
     "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
     "tokenize", "tokenize_hash", "frag_offsets", "frags_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP",

@@ -80,6 +80,12 @@ def _load():
         "kvh_meow128_batch": (I, [P, P, U32, SZ, P, U32, P, U32, P]),
         "kvh_meow128_var_seeded": (I, [P, P, SZ, P, P, U32, P]),
         "kvh_meow128_fixed_host": (I, [P, U32, SZ, U64, U64, P, U32]),
+        "kvh_meow128_var_host": (I, [P, P, SZ, U64, U64, P, U32]),
+        "kvh_meow128_fixed_host_multi": (I, [P, U32, SZ, U64, U64, P, U32, P, I]),
+        "kvh_meow128_var_host_multi": (I, [P, P, SZ, U64, U64, P, U32, P, I]),
+        "kvh_host_register": (I, [P, SZ]),
+        "kvh_shard_bounds": (I, [P, SZ, I, P]),
+        "kvh_host_unregister": (I, [P]),
         "kvh_host_alloc": (I, [C.POINTER(P), SZ]),
         "kvh_host_free": (I, [P]),
         "kvh_device_alloc": (I, [C.POINTER(P), SZ]),
@@ -416,6 +422,55 @@ def meow128_fixed_host(keys: np.ndarray, key_len: int, seed: Tuple[int, int],
                                      out.ctypes.data, KVH_FIXUP if fixup else 0),
           "kvh_meow128_fixed_host")
     return out
+
+
+def meow128_var_host(keys: np.ndarray, offsets: np.ndarray, seed: Tuple[int, int],
+                     out: Optional[np.ndarray] = None, fixup: bool = False) -> np.ndarray:
+    """Host keys + host u64 offsets [n+1] -> host hashes [n, 2] through the
+    byte-budgeted H2D/kernel/D2H pipeline (kvh_meow128_var_host)."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    if out is None:
+        out = np.empty((n, 2), dtype=np.uint64)
+    kb = keys if keys.size else np.zeros(1, np.uint8)
+    check(lib.kvh_meow128_var_host(kb.ctypes.data, offsets.ctypes.data, n, U64(seed[0]), U64(seed[1]),
+                                   out.ctypes.data, KVH_FIXUP if fixup else 0), "kvh_meow128_var_host")
+    return out
+
+
+def meow128_host_multi(keys: np.ndarray, seed: Tuple[int, int], devices: Sequence[int], key_len: int = 0,
+                       offsets: Optional[np.ndarray] = None, out: Optional[np.ndarray] = None,
+                       fixup: bool = False) -> np.ndarray:
+    """One host batch sharded over `devices` (one host thread each):
+    kvh_meow128_fixed_host_multi (key_len) or kvh_meow128_var_host_multi
+    (offsets)."""
+    dv = (C.c_int * len(devices))(*devices)
+    fl = KVH_FIXUP if fixup else 0
+    kb = keys if keys.size else np.zeros(1, np.uint8)
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        out = np.empty((n, 2), dtype=np.uint64) if out is None else out
+        check(lib.kvh_meow128_var_host_multi(kb.ctypes.data, offsets.ctypes.data, n, U64(seed[0]), U64(seed[1]),
+                                             out.ctypes.data, fl, dv, len(devices)), "kvh_meow128_var_host_multi")
+    else:
+        n = keys.size // key_len
+        out = np.empty((n, 2), dtype=np.uint64) if out is None else out
+        check(lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, key_len, n, U64(seed[0]), U64(seed[1]),
+                                               out.ctypes.data, fl, dv, len(devices)),
+              "kvh_meow128_fixed_host_multi")
+    return out
+
+
+def shard_bounds(n: int, nshards: int, offsets: Optional[np.ndarray] = None) -> np.ndarray:
+    """kvh_shard_bounds: the shard arithmetic of the _host_multi entries."""
+    b = np.zeros(nshards + 1, dtype=np.uint64)
+    op = None
+    if offsets is not None:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        op = offsets.ctypes.data
+    check(lib.kvh_shard_bounds(op, n, nshards, b.ctypes.data), "kvh_shard_bounds")
+    return b
 
 
 def host_empty(shape, dtype=np.uint8) -> np.ndarray:

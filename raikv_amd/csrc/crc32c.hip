@@ -265,6 +265,22 @@ __device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, u
 // go through the wave's LDS slice back to input order and leave as one
 // contiguous run.  NW waves per workgroup: the 128 KiB of replicated tables
 // leave room for NW * 3 KiB of window state.
+template <int R>
+__device__ __attribute__((noinline)) void crc_wide_window(const uint8_t* __restrict__ keys,
+                                                          const uint64_t* __restrict__ offs, uint64_t i0, uint32_t k,
+                                                          int nchunks, const uint32_t* seeds, uint32_t seed,
+                                                          uint32_t* out, const uint32_t* lds) {
+  const CrcLdsT<R> T(lds);
+  const uint32_t lane = threadIdx.x & 63;
+  for (int c = 0; c < nchunks; c++) {
+    const uint32_t j = 64 * c + lane;
+    if (j < k) {
+      const uint64_t a = offs[i0 + j], e = offs[i0 + j + 1];
+      out[i0 + j] = crc_key_pf(keys + a, e - a, seeds ? seeds[i0 + j] : seed, T);
+    }
+  }
+}
+
 template <int WIN, int NW, int SH = 0, int R = 32>
 __global__ void __launch_bounds__(NW * 64)
 k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
@@ -285,20 +301,18 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
   for (uint64_t w = (uint64_t)blockIdx.x * NW + wv; w < nwin; w += (uint64_t)gridDim.x * NW) {
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
-    if (offs[i0 + k] - offs[i0] >= (1ull << 32)) {
+    const WinOffs<WIN> W = win_load<WIN>(offs, i0, k);
+    bool wide = false;
+#pragma unroll
+    for (int m = 0; m < M; m++) wide |= W.e[m] - W.ws >= (1ull << 32);
+    if (__ballot(wide)) {
       // a window spanning 4 GiB or more: its records would hold u32 window
-      // offsets, so it runs in input order with u64 offsets (wave-uniform)
-#pragma unroll 1
-      for (int c = 0; c < M; c++) {
-        const uint32_t j = 64 * c + lane;
-        if (j < k) {
-          const uint64_t a = offs[i0 + j], e = offs[i0 + j + 1];
-          out[i0 + j] = crc_key_pf(keys + a, e - a, seeds ? seeds[i0 + j] : seed, T);
-        }
-      }
+      // offsets, so it runs in input order with u64 offsets (wave-uniform;
+      // out of line, off the hot path's register allocation)
+      crc_wide_window<R>(keys, offs, i0, k, M, seeds, seed, out, lds);
       continue;
     }
-    const uint64_t ws = wave_sort_window<WIN, SH>(offs, i0, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
+    const uint64_t ws = wave_sort_from<WIN, SH>(W, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
     // (running the lane's M keys as interleaved chains was slower: each
     // lane then steps as long as its longest key, chunk M-1's)
     uint32_t crc[M], ix[M];

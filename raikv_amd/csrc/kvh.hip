@@ -888,6 +888,29 @@ k_var5(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 // no longer stalls the whole workgroup (k_var5's 33 % barrier time).  Keys
 // are gathered from global memory (the window's ~12 KiB stay L2-hot across
 // its chunks); hashes are stored to their original slots.
+// The keys [i0, i0 + k) of a window whose bytes span 4 GiB or more, hashed
+// in input order with u64 offsets and lengths (k_var6 / k_var7 keep u32
+// window-relative records).  Out of line and without the LDS constant
+// records (every key of such a window is folded in-lane): the hot kernels'
+// register allocation does not see it.
+template <int NT>
+__device__ __attribute__((noinline)) void wide_window(const uint8_t* __restrict__ keys,
+                                                      const uint64_t* __restrict__ offs, uint64_t i0, uint32_t k,
+                                                      int nchunks, uint64_t s1, uint64_t s2,
+                                                      uint64_t* __restrict__ out, bool fix, const uint32_t* lds) {
+  const LdsTab<NT> T(lds);
+  const uint32_t lane = threadIdx.x & 63;
+  for (int c = 0; c < nchunks; c++) {
+    const uint32_t j = 64 * c + lane;
+    if (j < k) {
+      const uint64_t a = offs[i0 + j], len = offs[i0 + j + 1] - a;
+      const MeowConst K = make_const(s1, s2, len, T);
+      const RegK R{K};
+      store_h(out, i0 + j, meow_rt(keys + a, len, R, T), fix);
+    }
+  }
+}
+
 template <int WIN, int NW = kBlock / 64>
 struct Var6Cfg {
   static constexpr int kWaves = NW;
@@ -945,67 +968,63 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
     const uint64_t ws = offs[i0];
-    if (offs[i0 + k] - ws >= (1ull << 32)) {
-      // A window spanning 4 GiB or more (some key of >= 16 MiB; a key of
-      // >= 4 GiB): the records below hold u32 window offsets and lengths, so
-      // this window is hashed in input order with u64 offsets and lengths
-      // instead (wave-uniform branch).
-#pragma unroll 1
-      for (int c = 0; c < M; c++) {
-        const uint32_t j = 64 * c + lane;
-        if (j < k) {
-          const uint64_t a = offs[i0 + j], len = offs[i0 + j + 1] - a;
-          const LdsKV5<LdsTab<NT>, uint64_t> K(kfull, len, s1, s2, T, ftab);
-          store_h(out, i0 + j, meow_rt(keys + a, len, K, T), fix);
-        }
-      }
-      continue;
-    }
     uint64_t o[M];
     uint32_t L[M], b[M], r[M];
+    bool wide = false;
 #pragma unroll
     for (int m = 0; m < M; m++) {
       const uint32_t j = lane + 64 * m;
       const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
       o[m] = a - ws;
       L[m] = (uint32_t)(e - a);
+      wide |= e - ws >= (1ull << 32);
     }
-#pragma unroll
-    for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
-    wave_sync();
-#pragma unroll
-    for (int m = 0; m < M; m++) {
-      const uint32_t j = lane + 64 * m;
-      b[m] = (L[m] >> SH) < 255u ? (L[m] >> SH) : 255u;  // SH: see wave_sort_from
-      r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
+    // A window spanning 4 GiB or more (some key of >= 16 MiB; a key of
+    // >= 4 GiB): the records below hold u32 window offsets and lengths, so
+    // this window is hashed in input order with u64 offsets and lengths
+    // instead (wave-uniform), through the same hash call site.
+    const bool wwin = __ballot(wide) != 0;
+    if constexpr (PF) {
+      if (wwin) { wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds); continue; }
     }
-    wave_sync();
-    {  // exclusive scan of the 256 bucket counts, 4 per lane
-      uint32_t v[4], sum = 0;
+    if (!wwin) {
 #pragma unroll
-      for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
-      uint32_t inc = sum;
+      for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
+      wave_sync();
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (lane >= (uint32_t)d) inc += y;
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        b[m] = (L[m] >> SH) < 255u ? (L[m] >> SH) : 255u;  // SH: see wave_sort_from
+        r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
       }
-      uint32_t run = inc - sum;
+      wave_sync();
+      {  // exclusive scan of the 256 bucket counts, 4 per lane
+        uint32_t v[4], sum = 0;
 #pragma unroll
-      for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
-    }
-    wave_sync();
+        for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
+        uint32_t inc = sum;
 #pragma unroll
-    for (int m = 0; m < M; m++) {
-      const uint32_t j = lane + 64 * m;
-      if (j < k) {
-        const uint32_t pos = hist[b[m]] + r[m];
-        r_off[pos] = (uint32_t)o[m];
-        r_len[pos] = L[m];
-        r_idx[pos] = j;
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(inc, d, 64);
+          if (lane >= (uint32_t)d) inc += y;
+        }
+        uint32_t run = inc - sum;
+#pragma unroll
+        for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
       }
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        if (j < k) {
+          const uint32_t pos = hist[b[m]] + r[m];
+          r_off[pos] = (uint32_t)o[m];
+          r_len[pos] = L[m];
+          r_idx[pos] = j;
+        }
+      }
+      wave_sync();
     }
-    wave_sync();
     const uint8_t* base = keys + ws;
     if constexpr (PF) {
       // first 64 bytes of the next chunk's key are in flight while this
@@ -1044,11 +1063,21 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
         const uint32_t pos = 64 * c + lane;
         ix[c] = WIN;
         if (pos < k) {
-          const uint32_t kl = r_len[pos];
-          const LdsKV5<LdsTab<NT>> K(kfull, kl, s1, s2, T, ftab);
-          hs[c] = meow_rt(base + r_off[pos], kl, K, T);
+          const uint8_t* p;
+          uint64_t kl;
+          if (!wwin) {
+            p = base + r_off[pos];
+            kl = r_len[pos];
+            ix[c] = r_idx[pos];
+          } else {
+            const uint64_t a = offs[i0 + pos];
+            p = keys + a;
+            kl = offs[i0 + pos + 1] - a;
+            ix[c] = pos;
+          }
+          const LdsKV5<LdsTab<NT>, uint64_t> K(kfull, kl, s1, s2, T, ftab);
+          hs[c] = meow_rt(p, kl, K, T);
           if (fix) hs[c] = fixup(hs[c]);
-          ix[c] = r_idx[pos];
         }
       }
       wave_sync();
@@ -1065,6 +1094,187 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       }
     }
     wave_sync();  // records reused by the next window
+  }
+}
+
+// ---------------------------------------------------------------------
+// k_var7: k_var6's per-wave length-class windows with the LDS traffic that
+// the round-1 counters charged to it removed:
+//  * ranking without LDS atomics on shared addresses: a key's class c =
+//    min(len >> 4, 63) (16-byte length class: same full-block count, so the
+//    same trip counts; the stable counting sort keeps a class in address
+//    order).  The lanes of one 64-key sub-chunk that share c are found with
+//    6 ballots (one per bit of c, "match any"); the lowest of them adds the
+//    group's size to hist[c] (one LDS atomic per distinct class, at distinct
+//    addresses) and broadcasts the old count; each lane's rank is that plus
+//    its mbcnt in the group.  64 buckets: one per lane, one-wave scan.
+//    (k_var6: 256 buckets, one same-address atomic per key: 8-15 B keys,
+//    16 % of them 8 B, all land in bucket 0.)
+//  * per-length constants as one 16-byte array per field (F0..F3, G0..G3,
+//    TG2, CS2b, TCS0a for L < 64; F0..F3 for 64 <= L < 320) instead of
+//    176-byte / 64-byte records: lanes of a sorted chunk read lengths that
+//    differ by less than 8, which map to disjoint 4-bank groups.
+//  * the 4 GiB check from the lanes' offsets (one ballot), no extra load.
+template <class Tab, class LenT = uint32_t>
+struct LdsKV7 {
+  const Blk* c;  // field-major constant arrays, see k_var7
+  LenT L;
+  Blk m;
+  const Tab& T;
+  static constexpr int kF = 0, kG = 4 * kLT, kTG2 = 8 * kLT, kCS2b = 9 * kLT, kTCS0a = 10 * kLT, kFF = 11 * kLT;
+  static constexpr int kWords = 11 * kLT + 4 * kNF;  // Blk entries
+  __device__ __forceinline__ LdsKV7(const Blk* cc, LenT len, uint64_t s1, uint64_t s2, const Tab& t)
+      : c(cc), L(len), m(mixer(s1, s2, len)), T(t) {}
+  __device__ __forceinline__ uint32_t li() const { return L < (LenT)kLT ? (uint32_t)L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ Blk M() const { return m; }
+  __device__ __forceinline__ Blk F(int i) const {
+    if (L < (LenT)kLT) return c[kF + i * kLT + (uint32_t)L];
+    if (L < (LenT)(kLT + kNF)) return c[kFF + i * kNF + (uint32_t)(L - kLT)];
+    return aesT(bxor(ramp(i), m), T);
+  }
+  __device__ __forceinline__ Blk G(int i) const { return c[kG + i * kLT + li()]; }
+  __device__ __forceinline__ Blk TG2() const { return c[kTG2 + li()]; }
+  __device__ __forceinline__ Blk CS2b() const { return c[kCS2b + li()]; }
+  __device__ __forceinline__ Blk TCS0a() const { return c[kTCS0a + li()]; }
+};
+
+template <int NT, int WIN = 256, int NW = kBlock / 64>
+__global__ void __launch_bounds__(NW * 64)
+k_var7(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+       uint64_t* __restrict__ out, uint32_t flags) {
+  using KC = LdsKV7<LdsTab<NT>>;
+  constexpr int M = WIN / 64;
+  constexpr int kNB = 64;                          // length classes
+  constexpr int kRec = kNB * 4 + WIN * 12;         // hist + u32 off, len, idx
+  constexpr int kPerWave = kRec > WIN * 16 ? kRec : WIN * 16;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ Blk kc[KC::kWords];
+  __shared__ __attribute__((aligned(16))) uint8_t wavemem[NW * kPerWave];
+  static_assert(sizeof(lds) + sizeof(kc) + sizeof(wavemem) <= 163840, "LDS budget");
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + kNF); l += blockDim.x) {
+    if (l >= (uint32_t)kLT) {
+      const Blk Mx = mixer(s1, s2, l);
+#pragma unroll
+      for (int q = 0; q < 4; q++) kc[KC::kFF + q * kNF + (l - kLT)] = aesT(bxor(ramp(q), Mx), T);
+      continue;
+    }
+    const MeowConst k = make_const(s1, s2, l, T);
+#pragma unroll
+    for (int q = 0; q < 4; q++) { kc[KC::kF + q * kLT + l] = k.F[q]; kc[KC::kG + q * kLT + l] = k.G[q]; }
+    kc[KC::kTG2 + l] = k.TG2; kc[KC::kCS2b + l] = k.CS2b; kc[KC::kTCS0a + l] = k.TCS0a;
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* hist = (uint32_t*)(wavemem + wv * kPerWave);
+  uint32_t* r_off = hist + kNB;
+  uint32_t* r_len = r_off + WIN;
+  uint32_t* r_idx = r_len + WIN;
+  const uint64_t nwin = (n + WIN - 1) / WIN;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
+  for (uint64_t w = gw; w < nwin; w += tw) {
+    const uint64_t i0 = w * WIN;
+    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    const uint64_t ws = offs[i0];
+    uint32_t o[M], L[M], b[M], r[M];
+    bool wide = false;
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
+      o[m] = (uint32_t)(a - ws);
+      L[m] = (uint32_t)(e - a);
+      wide |= e - ws >= (1ull << 32);
+    }
+    // A window spanning 4 GiB or more (a key of >= 16 MiB) cannot use the
+    // u32 window-relative records: it is hashed in input order with u64
+    // offsets and lengths through the same hash call site (no second copy
+    // of the round code: k_var6's inlined u64 path cost 32 VGPR spills).
+    const bool wwin = __ballot(wide) != 0;
+    if (!wwin) {
+      hist[lane] = 0;
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        const bool v = j < k;
+        b[m] = (L[m] >> 4) < (uint32_t)(kNB - 1) ? (L[m] >> 4) : (uint32_t)(kNB - 1);
+        uint64_t eq = __ballot(v);
+#pragma unroll
+        for (int bit = 0; bit < 6; bit++) {
+          const uint64_t B = __ballot((b[m] >> bit) & 1u);
+          eq &= ((b[m] >> bit) & 1u) ? B : ~B;
+        }
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(eq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)eq, 0u));
+        uint32_t base = 0;
+        if (v && below == 0) base = atomicAdd(&hist[b[m]], (uint32_t)__popcll(eq));
+        const uint32_t lead = v ? (uint32_t)__builtin_ctzll(eq) : lane;
+        base = __shfl(base, lead, 64);
+        r[m] = base + below;
+      }
+      wave_sync();
+      {  // exclusive scan of the 64 class counts, one per lane
+        const uint32_t cnt = hist[lane];
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(inc, d, 64);
+          if (lane >= (uint32_t)d) inc += y;
+        }
+        hist[lane] = inc - cnt;
+      }
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        if (j < k) {
+          const uint32_t pos = hist[b[m]] + r[m];
+          r_off[pos] = o[m];
+          r_len[pos] = L[m];
+          r_idx[pos] = j;
+        }
+      }
+      wave_sync();
+    }
+    Blk hs[M];
+    uint32_t ix[M];
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t pos = 64 * c + lane;
+      ix[c] = WIN;
+      if (pos < k) {
+        const uint8_t* p;
+        uint64_t kl;
+        if (!wwin) {
+          p = keys + ws + r_off[pos];
+          kl = r_len[pos];
+          ix[c] = r_idx[pos];
+        } else {
+          const uint64_t a = offs[i0 + pos];
+          p = keys + a;
+          kl = offs[i0 + pos + 1] - a;
+          ix[c] = pos;
+        }
+        const LdsKV7<LdsTab<NT>, uint64_t> K(kc, kl, s1, s2, T);
+        hs[c] = meow_rt(p, kl, K, T);
+        if (fix) hs[c] = fixup(hs[c]);
+      }
+    }
+    wave_sync();
+    Blk* stage = (Blk*)hist;  // records consumed: the wave's area stages the hashes in input order
+#pragma unroll
+    for (int c = 0; c < M; c++)
+      if (ix[c] < (uint32_t)WIN) stage[ix[c]] = hs[c];
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t j = 64 * c + lane;
+      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
+    }
+    wave_sync();  // staging read before the next window's histogram
   }
 }
 
@@ -1491,21 +1701,27 @@ int same_len_host(const void* const* ptrs, size_t cnt, size_t sz, const uint64_t
   return seeded_host(ptrs, lens.data(), cnt, seeds.data(), x, 0);
 }
 
-// Per-device host pipeline state for kvh_meow128_fixed_host (grown on
-// demand, kept for the process lifetime).
+// Host pipeline state (kvh_meow128_{fixed,var}_host): streams, events and
+// buffer slots, grown on demand and kept for the process lifetime.  Each
+// device has kPipesPerDev of them, so that several host threads may drive one
+// device at once (kvh_*_host_multi with a device listed twice); a call holds
+// one pipeline for its duration.
 constexpr int kPipeSlots = 16;  // buffer slots allocated; g_tune_pipe_slots of them used
 constexpr int kMaxDev = 64;
+constexpr int kPipesPerDev = 4;
 Knob g_tune_pipe_mib{16};   // key bytes per pipeline chunk, MiB (knob 15)
 Knob g_tune_pipe_slots{4};  // chunks in flight (knob 16)
 struct HostPipe {
   std::mutex mu;
   hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
   hipEvent_t ev_in[kPipeSlots] = {}, ev_k[kPipeSlots] = {}, ev_out[kPipeSlots] = {};
-  uint8_t* dk[kPipeSlots] = {};
-  uint64_t* dout[kPipeSlots] = {};
-  uint8_t* hk[kPipeSlots] = {};
+  uint8_t* dk[kPipeSlots] = {};      // key bytes (device)
+  uint64_t* doff[kPipeSlots] = {};   // key offsets (device, variable length)
+  uint64_t* dout[kPipeSlots] = {};   // hashes (device)
+  uint8_t* hk[kPipeSlots] = {};      // pinned bounce buffers for pageable callers
+  uint64_t* hoff[kPipeSlots] = {};
   uint64_t* ho[kPipeSlots] = {};
-  size_t kcap = 0, ocap = 0, hkcap = 0, hocap = 0;
+  size_t kcap = 0, fcap = 0, ocap = 0, hkcap = 0, hfcap = 0, hocap = 0;
   // slots [0, ns) of buffer array b hold `want` bytes each (grow-only)
   template <class T, class A, class F>
   static hipError_t regrow(T* (&b)[kPipeSlots], size_t& cap, size_t want, int ns, A alloc, F release) {
@@ -1520,9 +1736,9 @@ struct HostPipe {
     }
     return hipSuccess;
   }
-  // streams, events and ns slots of buffers for chunks of kb key bytes / ob
-  // hash bytes on the current device
-  int reserve(int ns, size_t kb, size_t ob, bool need_hk, bool need_ho) {
+  // streams, events and ns slots for chunks of kb key bytes, fb offset bytes
+  // (0: fixed length) and ob hash bytes on the current device
+  int reserve(int ns, size_t kb, size_t fb, size_t ob, bool need_hk, bool need_hf, bool need_ho) {
     hipError_t e = hipSuccess;
     for (hipStream_t* st : {&s_in, &s_k, &s_out})
       if (e == hipSuccess && !*st) e = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
@@ -1533,14 +1749,178 @@ struct HostPipe {
     auto dfree = [](void* p) { return hipFree(p); };
     auto hmal = [](void** p, size_t b) { return hipHostMalloc(p, b, 0); };
     auto hfree = [](void* p) { return hipHostFree(p); };
-    if (e == hipSuccess) e = regrow(dk, kcap, kb, ns, dmal, dfree);
+    if (e == hipSuccess) e = regrow(dk, kcap, std::max<size_t>(kb, 16), ns, dmal, dfree);
+    if (e == hipSuccess && fb) e = regrow(doff, fcap, fb, ns, dmal, dfree);
     if (e == hipSuccess) e = regrow(dout, ocap, ob, ns, dmal, dfree);
-    if (e == hipSuccess && need_hk) e = regrow(hk, hkcap, kb, ns, hmal, hfree);
+    if (e == hipSuccess && need_hk) e = regrow(hk, hkcap, std::max<size_t>(kb, 16), ns, hmal, hfree);
+    if (e == hipSuccess && need_hf) e = regrow(hoff, hfcap, fb, ns, hmal, hfree);
     if (e == hipSuccess && need_ho) e = regrow(ho, hocap, ob, ns, hmal, hfree);
     return e == hipSuccess ? 0 : hip_err(e);
   }
 };
-HostPipe g_pipe[kMaxDev];
+HostPipe g_pipe[kMaxDev][kPipesPerDev];
+
+// a free pipeline of the current device (blocks on pipeline 0 when all are busy)
+std::unique_lock<std::mutex> pick_pipe(int dev, HostPipe** P) {
+  for (int i = 0; i < kPipesPerDev; i++) {
+    std::unique_lock<std::mutex> lk(g_pipe[dev][i].mu, std::try_to_lock);
+    if (lk.owns_lock()) { *P = &g_pipe[dev][i]; return lk; }
+  }
+  *P = &g_pipe[dev][0];
+  return std::unique_lock<std::mutex>(g_pipe[dev][0].mu);
+}
+
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  const bool pin = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
+  (void)hipGetLastError();
+  return pin;
+}
+
+// One host batch through H2D -> kernel -> D2H on the current device.
+// Chunk c is keys [lo_c, hi_c): fixed length (key_len > 0) in chunks of
+// `chunk_keys` keys, variable length (offs != nullptr, n+1 host offsets) in
+// chunks of at most `budget` key bytes and `chunk_keys` keys (a longer key
+// is a chunk of its own, the buffers grow to hold it).  Three streams (H2D,
+// kernel, D2H) linked by per-slot events, `slots` chunks in flight: chunk c
+// is copied in on s_in, hashed on s_k once its copy-in event fired, copied
+// out on s_out once its kernel event fired; a slot is refilled once its
+// previous chunk's copy-out event fired.  One stream per DMA direction lets
+// both PCIe directions run at once (full duplex).
+int host_pipeline(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, size_t n, uint64_t s1, uint64_t s2,
+                  uint64_t* out, uint32_t flags) {
+  if (n == 0) return set_err(0);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  if (dev < 0 || dev >= kMaxDev) return set_err(KVH_EINVAL);
+  HostPipe* P = nullptr;
+  std::unique_lock<std::mutex> lk = pick_pipe(dev, &P);
+  const bool var = offs != nullptr;
+  const size_t budget = (size_t)knob(g_tune_pipe_mib) << 20;
+  const size_t chunk_keys = var ? std::max<size_t>(1, budget / 8) : std::max<size_t>(1, budget / key_len);
+  // chunk boundaries; the largest chunk sizes the buffers
+  std::vector<size_t> bounds{0};
+  size_t max_bytes = 0, max_keys = 0;
+  while (bounds.back() < n) {
+    const size_t lo = bounds.back();
+    size_t hi = std::min(n, lo + chunk_keys);
+    if (var) {  // at most `budget` key bytes, at least one key
+      const uint64_t lim = offs[lo] + budget;
+      hi = std::max(lo + 1, (size_t)(std::upper_bound(offs + lo, offs + hi + 1, lim) - offs) - 1);
+      max_bytes = std::max<size_t>(max_bytes, offs[hi] - offs[lo]);
+    } else {
+      max_bytes = std::max<size_t>(max_bytes, (hi - lo) * key_len);
+    }
+    max_keys = std::max(max_keys, hi - lo);
+    bounds.push_back(hi);
+  }
+  const bool pin_k = is_pinned(keys), pin_o = is_pinned(out), pin_f = var && is_pinned(offs);
+  const int slots = std::min(std::max(knob(g_tune_pipe_slots), 2), kPipeSlots);
+  int rc = P->reserve(slots, max_bytes, var ? 8 * (max_keys + 1) : 0, 16 * max_keys, !pin_k, var && !pin_f, !pin_o);
+  if (rc) return rc;
+  size_t pend_lo[kPipeSlots] = {}, pend_cnt[kPipeSlots] = {};
+  auto drain = [&](int s) -> int {  // the slot's previous chunk has left the device
+    if (!pend_cnt[s]) return 0;
+    hipError_t x = hipEventSynchronize(P->ev_out[s]);
+    if (x != hipSuccess) return hip_err(x);
+    if (!pin_o) memcpy(out + 2 * pend_lo[s], P->ho[s], pend_cnt[s] * 16);
+    pend_cnt[s] = 0;
+    return 0;
+  };
+  for (size_t c = 0; !rc && c + 1 < bounds.size(); c++) {
+    const int s = (int)(c % slots);
+    if ((rc = drain(s))) break;
+    const size_t lo = bounds[c], cnt = bounds[c + 1] - lo;
+    const uint64_t base = var ? offs[lo] : (uint64_t)lo * key_len;
+    const size_t nbytes = var ? (size_t)(offs[lo + cnt] - base) : cnt * key_len;
+    const uint8_t* src = keys + base;
+    if (!pin_k && nbytes) { memcpy(P->hk[s], src, nbytes); src = P->hk[s]; }
+    const uint64_t* fsrc = var ? offs + lo : nullptr;
+    if (var && !pin_f) { memcpy(P->hoff[s], fsrc, 8 * (cnt + 1)); fsrc = P->hoff[s]; }
+    uint64_t* dst = pin_o ? out + 2 * lo : P->ho[s];
+    if ((nbytes && (e = hipMemcpyAsync(P->dk[s], src, nbytes, hipMemcpyHostToDevice, P->s_in)) != hipSuccess) ||
+        (var && (e = hipMemcpyAsync(P->doff[s], fsrc, 8 * (cnt + 1), hipMemcpyHostToDevice, P->s_in)) != hipSuccess) ||
+        (e = hipEventRecord(P->ev_in[s], P->s_in)) != hipSuccess ||
+        (e = hipStreamWaitEvent(P->s_k, P->ev_in[s], 0)) != hipSuccess) {
+      rc = hip_err(e); break;
+    }
+    // variable length: the chunk's offsets stay absolute (offs[lo] .. offs[hi]);
+    // the key pointer handed to the kernel is biased by -offs[lo], so every
+    // address it forms, keys + offs[i], lies inside this chunk's buffer
+    rc = var ? kvh_meow128_var((const uint8_t*)((uintptr_t)P->dk[s] - (uintptr_t)base), P->doff[s], cnt, s1, s2,
+                               P->dout[s], flags, P->s_k)
+             : kvh_meow128_fixed(P->dk[s], key_len, cnt, s1, s2, P->dout[s], flags, P->s_k);
+    if (rc) break;
+    if ((e = hipEventRecord(P->ev_k[s], P->s_k)) != hipSuccess ||
+        (e = hipStreamWaitEvent(P->s_out, P->ev_k[s], 0)) != hipSuccess ||
+        (e = hipMemcpyAsync(dst, P->dout[s], cnt * 16, hipMemcpyDeviceToHost, P->s_out)) != hipSuccess ||
+        (e = hipEventRecord(P->ev_out[s], P->s_out)) != hipSuccess) {
+      rc = hip_err(e); break;
+    }
+    pend_lo[s] = lo; pend_cnt[s] = cnt;
+  }
+  for (int s = 0; s < slots; s++) {
+    const int r2 = drain(s);
+    if (!rc) rc = r2;
+  }
+  if (rc) {  // leave the pipeline idle for the next call
+    (void)hipStreamSynchronize(P->s_in); (void)hipStreamSynchronize(P->s_k); (void)hipStreamSynchronize(P->s_out);
+  }
+  return rc ? rc : set_err(0);
+}
+
+// Shard d of n keys is [b[d], b[d+1]): equal index ranges (offs == nullptr)
+// or, for variable length, ranges holding equal key bytes: b[d] = the first
+// key whose start offset is >= offs[0] + total * d / ns (workload.py:
+// shard_var).  b[0] = 0, b[ns] = n, non-decreasing.
+void shard_bounds(const uint64_t* offs, size_t n, int ns, size_t* b) {
+  for (int d = 0; d <= ns; d++) {
+    if (!offs || n == 0) {
+      b[d] = (size_t)((unsigned __int128)n * d / ns);
+    } else {
+      const uint64_t tot = offs[n] - offs[0];
+      const uint64_t tgt = offs[0] + (uint64_t)((unsigned __int128)tot * d / ns);
+      b[d] = d == 0 ? 0 : d == ns ? n : (size_t)(std::lower_bound(offs, offs + n + 1, tgt) - offs);
+      if (b[d] > n) b[d] = n;
+    }
+  }
+}
+
+// Shards [lo_d, hi_d) of one host batch over ndev devices, one host thread
+// each (SURVEY.md §8 e: independent keys, no collective; each device writes
+// its disjoint slice of the caller's output, the same global layout as a
+// one-device call).  Fixed length: equal index ranges; variable length:
+// ranges of equal key BYTES (raikv_amd/workload.py: shard_var).
+int host_multi(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, size_t n, uint64_t s1, uint64_t s2,
+               uint64_t* out, uint32_t flags, const int* devices, int ndev) {
+  if (ndev < 1 || ndev > kMaxDev || !devices) return set_err(KVH_EINVAL);
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess) return hip_err(e);
+  for (int d = 0; d < ndev; d++)
+    if (devices[d] < 0 || devices[d] >= count || devices[d] >= kMaxDev) return set_err(KVH_EINVAL);
+  std::vector<size_t> lo(ndev + 1);
+  shard_bounds(offs, n, ndev, lo.data());
+  std::vector<int> rcs(ndev, 0);
+  std::vector<std::thread> th;
+  for (int d = 0; d < ndev; d++) {
+    th.emplace_back([&, d]() {
+      const size_t a = lo[d], b = std::max(lo[d], lo[d + 1]);
+      if (b == a) return;
+      const hipError_t se = hipSetDevice(devices[d]);
+      if (se != hipSuccess) { rcs[d] = hip_err(se); return; }
+      // variable length: shard offsets stay absolute into `keys`;
+      // fixed length: the shard's keys start at a * key_len
+      rcs[d] = offs ? host_pipeline(keys, 0, offs + a, b - a, s1, s2, out + 2 * a, flags)
+                    : host_pipeline(keys + (uint64_t)a * key_len, key_len, nullptr, b - a, s1, s2, out + 2 * a, flags);
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int d = 0; d < ndev; d++)
+    if (rcs[d]) return set_err(rcs[d]);
+  return set_err(0);
+}
 
 }  // namespace
 
@@ -1595,6 +1975,10 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
     case 7:
       hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
+      return launch_done();
+    case 14:
+      hipLaunchKernelGGL((k_var7<2>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out,
+                         flags);
       return launch_done();
     default:
       break;
@@ -1705,69 +2089,46 @@ int kvh_meow128_fixed_host(const void* keys, uint32_t key_len, size_t n, uint64_
                            uint64_t* out, uint32_t flags) {
   if (n == 0) return set_err(0);
   if (!keys || !out || key_len == 0) return set_err(KVH_EINVAL);
-  // Three-stage pipeline over kPipeSlots buffer slots: chunk i is copied in
-  // on the H2D stream, hashed on the compute stream once its copy-in event
-  // fires, and copied out on the D2H stream once its kernel event fires.  One
-  // stream per direction lets the two DMA directions run at once (PCIe is
-  // full duplex: ~57 GB/s each way, ~97 GB/s both; a stream carrying both
-  // directions of its chunks serialised them at ~56 GB/s in all, DESIGN.md
-  // §4.4).  A slot is refilled once its previous chunk's copy-out event has
-  // fired.  Streams, events and buffers persist per device across calls; the
-  // call holds the device's pipeline for its duration.  Host buffers are used
-  // directly when pinned; pageable memory goes through pinned bounce buffers.
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return hip_err(e);
-  if (dev < 0 || dev >= kMaxDev) return set_err(KVH_EINVAL);
-  HostPipe& P = g_pipe[dev];
-  std::lock_guard<std::mutex> lk(P.mu);
-  const size_t chunk = std::max<size_t>(1, ((size_t)knob(g_tune_pipe_mib) << 20) / key_len);
-  hipPointerAttribute_t ak, ao;
-  const bool pin_k = hipPointerGetAttributes(&ak, keys) == hipSuccess && ak.type == hipMemoryTypeHost;
-  const bool pin_o = hipPointerGetAttributes(&ao, out) == hipSuccess && ao.type == hipMemoryTypeHost;
-  (void)hipGetLastError();
-  const int slots = std::min(std::max(knob(g_tune_pipe_slots), 2), kPipeSlots);
-  int rc = P.reserve(slots, chunk * key_len, chunk * 16, !pin_k, !pin_o);
-  if (rc) return rc;
-  size_t pend_lo[kPipeSlots] = {}, pend_cnt[kPipeSlots] = {};
-  auto drain = [&](int s) -> int {  // the slot's previous chunk has left the device
-    if (!pend_cnt[s]) return 0;
-    hipError_t x = hipEventSynchronize(P.ev_out[s]);
-    if (x != hipSuccess) return hip_err(x);
-    if (!pin_o) memcpy(out + 2 * pend_lo[s], P.ho[s], pend_cnt[s] * 16);
-    pend_cnt[s] = 0;
-    return 0;
-  };
-  size_t idx = 0;
-  for (size_t lo = 0; !rc && lo < n; lo += chunk, idx++) {
-    const int s = (int)(idx % slots);
-    if ((rc = drain(s))) break;
-    const size_t cnt = std::min(chunk, n - lo);
-    const uint8_t* src = (const uint8_t*)keys + lo * key_len;
-    if (!pin_k) { memcpy(P.hk[s], src, cnt * key_len); src = P.hk[s]; }
-    uint64_t* dst = pin_o ? out + 2 * lo : P.ho[s];
-    if ((e = hipMemcpyAsync(P.dk[s], src, cnt * key_len, hipMemcpyHostToDevice, P.s_in)) != hipSuccess ||
-        (e = hipEventRecord(P.ev_in[s], P.s_in)) != hipSuccess ||
-        (e = hipStreamWaitEvent(P.s_k, P.ev_in[s], 0)) != hipSuccess) {
-      rc = hip_err(e); break;
-    }
-    if ((rc = kvh_meow128_fixed(P.dk[s], key_len, cnt, seed1, seed2, P.dout[s], flags, P.s_k))) break;
-    if ((e = hipEventRecord(P.ev_k[s], P.s_k)) != hipSuccess ||
-        (e = hipStreamWaitEvent(P.s_out, P.ev_k[s], 0)) != hipSuccess ||
-        (e = hipMemcpyAsync(dst, P.dout[s], cnt * 16, hipMemcpyDeviceToHost, P.s_out)) != hipSuccess ||
-        (e = hipEventRecord(P.ev_out[s], P.s_out)) != hipSuccess) {
-      rc = hip_err(e); break;
-    }
-    pend_lo[s] = lo; pend_cnt[s] = cnt;
-  }
-  for (int s = 0; s < slots; s++) {
-    const int r2 = drain(s);
-    if (!rc) rc = r2;
-  }
-  if (rc) {  // leave the pipeline idle for the next call
-    (void)hipStreamSynchronize(P.s_in); (void)hipStreamSynchronize(P.s_k); (void)hipStreamSynchronize(P.s_out);
-  }
-  return rc ? rc : set_err(0);
+  return host_pipeline((const uint8_t*)keys, key_len, nullptr, n, seed1, seed2, out, flags);
+}
+
+int kvh_meow128_var_host(const void* keys, const uint64_t* offsets, size_t n, uint64_t seed1, uint64_t seed2,
+                         uint64_t* out, uint32_t flags) {
+  if (n == 0) return set_err(0);
+  if (!keys || !offsets || !out) return set_err(KVH_EINVAL);
+  return host_pipeline((const uint8_t*)keys, 0, offsets, n, seed1, seed2, out, flags);
+}
+
+int kvh_meow128_fixed_host_multi(const void* keys, uint32_t key_len, size_t n, uint64_t seed1, uint64_t seed2,
+                                 uint64_t* out, uint32_t flags, const int* devices, int ndev) {
+  if (n == 0) return set_err(0);
+  if (!keys || !out || key_len == 0) return set_err(KVH_EINVAL);
+  return host_multi((const uint8_t*)keys, key_len, nullptr, n, seed1, seed2, out, flags, devices, ndev);
+}
+
+int kvh_meow128_var_host_multi(const void* keys, const uint64_t* offsets, size_t n, uint64_t seed1, uint64_t seed2,
+                               uint64_t* out, uint32_t flags, const int* devices, int ndev) {
+  if (n == 0) return set_err(0);
+  if (!keys || !offsets || !out) return set_err(KVH_EINVAL);
+  return host_multi((const uint8_t*)keys, 0, offsets, n, seed1, seed2, out, flags, devices, ndev);
+}
+
+int kvh_shard_bounds(const uint64_t* offsets, size_t n, int nshards, size_t* bounds) {
+  if (nshards < 1 || !bounds) return set_err(KVH_EINVAL);
+  shard_bounds(offsets, n, nshards, bounds);
+  return set_err(0);
+}
+
+int kvh_host_register(void* p, size_t bytes) {
+  if (!p || !bytes) return set_err(KVH_EINVAL);
+  const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterDefault);
+  return e == hipSuccess ? set_err(0) : hip_err(e);
+}
+
+int kvh_host_unregister(void* p) {
+  if (!p) return set_err(KVH_EINVAL);
+  const hipError_t e = hipHostUnregister(p);
+  return e == hipSuccess ? set_err(0) : hip_err(e);
 }
 
 int kvh_host_alloc(void** p, size_t bytes) {
@@ -2010,7 +2371,7 @@ int kvh_set_tuning(int k, int value) {
     case 2: return set(g_tune_generic, value ? 1 : 0);
     case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13) {
+    case 7: if (value != 0 && value != 7 && value != 13 && value != 14) {
 #ifdef KVH_EXPERIMENTS
               if (value < 2 || value > 12) return KVH_EINVAL;
 #else

@@ -1,0 +1,135 @@
+"""GPU: the PCIe-inclusive host pipelines (keys and hashes in host memory)
+and their one-process multi-device sharding, through the C-ABI.
+
+kvh_meow128_var_host is the path socket / shm-segment keys take
+(include/raikv/ev_key.h:83-114, test/ctest.c:202-233): variable-length keys
+in host memory.  Each result must equal the device-resident kernel on
+device copies of the same buffers (which test_gpu_parity.py and
+test_gpu_fullsize.py pin to the oracle), plus an oracle sample here.
+kvh_meow128_{fixed,var}_host_multi shard one host batch over a device list
+(one host thread per entry); on the one-GPU box the list repeats device 0,
+which runs the shards concurrently on separate pipelines of that device.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle_lib import load_oracle, orc_var  # noqa: E402
+
+ORC = load_oracle()
+STATIC = (0xA8E0BCC94D1855F5, 0xAD3BEC1E8DE4A1A3)
+
+
+@pytest.fixture(scope="module")
+def kvh():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
+    import raikv_amd
+    return raikv_amd
+
+
+def dev_hash_var(kvh, keys: np.ndarray, offs: np.ndarray, seed, fixup=False):
+    base = int(offs[0])
+    k = torch.from_numpy(keys[base:int(offs[-1])].copy() if offs[-1] > base else np.zeros(1, np.uint8)).cuda()
+    o = torch.from_numpy((offs - np.uint64(base)).view(np.int64)).cuda()
+    out = kvh.meow128_var(k, o, seed, fixup=fixup)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint64)
+
+
+def zipf_batch(n, seed, lead=0, long_keys=()):
+    from raikv_amd.workload import zipf_lengths
+    lens = zipf_lengths(n, 8, 256, seed=seed).astype(np.uint64)
+    for i, L in long_keys:
+        lens[i] = L
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(lens)
+    offs += np.uint64(lead)
+    keys = np.random.default_rng(seed).integers(0, 256, int(offs[-1]) + 7, dtype=np.uint8)
+    return keys, offs
+
+
+@pytest.mark.parametrize("mib,slots", [(16, 4), (1, 2), (1, 16)])
+def test_var_host_pipeline(kvh, mib, slots):
+    """Zipf keys with a nonzero first offset, keys longer than the chunk
+    budget (3 MiB with 1 MiB chunks: a chunk of their own) and runs of empty
+    keys; pageable, kvh_host_alloc-pinned and kvh_host_register'ed buffers;
+    ragged last chunk and slot reuse."""
+    n = 400_003
+    keys, offs = zipf_batch(n, 7, lead=5, long_keys=[(10, 3 << 20), (200_000, 3 << 20), (200_001, 1 << 20),
+                                                       (n - 1, 2 << 20)])
+    lens = np.diff(offs)
+    lens[5000:5100] = 0
+    offs[1:] = offs[0] + np.cumsum(lens)
+    want = dev_hash_var(kvh, keys, offs, STATIC)
+    pm, ps = kvh.lib.kvh_set_tuning(15, mib), kvh.lib.kvh_set_tuning(16, slots)
+    try:
+        got = kvh.meow128_var_host(keys, offs, STATIC)
+        np.testing.assert_array_equal(got, want)
+        # pinned (kvh_host_alloc) keys, offsets and output
+        hk = kvh.host_empty(keys.shape, np.uint8)
+        hk[:] = keys
+        hf = kvh.host_empty(offs.shape, np.uint64)
+        hf[:] = offs
+        ho = kvh.host_empty((n, 2), np.uint64)
+        kvh.meow128_var_host(hk, hf, STATIC, out=ho, fixup=True)
+        np.testing.assert_array_equal(ho, dev_hash_var(kvh, keys, offs, STATIC, fixup=True))
+        # a caller's own buffer page-locked in place (raikv's shm segment)
+        reg = np.empty(keys.size + 4096, dtype=np.uint8)
+        view = reg[:keys.size]
+        view[:] = keys
+        assert kvh.lib.kvh_host_register(view.ctypes.data, view.nbytes) == 0
+        try:
+            np.testing.assert_array_equal(kvh.meow128_var_host(view, offs, STATIC), want)
+        finally:
+            assert kvh.lib.kvh_host_unregister(view.ctypes.data) == 0
+    finally:
+        kvh.lib.kvh_set_tuning(15, pm)
+        kvh.lib.kvh_set_tuning(16, ps)
+    # oracle sample (short keys and a 3 MiB one)
+    idx = np.sort(np.concatenate([np.random.default_rng(1).choice(n, 3000, replace=False), [10]]))
+    sub = np.concatenate([keys[int(offs[i]):int(offs[i + 1])] for i in idx])
+    so = np.zeros(len(idx) + 1, dtype=np.uint64)
+    so[1:] = np.cumsum(lens[idx])
+    np.testing.assert_array_equal(want[idx], orc_var(ORC, sub, so, STATIC))
+
+
+def test_var_host_edges(kvh):
+    keys = np.frombuffer(b"hello\0", dtype=np.uint8).copy()
+    got = kvh.meow128_var_host(keys, np.array([0, 6], dtype=np.uint64), STATIC)
+    assert "%016x:%016x" % (int(got[0, 0]), int(got[0, 1])) == "2aa73a1eeb0b2d45:fd102121185ce157"
+    empty = kvh.meow128_var_host(keys, np.zeros(1001, dtype=np.uint64), (7, 9))
+    np.testing.assert_array_equal(empty, dev_hash_var(kvh, keys, np.zeros(1001, dtype=np.uint64), (7, 9)))
+    assert kvh.meow128_var_host(keys, np.zeros(1, dtype=np.uint64), STATIC).shape == (0, 2)
+    assert kvh.lib.kvh_meow128_var_host(None, None, 5, 0, 0, None, 0) == -22
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_device_fixed_and_var(kvh, devices):
+    """One host batch over a device list: the output equals the one-device
+    call (the same global layout); ragged shard sizes; more shards than keys."""
+    rng = np.random.default_rng(len(devices))
+    for n, L in ((1_000_003, 16), (777, 32), (2, 16)):
+        kb = rng.integers(0, 256, n * L, dtype=np.uint8)
+        want = kvh.meow128_fixed_host(kb, L, STATIC)
+        np.testing.assert_array_equal(kvh.meow128_host_multi(kb, STATIC, devices, key_len=L), want)
+        np.testing.assert_array_equal(kvh.meow128_host_multi(kb, STATIC, devices, key_len=L, fixup=True),
+                                      kvh.meow128_fixed_host(kb, L, STATIC, fixup=True))
+    for n in (300_001, 3, 1):
+        keys, offs = zipf_batch(n, 11 + n, lead=3)
+        want = dev_hash_var(kvh, keys, offs, STATIC)
+        np.testing.assert_array_equal(kvh.meow128_host_multi(keys, STATIC, devices, offsets=offs), want)
+
+
+def test_multi_device_rejects_bad_device_lists(kvh):
+    kb = np.zeros(1600, np.uint8)
+    out = np.zeros((100, 2), np.uint64)
+    bad = (C.c_int * 2)(0, 9999)
+    assert kvh.lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, 16, 100, 0, 0, out.ctypes.data, 0, bad, 2) == -22
+    assert kvh.lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, 16, 100, 0, 0, out.ctypes.data, 0, bad, 0) == -22
+    neg = (C.c_int * 1)(-1)
+    assert kvh.lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, 16, 100, 0, 0, out.ctypes.data, 0, neg, 1) == -22

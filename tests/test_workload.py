@@ -48,3 +48,28 @@ def test_var_shards_balance_bytes():
     assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
     b = [int(offs[hi] - offs[lo]) for lo, hi in rs]
     assert max(b) - min(b) < 3 * 256 + 0.02 * sum(b)
+
+
+def test_c_abi_shard_bounds_match_workload_rules():
+    """kvh_shard_bounds (the shard arithmetic of kvh_meow128_*_host_multi,
+    host-only) equals workload.shard_range / shard_var, also with a nonzero
+    first offset, empty keys, one huge key and more shards than keys."""
+    import raikv_amd as kvh
+    for n in (0, 1, 2, 7, 1000, 100_003):
+        for w in (1, 2, 3, 8):
+            b = kvh.shard_bounds(n, w)
+            assert [int(x) for x in b] == [shard_range(n, r, w)[0] for r in range(w)] + [n]
+    rng = np.random.default_rng(0)
+    for n in (1, 5, 999, 50_000):
+        lens = rng.integers(0, 300, n)
+        if n > 10:
+            lens[n // 3] = 10_000_000
+            lens[: n // 10] = 0
+        offs = offsets_from_lengths(lens)
+        for w in (1, 2, 3, 8, 16):
+            b = [int(x) for x in kvh.shard_bounds(n, w, offs)]
+            assert b == [shard_var(offs, r, w)[0] for r in range(w)] + [n], (n, w)
+            assert all(b[i] <= b[i + 1] for i in range(w))
+            # a nonzero first offset (a slice of a bigger buffer) shifts nothing
+            b2 = [int(x) for x in kvh.shard_bounds(n, w, offs + np.uint64(12345))]
+            assert b2 == b
