@@ -161,6 +161,30 @@ def _stream_ptr(stream) -> Optional[int]:
     return None
 
 
+def _as_torch_stream(stream):
+    if hasattr(stream, "wait_stream"):
+        return stream
+    return torch.cuda.ExternalStream(int(getattr(stream, "cuda_stream", stream)))
+
+
+def _after_current(stream) -> None:
+    """A caller's stream first waits for torch's current stream, on which
+    the count / scratch / output tensors of the call were just allocated and
+    zeroed."""
+    if stream is not None:
+        _as_torch_stream(stream).wait_stream(torch.cuda.current_stream())
+
+
+def _count(cnt, stream) -> int:
+    """Read a device count written by kernels on `stream`.  Tensor.item()
+    waits only for torch's current stream; a caller's own (non-blocking)
+    stream is synchronised first, or the zero-initialised count could be
+    read before the kernels that write it have run."""
+    if stream is not None:
+        _as_torch_stream(stream).synchronize()
+    return int(cnt.item())
+
+
 def _dev_ptr(t) -> int:
     if not t.is_cuda:
         raise KvhError("expected a device tensor")
@@ -256,9 +280,10 @@ def tokenize(text, max_token: int = 256, cap: Optional[int] = None, stream=None)
         cap = n // 2 + 1
     offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=text.device)
     lens = torch.empty((max(cap, 1),), dtype=torch.int32, device=text.device)
+    _after_current(stream)
     check(lib.kvh_tokenize(_dev_ptr(text) if n else None, n, max_token, _dev_ptr(offs), _dev_ptr(lens), cap,
                            _dev_ptr(cnt), _dev_ptr(scratch), scratch.numel() * 8, _stream_ptr(stream)), "kvh_tokenize")
-    k = int(cnt.item())
+    k = _count(cnt, stream)
     return offs[:min(k, cap)], lens[:min(k, cap)]
 
 
@@ -275,12 +300,13 @@ def tokenize_hash(text, seed: Tuple[int, int], max_token: int = 256, cap: Option
     offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=text.device)
     lens = torch.empty((max(cap, 1),), dtype=torch.int32, device=text.device)
     out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=text.device)
+    _after_current(stream)
     check(lib.kvh_tokenize_hash(_dev_ptr(text) if n else None, n, max_token, U64(seed[0] & (2**64 - 1)),
                                 U64(seed[1] & (2**64 - 1)),
                                 (KVH_FIXUP if fixup else 0) | (KVH_NULTERM if nulterm else 0), _dev_ptr(offs),
                                 _dev_ptr(lens), _dev_ptr(out), cap, _dev_ptr(cnt), _dev_ptr(scratch),
                                 scratch.numel() * 8, _stream_ptr(stream)), "kvh_tokenize_hash")
-    k = min(int(cnt.item()), cap)
+    k = min(_count(cnt, stream), cap)
     return offs[:k], lens[:k], out[:k]
 
 
@@ -308,9 +334,10 @@ def frag_offsets(buf, cap: Optional[int] = None, stream=None):
     if cap is None:
         cap = n // 2 + 1
     offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=buf.device)
+    _after_current(stream)
     check(lib.kvh_frag_offsets(_dev_ptr(buf) if n else None, n, _dev_ptr(offs), cap, _dev_ptr(cnt), _dev_ptr(scratch),
                                scratch.numel() * 8, _stream_ptr(stream)), "kvh_frag_offsets")
-    return offs[:min(int(cnt.item()), cap)]
+    return offs[:min(_count(cnt, stream), cap)]
 
 
 def frags_hash(buf, seed: Tuple[int, int], cap: Optional[int] = None, fixup: bool = True, stream=None):
@@ -324,10 +351,11 @@ def frags_hash(buf, seed: Tuple[int, int], cap: Optional[int] = None, fixup: boo
         cap = n // 2 + 1
     offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=buf.device)
     out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=buf.device)
+    _after_current(stream)
     check(lib.kvh_frags_hash(_dev_ptr(buf) if n else None, n, U64(seed[0] & (2**64 - 1)), U64(seed[1] & (2**64 - 1)),
                              KVH_FIXUP if fixup else 0, _dev_ptr(offs), _dev_ptr(out), cap, _dev_ptr(cnt),
                              _dev_ptr(scratch), scratch.numel() * 8, _stream_ptr(stream)), "kvh_frags_hash")
-    k = min(int(cnt.item()), cap)
+    k = min(_count(cnt, stream), cap)
     return offs[:k], out[:k]
 
 

@@ -1097,6 +1097,7 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
   }
 }
 
+#ifdef KVH_EXPERIMENTS
 // ---------------------------------------------------------------------
 // k_var7: k_var6's per-wave length-class windows with the LDS traffic that
 // the round-1 counters charged to it removed:
@@ -1138,7 +1139,7 @@ struct LdsKV7 {
   __device__ __forceinline__ Blk TCS0a() const { return c[kTCS0a + li()]; }
 };
 
-template <int NT, int WIN = 256, int NW = kBlock / 64>
+template <int NT, int WIN = 256, int NW = kBlock / 64, int HV = 0>
 __global__ void __launch_bounds__(NW * 64)
 k_var7(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -1259,7 +1260,9 @@ k_var7(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
           ix[c] = pos;
         }
         const LdsKV7<LdsTab<NT>, uint64_t> K(kc, kl, s1, s2, T);
-        hs[c] = meow_rt(p, kl, K, T);
+        // HV 1: every load of the key issued before its rounds (meow_var)
+        if constexpr (HV == 1) hs[c] = meow_var(p, kl, K, T);
+        else hs[c] = meow_rt(p, kl, K, T);
         if (fix) hs[c] = fixup(hs[c]);
       }
     }
@@ -1277,6 +1280,7 @@ k_var7(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     wave_sync();  // staging read before the next window's histogram
   }
 }
+#endif  // KVH_EXPERIMENTS
 
 #ifdef KVH_EXPERIMENTS
 // ---------------------------------------------------------------------
@@ -1976,15 +1980,27 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
       hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
       return launch_done();
-    case 14:
-      hipLaunchKernelGGL((k_var7<2>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out,
-                         flags);
-      return launch_done();
     default:
       break;
   }
 #ifdef KVH_EXPERIMENTS
   switch (var) {
+    case 14:
+      hipLaunchKernelGGL((k_var7<2>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out,
+                         flags);
+      return launch_done();
+    case 15:
+      hipLaunchKernelGGL((k_var7<2, 256, kBlock / 64, 1>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n,
+                         seed1, seed2, out, flags);
+      return launch_done();
+    case 16:
+      hipLaunchKernelGGL((k_var7<2, 256, 12, 1>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n,
+                         seed1, seed2, out, flags);
+      return launch_done();
+    case 17:
+      hipLaunchKernelGGL((k_var7<2, 256, 12, 0>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n,
+                         seed1, seed2, out, flags);
+      return launch_done();
     case 11: hipLaunchKernelGGL((k_var6<2, 384, false, 12>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     case 12: hipLaunchKernelGGL((k_var6<2, 512, false, 10>), dim3(cus), dim3(640), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     case 8: hipLaunchKernelGGL((k_var6<2, 128>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
@@ -2371,9 +2387,9 @@ int kvh_set_tuning(int k, int value) {
     case 2: return set(g_tune_generic, value ? 1 : 0);
     case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13 && value != 14) {
+    case 7: if (value != 0 && value != 7 && value != 13) {
 #ifdef KVH_EXPERIMENTS
-              if (value < 2 || value > 12) return KVH_EINVAL;
+              if (value < 2 || value > 17) return KVH_EINVAL;
 #else
               return KVH_EINVAL;
 #endif

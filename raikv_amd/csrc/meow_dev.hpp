@@ -407,9 +407,10 @@ __device__ __forceinline__ Blk meow_rt(const uint8_t* p, LenT L, const KGet& K, 
 // Variable-length Meow with every load issued before the rounds that need
 // it: the trail chunks and block 0 are requested up front, block b+1 while
 // block b is absorbed.  Same dataflow and folding as meow_rt.
-template <class Tab, class KGet>
-__device__ __forceinline__ Blk meow_var(const uint8_t* p, uint32_t L, const KGet& K, const Tab& T) {
-  const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
+template <class Tab, class KGet, class LenT = uint32_t>
+__device__ __forceinline__ Blk meow_var(const uint8_t* p, LenT L, const KGet& K, const Tab& T) {
+  const LenT nb = L >> 6;
+  const uint32_t C = (uint32_t)L & 48, t = (uint32_t)L & 15;
   const uint8_t* q = p + 64 * (uint64_t)nb;
   const Blk z = bzero();
   // trail chunks (key_hash.c:1200-1210) and the first full block, all in flight together
@@ -424,7 +425,7 @@ __device__ __forceinline__ Blk meow_var(const uint8_t* p, uint32_t L, const KGet
     if (nb > 1) { n0 = load16_full(p + 64); n1 = load16_full(p + 80); n2 = load16_full(p + 96); n3 = load16_full(p + 112); }
     S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
     S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
-    for (uint32_t b = 1; b < nb; b++) {
+    for (LenT b = 1; b < nb; b++) {
       k0 = n0; k1 = n1; k2 = n2; k3 = n3;
       if (b + 1 < nb) {
         const uint8_t* r = p + 64 * (uint64_t)(b + 1);

@@ -293,3 +293,27 @@ def test_frag_stream_tiny(kvh):
         got = host(kvh.frag_offsets(dev))
         want = {b"": [], b"\x00": [], b"\x00\x00": [0], b"\x01\x00a": [0], b"\x01\x00a\x00": [0], b"\x05\x00ab": []}[b]
         np.testing.assert_array_equal(got, np.array(want, dtype=np.uint64), err_msg=repr(b))
+
+
+def test_side_stream_counts(kvh):
+    """the count-returning calls on a caller's own non-blocking
+    stream (torch.cuda.Stream and a raw stream handle) read the count only
+    after their kernels ran, and order after the current stream's zero fill
+    of it: the same results as on the current stream, repeatedly."""
+    text = torch.from_numpy(G["text"]).cuda()
+    frags = torch.from_numpy(G["frags"]).cuda()
+    want_o, want_l = orc_tokenize(ORC, G["text"], 256)
+    side = torch.cuda.Stream()
+    for st in (side, side.cuda_stream):
+        for _ in range(3):
+            o, l = kvh.tokenize(text, 256, stream=st)
+            np.testing.assert_array_equal(host(o), want_o)
+            np.testing.assert_array_equal(host(l), want_l)
+            o2, l2, h2 = kvh.tokenize_hash(text, SEED, 256, stream=st)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(host(h2), G["hashes"])
+            ro = kvh.frag_offsets(frags, stream=st)
+            np.testing.assert_array_equal(host(ro), G["rec_offs"])
+            ro2, hh = kvh.frags_hash(frags, SEED, stream=st)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(host(hh), G["hashes"])
