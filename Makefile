@@ -12,7 +12,7 @@ HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/
             raikv_amd/csrc/ht_pos.hpp raikv_amd/csrc/bs_prelude.hpp raikv_amd/csrc/bs_aes.hpp \
             raikv_amd/csrc/bs_meow.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
-CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/paths_gpu tools/copy_peak
+CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/paths_gpu tools/copy_peak tools/fetch_calib
 
 all: $(LIB) oracle cpptests
 
@@ -60,6 +60,10 @@ tests/cpp/e2e_host: tests/cpp/e2e_host.cpp $(LIB) include/kvh.h
 
 # measurement: the box's achievable streaming rate for bench.py's roofline
 tools/copy_peak: tools/copy_peak.hip
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
+
+# measurement: FETCH_SIZE calibration for gather access patterns
+tools/fetch_calib: tools/fetch_calib.hip
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
 # TEST ONLY: the bitsliced Meow chain run on the host against the oracle

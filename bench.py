@@ -392,7 +392,7 @@ def main():
     from raikv_amd import dist as kdist
     rank, world, local = kdist.env_ranks()
     kdist.init(world)  # gloo control plane only: barrier + max time
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))  # one GPU per rank; ranks share a GPU only where fewer are visible
     import raikv_amd as kvh
     from raikv_amd.workload import STATIC_SEED, C3_SEEDS, zipf_lengths, offsets_from_lengths
 

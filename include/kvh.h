@@ -144,6 +144,15 @@ int kvh_device_free(void *p);
  * Drop-ins for include/raikv/key_hash.h (host pointers, synchronous).  They
  * execute on the current GPU through kvh_meow128_var_seeded; results are
  * bit-identical to the reference.  Return 0 or a negative error.
+ *
+ * LATENCY: each call is a host->device copy, a kernel and a device->host
+ * copy, serialised behind one staging buffer: tens of microseconds per call
+ * against the reference CPU's 5-20 ns per key.  They exist for API
+ * completeness and for tests; never call them per key in a hot loop (e.g.
+ * KeyCtx::set_key_hash, key_ctx.cpp:98-105).  Batch instead: hash a socket
+ * or shm batch with kvh_meow128_fixed_host / kvh_meow128_var_host (or the
+ * device entries) and hand each (h1, h2) to KeyCtx::set_hash
+ * (key_ctx.h:188-192), INTEGRATION.md §3.
  * ------------------------------------------------------------------- */
 /* key_hash.h:61 kv_hash_meow128 */
 int kvh_hash_meow128(const void *p, size_t sz, uint64_t *h1, uint64_t *h2);
@@ -281,11 +290,17 @@ int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
                                 void *pos, uint32_t flags, void *stream);
 
 /* ---------------------------------------------------------------------
- * Batch order by table position: kv_ht_radix_sort
- * (src/radix_sort.cpp:31-41) + ctest.c:96-104's duplicate marking.
- * Order: by ht_mod(h1) ascending (the reference's order); equal slots,
- * which the reference leaves in unspecified order, are ordered by
- * (h1 << 1, h1, h2) so that all duplicates are adjacent.
+ * Batch order by table position: the role of
+ * kv_ht_radix_sort (src/radix_sort.cpp:31-41) + ctest.c:96-104's duplicate
+ * marking.  CONTRACT: the slot sequence equals kv_ht_radix_sort's (ht_mod(h1)
+ * ascending) and every slot holds the same rows; the order WITHIN a slot and
+ * the duplicate count differ.  The reference's in-place bit-pivot sort
+ * (include/raikv/radix_sort.h:31-33) leaves equal slots in an input-dependent
+ * order, so ctest's adjacent-pair scan finds only the duplicates that land
+ * next to each other; here equal slots are ordered by (h1 << 1, h1, h2), all
+ * duplicates are adjacent and the count is the true one (reference fixtures:
+ * 99 vs 500 on the 600-entry table, 992 vs 1000 on a 64 MiB one; tests/golden/
+ * sort_*.npz).  Not a bit-identical drop-in for kv_ht_radix_sort.
  * ------------------------------------------------------------------- */
 #define KVH_DEDUP     0x8u  /* zero h1 of an element equal (h1,h2) to its successor, count it */
 
@@ -304,9 +319,10 @@ int kvh_ht_sort(const uint64_t *hashes, const uint64_t *items, size_t n,
                 const kvh_ht_geom_t *geom, uint64_t *hashes_out,
                 uint64_t *items_out, uint64_t *dup_count, uint32_t flags,
                 void *scratch, size_t scratch_bytes, void *stream);
-/* host drop-in for kv_ht_radix_sort(ar, ar_size, ht) (radix_sort.h:19-20):
+/* host form of kv_ht_radix_sort(ar, ar_size, ht) (radix_sort.h:19-20):
  * sorts ar[] in place (synchronous, on the current GPU); the table is
- * given by its geometry. */
+ * given by its geometry.  Same slot order as the reference; tie order as
+ * described above (the reference's is not reproduced). */
 int kvh_ht_radix_sort(kvh_ht_sort_t *ar, uint32_t ar_size,
                       const kvh_ht_geom_t *geom);
 

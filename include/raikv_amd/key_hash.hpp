@@ -124,6 +124,26 @@ inline void hash_multiseed(const void* keys, uint32_t key_len, size_t n, const s
         "kvh::hash_multiseed");
 }
 
+// ---- keys and hashes in HOST memory (socket / shm batches): the PCIe-inclusive
+// pipelines, synchronous.  devices empty: the current device; else one host
+// thread per listed device, each writing its disjoint slice of out.
+inline void hash_fixed_host(const void* keys, uint32_t key_len, size_t n, const HashSeed& hs, uint64_t* out,
+                            bool fixup = true, const std::vector<int>& devices = {}) {
+  const uint32_t f = fixup ? KVH_FIXUP : 0u;
+  check(devices.empty() ? kvh_meow128_fixed_host(keys, key_len, n, hs.hash1, hs.hash2, out, f)
+                        : kvh_meow128_fixed_host_multi(keys, key_len, n, hs.hash1, hs.hash2, out, f, devices.data(),
+                                                       (int)devices.size()),
+        "kvh::hash_fixed_host");
+}
+inline void hash_var_host(const void* keys, const uint64_t* offsets, size_t n, const HashSeed& hs, uint64_t* out,
+                          bool fixup = true, const std::vector<int>& devices = {}) {
+  const uint32_t f = fixup ? KVH_FIXUP : 0u;
+  check(devices.empty() ? kvh_meow128_var_host(keys, offsets, n, hs.hash1, hs.hash2, out, f)
+                        : kvh_meow128_var_host_multi(keys, offsets, n, hs.hash1, hs.hash2, out, f, devices.data(),
+                                                     (int)devices.size()),
+        "kvh::hash_var_host");
+}
+
 // ---- the calls either side of the hash, same shape
 
 // Table geometry from the map's header fields (shm_ht.h:143-157, ht_init.cpp:117-156).

@@ -48,6 +48,36 @@ int main() {
   CHECK(d2h(h1, 2 * n) == d2h(h2, 2 * n), "fused hashes differ");
   CHECK(d2h(p1, pk * n) == d2h(p2, pk * n), "fused positions differ");
 
+  // host-memory pipelines (kvh::hash_*_host, one device and a repeated
+  // device list) == the device-resident kernels
+  {
+    std::vector<uint64_t> hh(2 * n), hm(2 * n);
+    kvh::hash_fixed_host(keys.data(), L, n, hs, hh.data(), true);
+    kvh::hash_fixed_host(keys.data(), L, n, hs, hm.data(), true, {0, 0, 0});
+    const std::vector<uint64_t> dh = d2h(h2, 2 * n);
+    CHECK(hh == dh, "hash_fixed_host differs from hash_fixed");
+    CHECK(hm == dh, "hash_fixed_host over {0,0,0} differs");
+    const size_t nv = 50001;
+    std::vector<uint64_t> off(nv + 1, 0);
+    for (size_t i = 0; i < nv; i++) off[i + 1] = off[i] + 8 + rng() % 249;
+    std::vector<uint8_t> vk(off[nv]);
+    for (auto& b : vk) b = (uint8_t)rng();
+    uint8_t* dvk = dalloc<uint8_t>(vk.size());
+    uint64_t* doff = dalloc<uint64_t>(nv + 1);
+    uint64_t* dvh = dalloc<uint64_t>(2 * nv);
+    h2d(dvk, vk);
+    h2d(doff, off);
+    kvh::hash_var(dvk, doff, nv, hs, dvh, true);
+    (void)hipDeviceSynchronize();
+    std::vector<uint64_t> vh(2 * nv), vm(2 * nv);
+    kvh::hash_var_host(vk.data(), off.data(), nv, hs, vh.data(), true);
+    kvh::hash_var_host(vk.data(), off.data(), nv, hs, vm.data(), true, {0, 0});
+    const std::vector<uint64_t> want = d2h(dvh, 2 * nv);
+    CHECK(vh == want, "hash_var_host differs from hash_var");
+    CHECK(vm == want, "hash_var_host over {0,0} differs");
+    (void)hipFree(dvk); (void)hipFree(doff); (void)hipFree(dvh);
+  }
+
   // f2: table order by home slot, duplicates adjacent and counted
   std::vector<uint64_t> hh = d2h(h2, 2 * n);
   for (size_t i = 0; i < 100; i++) {  // 100 duplicated pairs

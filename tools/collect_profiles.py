@@ -8,20 +8,29 @@ src, rnd = sys.argv[1], sys.argv[2]
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
-HOT = ("k_fixed", "k_var", "k_generic", "k_fixed_ms", "k_fixed_dma")
+HOT = ("k_fixed", "k_var", "k_generic", "k_fixed_ms")
 HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",), "f4": ("k_crc_fixed",), "f4v": ("k_crc_var",),
               "c2": ("k_var6",), "c3": ("k_fixed_lanes",)}
 # configs whose unit of work is one call of several kernels: (kernel name parts,
 # calls in the PMC run (run_kernel.py --reps), calls in the traced bench run (W + K))
 MULTI = {"f2": (("k_sort", "onesweep", "radix", "rocprim"), 5, 200),
          "f3": (("k_tok", "k_spans"), 5, 200)}
+# configs whose hot kernel gathers 16-byte key pieces in length-sorted windows: keys per launch
+GATHER = {"c2": 100_000_000}
+calib = os.path.join(src, "calib", "fetch_calib.json")
+GATHER_FACTOR = 1.0
+if os.path.exists(calib):
+    for k, v in json.load(open(calib)).items():
+        if "k_gather<16>" in k:
+            GATHER_FACTOR = (4 << 30) / (v["FETCH_SIZE"] * 1024)
+    shutil.copy(calib, os.path.join(dst, "fetch_calib.json"))
 tpath = os.path.join(root, "profiles", "pmc_traffic.json")
 spath = os.path.join(dst, "summary.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
 summary = json.load(open(spath)) if os.path.exists(spath) else {}
 for c in sorted(os.listdir(src)):
     d = os.path.join(src, c)
-    if not os.path.isdir(d):
+    if not os.path.isdir(d) or c == "calib":
         continue
     shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{c}_kernel_stats.csv"))
     shutil.copy(os.path.join(d, "pmc_summary.json"), os.path.join(dst, f"{c}_pmc_summary.json"))
@@ -47,10 +56,21 @@ for c in sorted(os.listdir(src)):
     pmc = json.load(open(os.path.join(d, "pmc_summary.json")))
     for k, v in pmc.items():
         if any(h in k for h in hot_names) and "FETCH_SIZE" in v:
-            hbm = v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024
+            if c in GATHER:
+                # variable-length kernels: the u64 offsets stream coalesced (FETCH_SIZE = 1/2 of
+                # the bytes, the guide's rule), the key bytes are 16-byte gathers in sorted
+                # windows, calibrated on a known byte count by tools/fetch_calib.hip
+                # (profiles/<round>/fetch_calib.json: true/FETCH_SIZE = GATHER_FACTOR)
+                offs_b = 8 * (GATHER[c] + 1)
+                hbm = (v["FETCH_SIZE"] * 1024 - offs_b / 2) * GATHER_FACTOR + offs_b + v["WRITE_SIZE"] * 1024
+                how = (f"(FETCH_SIZE x1024 - offsets/2) x {GATHER_FACTOR:.3f} (16-B gather calibration) + "
+                       f"offsets + WRITE_SIZE x1024")
+            else:
+                hbm = v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024
+                how = "FETCH_SIZE x2 + WRITE_SIZE, x1024"
             traffic[c] = {"hbm_bytes_per_launch": hbm, "kernel": k,
                           "fetch_size_kb": v["FETCH_SIZE"], "write_size_kb": v["WRITE_SIZE"],
-                          "source": f"profiles/{rnd}/{c}_pmc_summary.json (FETCH_SIZE x2 + WRITE_SIZE, x1024)"}
+                          "source": f"profiles/{rnd}/{c}_pmc_summary.json ({how})"}
             clk = None
             if hot and "GRBM_GUI_ACTIVE" in v:
                 clk = v["GRBM_GUI_ACTIVE"] / 8 / (float(hot[0]["AverageNs"]) * 1e-9) / 1e9

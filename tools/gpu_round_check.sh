@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round check on the GPU box: full gpu test suite, smoke, the driver's bench
+# protocol per config, and a 2-rank bench (the N>1 path, both ranks on the
+# box's GPU).  usage: tools/gpu_round_check.sh <outdir> "<configs>"
+set -o pipefail
+O=${1:-gpurun_out/round}; CFGS=${2:-c1}
+cd ${GRAFT_REPO_ROOT:-.}; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/gpu_tests.txt 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/gpu_tests.txt; tail -2 $O/gpu_tests.txt; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || exit 1
+for c in $CFGS; do
+  timeout -k 10 400 python3 bench.py --config $c --steps 20 --warmup 5 > $O/bench_$c.json 2> $O/bench_$c.log || exit 1
+  echo "== $c"; cut -c1-300 $O/bench_$c.json
+done
+timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 20 --warmup 5 > $O/bench_c1_2ranks.json 2> $O/bench_c1_2ranks.log || exit 1
+cut -c1-300 $O/bench_c1_2ranks.json

@@ -10,7 +10,8 @@ export TMPDIR=/tmp
 mkdir -p $OUT
 for c in $CFGS; do
   mkdir -p $OUT/$c
-  B="python3 bench.py --config $c --no-cpu-baseline"
+  # the driver's protocol (W = 5, K = 20, after the settle phase); no e2e / copy-probe legs
+  B="python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-copy-peak"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- $B > $OUT/$c/bench.json 2> $OUT/$c/trace.err || exit 1
   R="python3 tools/run_kernel.py --config $c --reps 5"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- $R > $OUT/$c/fetch.log 2>&1 || exit 1
@@ -18,3 +19,10 @@ for c in $CFGS; do
   timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU --output-format csv -d $OUT/$c/sq -o run -- $R > $OUT/$c/sq.log 2>&1 || exit 1
   python3 tools/pmc_summary.py $OUT/$c/fetch $OUT/$c/write $OUT/$c/sq > $OUT/$c/pmc_summary.json || exit 1
 done
+if [ -x tools/fetch_calib ]; then
+  mkdir -p $OUT/calib
+  for w in stream gather16 gather4; do
+    timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/calib/$w -o run -- tools/fetch_calib $w 3 > $OUT/calib/$w.log 2>&1 || exit 1
+  done
+  python3 tools/pmc_summary.py $OUT/calib/stream $OUT/calib/gather16 $OUT/calib/gather4 > $OUT/calib/fetch_calib.json || exit 1
+fi
