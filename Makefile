@@ -14,7 +14,9 @@ HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/
 
 CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/paths_gpu tools/copy_peak tools/fetch_calib
 
-all: $(LIB) oracle cpptests
+KV_LIB   := raikv_amd/libkvh_kv.so
+
+all: $(LIB) $(KV_LIB) oracle cpptests
 
 # one object per translation unit so `make -j` compiles them in parallel
 raikv_amd/csrc/%.o: raikv_amd/csrc/%.hip $(HDRS)
@@ -22,6 +24,11 @@ raikv_amd/csrc/%.o: raikv_amd/csrc/%.hip $(HDRS)
 
 $(LIB): $(OBJS) raikv_amd/csrc/kvh.map
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(OBJS)
+
+# link-compatible kv_* Meow symbols (include/kvh_kv.h) over libkvh.so
+$(KV_LIB): raikv_amd/csrc/kv_compat.cpp raikv_amd/csrc/kv_compat.map include/kvh_kv.h include/kvh.h $(LIB)
+	g++ -O2 -std=c++17 -fPIC -shared $(INC) -Wl,--version-script=raikv_amd/csrc/kv_compat.map -o $@ $< \
+	    -L raikv_amd -lkvh -Wl,-rpath,'$$ORIGIN'
 
 # Research build (NOT the product): the same sources with -DKVH_EXPERIMENTS,
 # which adds the superseded kernels and the ablation builds (outputs that are
@@ -71,7 +78,7 @@ tests/cpp/bs_host_test: tests/cpp/bs_host_test.cpp raikv_amd/csrc/bs_aes.hpp rai
 	g++ -O2 -std=c++17 -o $@ $< -Loracle -loracle -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 clean:
-	rm -f $(LIB) $(OBJS) $(CPP_TESTS) $(EXP_LIB) $(EXP_OBJS)
+	rm -f $(LIB) $(KV_LIB) $(OBJS) $(CPP_TESTS) $(EXP_LIB) $(EXP_OBJS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle cpptests clean experiments

@@ -1,0 +1,96 @@
+// kv_compat.cpp -- link-compatible kv_* Meow symbols over the C-ABI
+// (libkvh_kv.so).  A raikv build that drops src/key_hash.c's Meow family and
+// links this library instead keeps every call site of
+// include/raikv/key_hash.h:59-130 unchanged: same names, same argument
+// meaning, same x[] layouts, void returns.  Each call runs on the current
+// GPU through libkvh.so's host drop-ins (one device round trip per call: the
+// latency trap include/kvh.h documents above them -- this library is for
+// link compatibility and tests; batches belong on kvh_meow128_*_host /
+// KeyCtx::set_hash).
+//
+// The reference functions have no error path.  A device error here cannot be
+// returned, and a silently wrong hash would corrupt a table, so it aborts the
+// process with the HIP error string.  HMAC-Meow (key_hash.h:100-109) is a
+// different function and out of scope.
+#include <stdio.h>
+#include <stdlib.h>
+#include "kvh_kv.h"
+#include "kvh.h"
+
+static void must(int rc, const char* what) {
+  if (rc != 0) {
+    fprintf(stderr, "libkvh_kv: %s failed: %d (%s)\n", what, rc, kvh_strerror(rc));
+    abort();
+  }
+}
+
+extern "C" {
+
+void kv_hash_meow128(const void* p, size_t sz, uint64_t* h1, uint64_t* h2) {
+  must(kvh_hash_meow128(p, sz, h1, h2), "kv_hash_meow128");
+}
+
+uint64_t kv_hash_meow64(const void* p, size_t sz, uint64_t seed) {
+  const uint64_t h = kvh_hash_meow64(p, sz, seed);
+  must(kvh_last_error(), "kv_hash_meow64");
+  return h;
+}
+
+void kv_hash_meow128_vec(const meow_vec_t* vec, size_t vec_sz, uint64_t* h1, uint64_t* h2) {
+  // meow_vec_t and kvh_meow_vec_t are both {const void *p; size_t sz;}
+  must(kvh_hash_meow128_vec((const kvh_meow_vec_t*)vec, vec_sz, h1, h2), "kv_hash_meow128_vec");
+}
+
+void kv_meow128_init(meow_ctx_t* m, meow_block_t* b, uint64_t k1, uint64_t k2, size_t total_update_sz) {
+  must(kvh_meow128_init((kvh_meow_ctx_t*)m, (kvh_meow_block_t*)b, k1, k2, total_update_sz), "kv_meow128_init");
+}
+
+void kv_meow128_update(meow_ctx_t* m, meow_block_t* b, const void* p, size_t sz) {
+  must(kvh_meow128_update((kvh_meow_ctx_t*)m, (kvh_meow_block_t*)b, p, sz), "kv_meow128_update");
+}
+
+void kv_meow128_final(meow_ctx_t* m, meow_block_t* b, uint64_t* k1, uint64_t* k2) {
+  must(kvh_meow128_final((kvh_meow_ctx_t*)m, (kvh_meow_block_t*)b, k1, k2), "kv_meow128_final");
+}
+
+void kv_meow_test(const void* p, size_t sz, uint64_t* k1, uint64_t* k2) {
+  must(kvh_meow_test(p, sz, k1, k2), "kv_meow_test");
+}
+
+void kv_hash_meow128_2_same_length(const void* p, const void* p2, size_t sz, uint64_t* x4) {
+  must(kvh_hash_meow128_2_same_length(p, p2, sz, x4), "kv_hash_meow128_2_same_length");
+}
+
+void kv_hash_meow128_4_same_length_a(const void** p, size_t sz, uint64_t* x) {
+  must(kvh_hash_meow128_4_same_length_a(p, sz, x), "kv_hash_meow128_4_same_length_a");
+}
+
+void kv_hash_meow128_8_same_length_a(const void** p, size_t sz, uint64_t* x) {
+  must(kvh_hash_meow128_8_same_length_a(p, sz, x), "kv_hash_meow128_8_same_length_a");
+}
+
+void kv_hash_meow128_4_same_length(const void* p, const void* p2, const void* p3, const void* p4, size_t sz,
+                                   uint64_t* x) {
+  must(kvh_hash_meow128_4_same_length(p, p2, p3, p4, sz, x), "kv_hash_meow128_4_same_length");
+}
+
+void kv_hash_meow128_4_same_length_4_seed(const void* p, const void* p2, const void* p3, const void* p4, size_t sz,
+                                          uint64_t* x) {
+  must(kvh_hash_meow128_4_same_length_4_seed(p, p2, p3, p4, sz, x), "kv_hash_meow128_4_same_length_4_seed");
+}
+
+void kv_hash_meow128_8_same_length(const void* p, const void* p2, const void* p3, const void* p4, const void* p5,
+                                   const void* p6, const void* p7, const void* p8, size_t sz, uint64_t* x) {
+  must(kvh_hash_meow128_8_same_length(p, p2, p3, p4, p5, p6, p7, p8, sz, x), "kv_hash_meow128_8_same_length");
+}
+
+void kv_hash_meow128_2_diff_length(const void* p, size_t sz, const void* p2, size_t sz2, uint64_t* x) {
+  must(kvh_hash_meow128_2_diff_length(p, sz, p2, sz2, x), "kv_hash_meow128_2_diff_length");
+}
+
+void kv_hash_meow128_4_diff_length(const void* p, size_t sz, const void* p2, size_t sz2, const void* p3,
+                                   size_t s3, const void* p4, size_t s4, uint64_t* x) {
+  must(kvh_hash_meow128_4_diff_length(p, sz, p2, sz2, p3, s3, p4, s4, x), "kv_hash_meow128_4_diff_length");
+}
+
+}  // extern "C"

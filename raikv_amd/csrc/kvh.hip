@@ -1575,10 +1575,37 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
   }
 }
 
+template <int L, int NT, int U>
+int launch_lanes_v(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
+                   uint32_t flags, hipStream_t st, int cus) {
+  const uint32_t grid = grid_for(n * arity, cus, NT == 4 ? 1 : 2);
+#define KVH_LANES_V(LAv)                                                                                \
+  hipLaunchKernelGGL((k_fixed_lanes<L, NT, true, U, LAv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \
+                     s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13],   \
+                     s[14], s[15])
+  if (arity == 2) KVH_LANES_V(2); else if (arity == 4) KVH_LANES_V(4); else KVH_LANES_V(8);
+#undef KVH_LANES_V
+  return launch_done();
+}
+
 template <int L>
 int launch_lanes_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
                    uint32_t flags, hipStream_t st, int cus) {
   const bool a16 = ((uintptr_t)keys & 15) == 0;
+  if constexpr (L == 32) {  // C3's length: table layout / keys per lane from knobs 0 / 3 (tools/tune.py)
+    const int nt = knob(g_tune_nt), kpl = knob(g_tune_kpl);
+    if (a16 && (nt || kpl)) {
+      switch ((nt ? nt : 2) * 10 + (kpl ? kpl : 2)) {
+        case 22: break;
+        case 21: return launch_lanes_v<L, 2, 1>(keys, n, s, arity, out, flags, st, cus);
+        case 24: return launch_lanes_v<L, 2, 4>(keys, n, s, arity, out, flags, st, cus);
+        case 41: return launch_lanes_v<L, 4, 1>(keys, n, s, arity, out, flags, st, cus);
+        case 42: return launch_lanes_v<L, 4, 2>(keys, n, s, arity, out, flags, st, cus);
+        case 44: return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);
+        default: return set_err(KVH_EINVAL);
+      }
+    }
+  }
   const uint32_t grid = grid_for(n * arity, cus, 2);
 #define KVH_LANES(A16v, LAv)                                                                            \
   hipLaunchKernelGGL((k_fixed_lanes<L, 2, A16v, 2, LAv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \

@@ -66,3 +66,18 @@ def test_cpp_host_mirror_compiles():
                        input=src, text=True, capture_output=True)
     assert r.returncode == 0, r.stderr
     assert subprocess.run([exe]).returncode == 0
+
+
+def test_kv_compat_library_exports_the_meow_family():
+    """libkvh_kv.so (link compatibility with include/raikv/key_hash.h:59-130)
+    exports exactly the kv_* names include/kvh_kv.h declares, and links
+    libkvh.so (it hashes on the GPU through the C-ABI)."""
+    lib = os.path.join(ROOT, "raikv_amd", "libkvh_kv.so")
+    assert os.path.exists(lib), "build it with make"
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "kvh_kv.h")).read(), flags=re.S)
+    want = set(re.findall(r"\b(kv_[a-z0-9_]+)\s*\(", src))
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    got = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    assert got == want and len(want) == 15, sorted(got ^ want)
+    deps = subprocess.run(["ldd", lib], capture_output=True, text=True).stdout
+    assert "libkvh.so" in deps

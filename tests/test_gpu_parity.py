@@ -399,3 +399,38 @@ def test_partition_vectors_against_reference(kvh, variant):
         assert lib.kvh_hash_meow128_4_diff_length(cb, n, C.c_void_p(base + n), m - n, C.c_void_p(base + m), o - m,
                                                   C.c_void_p(base + o), 128 - o, x) == 0
         assert list(x) == [int(v) for v in d[t]], (n, m, o)
+
+
+def test_kv_compat_symbols_against_reference_vectors(kvh):
+    """libkvh_kv.so's kv_* symbols (same names and signatures as
+    include/raikv/key_hash.h) reproduce the reference's vectors on the GPU."""
+    lib = C.CDLL(os.path.join(ROOT, "raikv_amd", "libkvh_kv.so"))
+    U = C.c_uint64
+    lib.kv_hash_meow128.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(U), C.POINTER(U)]
+    lib.kv_hash_meow128.restype = None
+    lib.kv_hash_meow64.argtypes = [C.c_void_p, C.c_size_t, U]
+    lib.kv_hash_meow64.restype = U
+    for k in VEC["kat"]:
+        key = bytes.fromhex(k["key_hex"])
+        a, b = U(k["seed"][0]), U(k["seed"][1])
+        lib.kv_hash_meow128(C.create_string_buffer(key, max(1, len(key))), len(key), C.byref(a), C.byref(b))
+        assert "%016x:%016x" % (a.value, b.value) == k["h"]
+    for m in VEC["meow64"]:
+        key = bytes.fromhex(m["key_hex"])
+        assert lib.kv_hash_meow64(C.create_string_buffer(key, max(1, len(key))), len(key), U(m["seed"])) == m["h"]
+    r = VEC["variants"]["results"]
+    keys = [k.encode() for k in VEC["variants"]["keys"]]
+    s1, s2 = VEC["variants"]["seed"]
+    L = len(keys[0])
+    bufs = [C.create_string_buffer(k, L) for k in keys]
+    x = (U * 8)(*([s1, s2] * 4))
+    lib.kv_hash_meow128_4_diff_length(bufs[0], C.c_size_t(L), bufs[1], C.c_size_t(L), bufs[2], C.c_size_t(L),
+                                      bufs[3], C.c_size_t(L), x)
+    assert list(x) == r["4_diff"]
+    x = (U * 8)(*r["4_same_4_seed"]["seeds"])
+    lib.kv_hash_meow128_4_same_length_4_seed(bufs[0], bufs[1], bufs[2], bufs[3], C.c_size_t(L), x)
+    assert list(x) == r["4_same_4_seed"]["x"]
+    for i in range(4):
+        a, b = U(s1), U(s2)
+        lib.kv_meow_test(bufs[i], C.c_size_t(L), C.byref(a), C.byref(b))
+        assert [a.value, b.value] == r["stream"][i]
