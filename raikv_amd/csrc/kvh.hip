@@ -1592,10 +1592,14 @@ template <int L>
 int launch_lanes_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
                    uint32_t flags, hipStream_t st, int cus) {
   const bool a16 = ((uintptr_t)keys & 15) == 0;
-  if constexpr (L == 32) {  // C3's length: table layout / keys per lane from knobs 0 / 3 (tools/tune.py)
+  if constexpr (L == 32) {
+    // C3's length: Td0..Td3 in LDS (no rotates, one 16-wave workgroup per CU)
+    // and 2 keys per lane by default -- 118 vs 112 G hash/s for Td0/Td1 with
+    // two workgroups per CU (tools/tune.py, profiles/r02/c3_layout_ab.txt);
+    // knobs 0 / 3 select the others
     const int nt = knob(g_tune_nt), kpl = knob(g_tune_kpl);
-    if (a16 && (nt || kpl)) {
-      switch ((nt ? nt : 2) * 10 + (kpl ? kpl : 2)) {
+    if (a16) {
+      switch ((nt ? nt : 4) * 10 + (kpl ? kpl : 2)) {
         case 22: break;
         case 21: return launch_lanes_v<L, 2, 1>(keys, n, s, arity, out, flags, st, cus);
         case 24: return launch_lanes_v<L, 2, 4>(keys, n, s, arity, out, flags, st, cus);
