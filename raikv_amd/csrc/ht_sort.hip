@@ -23,11 +23,18 @@
 //   4. k_sort_place  hashes_out / items_out[j] = record idx[j] (one random
 //                    read per element)
 //   5. k_sort_fixup  runs of equal sorted prefix (equal slot and equal top
-//                    h1 bits: ≈3 % of the elements, and duplicates)
-//                    insertion-sorted in the outputs by the full comparator
-//                    (O(run) when the run is all equal): the order is a full
-//                    64-bit sort's; with KVH_DEDUP the h1 of an element equal
-//                    to its successor set to 0 and counted
+//                    h1 bits: ≈3 % of the elements, and duplicates) of at
+//                    most kShortRun elements insertion-sorted in the outputs
+//                    by the full comparator: the order is a full 64-bit
+//                    sort's; with KVH_DEDUP the h1 of an element equal to its
+//                    successor set to 0 and counted.  Longer runs (only
+//                    non-uniform "hashes" or mass duplicates make them) are
+//                    listed for
+//   6. k_sort_long   one workgroup per listed run: a bitonic sort network
+//                    over the run's records (O(R log² R) work, R / 256-way
+//                    parallel, instead of one thread's O(R²) insertion sort),
+//                    the input order as the last tie-break so it stays the
+//                    stable order insertion sort gives; same dedup
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -45,6 +52,8 @@ using namespace kvh::rt;
 namespace {
 
 constexpr int kSB = 256;
+// runs longer than this go to k_sort_long (insertion sort is O(R²) per thread)
+constexpr uint64_t kShortRun = 64;
 
 // (h1, h2, item) padded to 32 bytes: one aligned random read per record
 struct __attribute__((aligned(16))) Rec {
@@ -65,8 +74,10 @@ __device__ __forceinline__ bool rec_less(uint64_t a1, uint64_t a2, uint64_t b1, 
 template <class K, bool PACK>
 __global__ void __launch_bounds__(kSB)
 k_sort_keys(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, HtGeom g,
-            uint32_t sbits, uint32_t lo, K* __restrict__ key, uint32_t* __restrict__ idx, Rec* __restrict__ rec) {
+            uint32_t sbits, uint32_t lo, K* __restrict__ key, uint32_t* __restrict__ idx, Rec* __restrict__ rec,
+            uint32_t* __restrict__ nlong) {
   const uint64_t i = (uint64_t)blockIdx.x * kSB + threadIdx.x;
+  if (i == 0) *nlong = 0;  // k_sort_fixup's long-run list, empty per call
   if (i >= n) return;
   const uint64_t h1 = h[2 * i];
   const uint64_t slot = ht_mod(g, h1);
@@ -103,22 +114,40 @@ k_sort_place(const uint64_t* __restrict__ h, const Rec* __restrict__ rec, const 
   if (items_out) items_out[j] = it;
 }
 
-// Runs of equal sorted prefix (equal slot and top h1 bits) are put in the
-// full order (h1 << 1, h1, h2) by insertion sort -- O(run) for an all-equal
-// run -- and, with dedup, every element equal (h1, h2) to its successor gets
-// h1 = 0 (ctest.c:96-104).  Equal pairs share a prefix, so runs are the only
-// place duplicates occur.  Grid-stride; one atomic per workgroup.
+__device__ __forceinline__ uint32_t block_sum(uint32_t d, uint32_t* wsum) {
+  for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = d;
+  __syncthreads();
+  uint32_t t = 0;
+  for (int w = 0; w < kSB / 64; w++) t += wsum[w];
+  __syncthreads();
+  return t;
+}
+
+// Runs of equal sorted prefix (equal slot and top h1 bits) of at most
+// kShortRun elements are put in the full order (h1 << 1, h1, h2) by
+// insertion sort -- stable, so exact duplicates keep the input order the
+// radix sort left them in -- and, with dedup, every element equal (h1, h2)
+// to its successor gets h1 = 0 (ctest.c:96-104).  Equal pairs share a
+// prefix, so runs are the only place duplicates occur.  A longer run's start
+// is appended to runs[] for k_sort_long (at most kShortRun + 1 key reads per
+// thread here).  Grid-stride; one atomic per workgroup.
 template <class K>
 __global__ void __launch_bounds__(kSB)
 k_sort_fixup(const K* __restrict__ key, uint64_t n, uint64_t* __restrict__ h, uint64_t* __restrict__ items,
-             uint32_t dedup, unsigned long long* __restrict__ dups) {
+             uint32_t dedup, unsigned long long* __restrict__ dups, uint32_t* __restrict__ nlong,
+             uint32_t* __restrict__ runs) {
   __shared__ uint32_t wsum[kSB / 64];
   uint32_t d = 0;
   const uint64_t stride = (uint64_t)gridDim.x * kSB;
   for (uint64_t j = (uint64_t)blockIdx.x * kSB + threadIdx.x; j + 1 < n; j += stride) {
     if (key[j + 1] != key[j] || (j > 0 && key[j - 1] == key[j])) continue;  // run starts only
     uint64_t e = j + 2;
-    while (e < n && key[e] == key[j]) e++;
+    while (e < n && e - j <= kShortRun && key[e] == key[j]) e++;
+    if (e - j > kShortRun) {
+      runs[atomicAdd(nlong, 1u)] = (uint32_t)j;
+      continue;
+    }
     for (uint64_t a = j + 1; a < e; a++) {  // insertion sort of [j, e)
       const uint64_t v1 = h[2 * a], v2 = h[2 * a + 1], vi = items ? items[a] : 0;
       uint64_t b = a;
@@ -140,21 +169,110 @@ k_sort_fixup(const K* __restrict__ key, uint64_t n, uint64_t* __restrict__ h, ui
     }
   }
   if (dedup && dups) {
-    for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = d;
+    const uint32_t t = block_sum(d, wsum);
+    if (threadIdx.x == 0 && t) atomicAdd(dups, (unsigned long long)t);
+  }
+}
+
+// record order within a long run: the full comparator, then the position the
+// radix sort left the element at (the stable tie-break), kept in Rec::pad
+__device__ __forceinline__ bool run_less(const Rec& a, const Rec& b) {
+  if (a.h1 != b.h1 || a.h2 != b.h2) return rec_less(a.h1, a.h2, b.h1, b.h2);
+  return a.pad < b.pad;
+}
+
+// One workgroup per long run (grid-stride over the list): find the run's end
+// (256 keys per step), copy it to rec[j, e) with its positions (the records
+// k_sort_place read are consumed by then; stream order), sort that in place
+// with an all-ascending bitonic network -- every compare-exchange puts the
+// smaller record at the lower index, so the pad to a power of two is virtual:
+// a comparator whose upper index is past the run is a no-op -- then write it
+// back with the dedup marks.  Already-ordered runs (e.g. all duplicates) skip
+// the network.
+template <class K>
+__global__ void __launch_bounds__(kSB)
+k_sort_long(const K* __restrict__ key, uint64_t n, uint64_t* __restrict__ h, uint64_t* __restrict__ items,
+            Rec* __restrict__ rec, uint32_t dedup, unsigned long long* __restrict__ dups,
+            const uint32_t* __restrict__ nlong, const uint32_t* __restrict__ runs) {
+  __shared__ uint32_t wsum[kSB / 64];
+  __shared__ uint64_t s_end;
+  const uint32_t count = *nlong;
+  const uint32_t tid = threadIdx.x;
+  uint32_t d = 0;
+  for (uint32_t r = blockIdx.x; r < count; r += gridDim.x) {
+    const uint64_t j = runs[r];
+    const K kj = key[j];
+    if (tid == 0) s_end = n;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t t = 0;
-      for (int w = 0; w < kSB / 64; w++) t += wsum[w];
-      if (t) atomicAdd(dups, (unsigned long long)t);
+    for (uint64_t base = j + 1 + kShortRun; base < n; base += kSB) {
+      const uint64_t x = base + tid;
+      const bool stop = x < n && key[x] != kj;
+      if (stop) atomicMin((unsigned long long*)&s_end, (unsigned long long)x);
+      __syncthreads();
+      const bool done = s_end < n;
+      __syncthreads();
+      if (done) break;
     }
+    const uint64_t len = s_end - j;
+    Rec* R = rec + j;
+    uint32_t unordered = 0;
+    for (uint64_t t = tid; t < len; t += kSB) {
+      Rec v;
+      v.h1 = h[2 * (j + t)];
+      v.h2 = h[2 * (j + t) + 1];
+      v.item = items ? items[j + t] : 0;
+      v.pad = t;
+      R[t] = v;
+      if (t + 1 < len) unordered |= rec_less(h[2 * (j + t + 1)], h[2 * (j + t + 1) + 1], v.h1, v.h2);
+    }
+    if (block_sum(unordered, wsum)) {
+      uint64_t P = 1;
+      while (P < len) P <<= 1;
+      for (uint64_t k = 2; k <= P; k <<= 1) {
+        for (uint64_t jj = k >> 1; jj > 0; jj >>= 1) {
+          for (uint64_t t = tid; t < P / 2; t += kSB) {
+            const uint64_t off = t & (jj - 1);
+            uint64_t a, b;
+            if (jj == (k >> 1)) {  // first step of the merge: the mirror comparator
+              a = (t / jj) * k + off;
+              b = (t / jj) * k + k - 1 - off;
+            } else {
+              a = (t / jj) * 2 * jj + off;
+              b = a + jj;
+            }
+            if (b >= len) continue;
+            const Rec x = R[a], y = R[b];
+            if (run_less(y, x)) { R[a] = y; R[b] = x; }
+          }
+          __syncthreads();
+        }
+      }
+    }
+    __syncthreads();
+    for (uint64_t t = tid; t < len; t += kSB) {
+      const Rec v = R[t];
+      bool dup = false;
+      if (dedup && t + 1 < len) {
+        const Rec w = R[t + 1];
+        dup = v.h1 == w.h1 && v.h2 == w.h2;
+      }
+      d += dup;
+      h[2 * (j + t)] = dup ? 0 : v.h1;
+      h[2 * (j + t) + 1] = v.h2;
+      if (items) items[j + t] = v.item;
+    }
+    __syncthreads();
+  }
+  if (dedup && dups) {
+    const uint32_t t = block_sum(d, wsum);
+    if (tid == 0 && t) atomicAdd(dups, (unsigned long long)t);
   }
 }
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct SortLayout {
-  size_t key_in, key_out, idx_in, idx_out, rec, tmp, tmp_bytes, total;
+  size_t key_in, key_out, idx_in, idx_out, rec, runs, tmp, tmp_bytes, total;
 };
 
 int sort_layout(size_t n, SortLayout* L) {
@@ -173,6 +291,7 @@ int sort_layout(size_t n, SortLayout* L) {
   L->idx_in = o; o += al256(4 * n);
   L->idx_out = o; o += al256(4 * n);
   L->rec = o; o += al256(sizeof(Rec) * n);
+  L->runs = o; o += al256(4 * (n / (kShortRun + 1) + 2));  // count, then run starts
   L->tmp = o; o += al256(tmp);
   L->tmp_bytes = tmp;
   L->total = o;
@@ -207,6 +326,8 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   uint32_t* iin = (uint32_t*)(s + L.idx_in);
   uint32_t* iout = (uint32_t*)(s + L.idx_out);
   Rec* rec = (Rec*)(s + L.rec);
+  uint32_t* nlong = (uint32_t*)(s + L.runs);
+  uint32_t* runs = nlong + 1;
   HtGeom g;
   g.size = geom->ht_size;
   g.mask = geom->ht_mod_mask;
@@ -235,6 +356,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   int cus = 0;
   if ((rc = device_cus(&cus))) return rc;
   const uint32_t fgrid = (uint32_t)std::min<uint64_t>(grid, (uint64_t)cus * 8);
+  const uint32_t lgrid = (uint32_t)cus * 2;  // long runs: one workgroup each, grid-stride
   size_t tb = L.tmp_bytes;
   hipError_t e;
   if (k32) {
@@ -242,10 +364,10 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
     uint32_t* k32out = (uint32_t*)kout;
     if (items)
       hipLaunchKernelGGL((k_sort_keys<uint32_t, true>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
-                         sb, lo, k32in, iin, rec);
+                         sb, lo, k32in, iin, rec, nlong);
     else
       hipLaunchKernelGGL((k_sort_keys<uint32_t, false>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
-                         sb, lo, k32in, iin, rec);
+                         sb, lo, k32in, iin, rec, nlong);
     if ((rc = launch_done())) return rc;
     e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, k32in, k32out, iin, iout, n, 0u, nb, st);
     if (e != hipSuccess) return hip_err(e);
@@ -253,15 +375,18 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                        (uint64_t)n, h_out, items_out);
     if ((rc = launch_done())) return rc;
     hipLaunchKernelGGL((k_sort_fixup<uint32_t>), dim3(fgrid), dim3(kSB), 0, st, (const uint32_t*)k32out, (uint64_t)n,
-                       h_out, items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count);
+                       h_out, items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, nlong, runs);
+    if ((rc = launch_done())) return rc;
+    hipLaunchKernelGGL((k_sort_long<uint32_t>), dim3(lgrid), dim3(kSB), 0, st, (const uint32_t*)k32out, (uint64_t)n,
+                       h_out, items_out, rec, dedup ? 1u : 0u, (unsigned long long*)dup_count, nlong, runs);
     return launch_done();
   }
   if (items)
     hipLaunchKernelGGL((k_sort_keys<uint64_t, true>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
-                       sb, lo, kin, iin, rec);
+                       sb, lo, kin, iin, rec, nlong);
   else
     hipLaunchKernelGGL((k_sort_keys<uint64_t, false>), dim3(grid), dim3(kSB), 0, st, hashes, items, (uint64_t)n, g,
-                       sb, lo, kin, iin, rec);
+                       sb, lo, kin, iin, rec, nlong);
   if ((rc = launch_done())) return rc;
   e = rocprim::radix_sort_pairs((void*)(s + L.tmp), tb, kin, kout, iin, iout, n, 0u, 64u - lo, st);
   if (e != hipSuccess) return hip_err(e);
@@ -269,7 +394,10 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                      (uint64_t)n, h_out, items_out);
   if ((rc = launch_done())) return rc;
   hipLaunchKernelGGL((k_sort_fixup<uint64_t>), dim3(fgrid), dim3(kSB), 0, st, (const uint64_t*)kout, (uint64_t)n,
-                     h_out, items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count);
+                     h_out, items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, nlong, runs);
+  if ((rc = launch_done())) return rc;
+  hipLaunchKernelGGL((k_sort_long<uint64_t>), dim3(lgrid), dim3(kSB), 0, st, (const uint64_t*)kout, (uint64_t)n,
+                     h_out, items_out, rec, dedup ? 1u : 0u, (unsigned long long*)dup_count, nlong, runs);
   return launch_done();
 }
 

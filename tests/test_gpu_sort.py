@@ -97,6 +97,65 @@ def test_edges(kvh):
     assert np.all(host(oh)[:-1, 0] == 0) and host(oh)[-1, 0] == 12345
 
 
+@pytest.mark.parametrize("sort_bits", [0, 33], ids=["auto_u32", "u64_33"])
+def test_long_runs(kvh, sort_bits):
+    """Runs of equal sort prefix longer than k_sort_fixup's insertion-sort
+    limit (64) go to k_sort_long's bitonic network: one 30000-element run
+    (one h1, random h2 with duplicates), 60 runs of ~500 (60 h1 values), a
+    run already in order (skips the network), mixed with random pairs; items
+    carried, stable among exact duplicates, dedup counted -- against the
+    oracle order."""
+    g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
+    og = orc_geom(ORC, 64 << 20, 64, 1.0, 4, 4)
+    rng = np.random.default_rng(11)
+    one = np.stack([np.full(30000, 0x1234_5678_9abc_def0, dtype=np.uint64),
+                    rng.integers(0, 8000, 30000, dtype=np.uint64)], axis=1)
+    many = np.stack([rng.integers(0, 2 ** 63, 60, dtype=np.uint64)[rng.integers(0, 60, 30000)],
+                     rng.integers(0, 2 ** 20, 30000, dtype=np.uint64)], axis=1)
+    ordered = np.stack([np.full(3000, 0x0fed_cba9_8765_4321, dtype=np.uint64),
+                        np.arange(3000, dtype=np.uint64)], axis=1)
+    rand = rng.integers(0, 2 ** 63, size=(20000, 2), dtype=np.uint64)
+    h = np.concatenate([one, many, ordered, rand])
+    h = h[rng.permutation(len(h))]
+    items = rng.integers(0, 2 ** 63, len(h), dtype=np.uint64)
+    prev = kvh.lib.kvh_set_tuning(17, sort_bits)
+    try:
+        srt = kvh.HtSorter(g, len(h))
+        for dedup in (False, True):
+            oh, oi = srt.sort(dev(h), items=dev(items), dedup=dedup)
+            wh, wi, wd = np_ht_sort(og, h, items=items, dedup=dedup)
+            np.testing.assert_array_equal(host(oh), wh)
+            np.testing.assert_array_equal(host(oi), wi)
+            if dedup:
+                assert int(srt.dups.item()) == wd > 20000
+        oh, oi = srt.sort(dev(h), dedup=True)  # items = input index
+        wh, wi, wd = np_ht_sort(og, h, dedup=True)
+        np.testing.assert_array_equal(host(oh), wh)
+        np.testing.assert_array_equal(host(oi), wi)
+    finally:
+        kvh.lib.kvh_set_tuning(17, prev)
+
+
+def test_long_run_bound(kvh):
+    """A 2M-element batch with one h1 (a single run of distinct h2 in
+    reverse order): O(R log^2 R) on one workgroup, well under the test
+    timeout, where the insertion sort it replaces is O(R^2)."""
+    import time
+    n = 2_000_000
+    h = np.stack([np.full(n, 77, dtype=np.uint64), np.arange(n, 0, -1, dtype=np.uint64)], axis=1)
+    g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
+    srt = kvh.HtSorter(g, n)
+    d = dev(h)
+    t0 = time.time()
+    oh, oi = srt.sort(d, dedup=True)
+    out = host(oh)
+    dt = time.time() - t0
+    assert np.array_equal(out[:, 1], np.arange(1, n + 1, dtype=np.uint64))
+    assert np.array_equal(host(oi), np.arange(n - 1, -1, -1, dtype=np.uint64))
+    assert int(srt.dups.item()) == 0
+    assert dt < 30, dt
+
+
 def test_full_size_properties(kvh):
     """100M fixed-up hashes of C1 keys with 1% duplicates into a 64 GiB
     table: output slots non-decreasing, items a permutation, rows equal the
