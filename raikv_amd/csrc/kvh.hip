@@ -1099,6 +1099,345 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 
 #ifdef KVH_EXPERIMENTS
 // ---------------------------------------------------------------------
+// k_var8: k_var6's length-sorted per-wave windows, hashed as balanced
+// per-state CHAINS.  Until Compress, Meow's four states never meet: state s
+// absorbs its own 16-byte column of every 64-byte block, its own trail chunk
+// and its own Mix round (key_hash.c:1155-1160, 1200-1226).  Per (key, state)
+// that is a chain of nch = nb + (trail chunk of s ? 1 : 0) units over the
+// chain's chunks c_0..c_{nch-1}:
+//   X = F_s ^ c_0 (the folded first absorb), then for u < nch
+//   X = AESDEC(AESDEC(X, c_u), u + 1 < nch ? c_{u+1} : M)
+// (the round-key sequence c_0 | c_1 c_1 | ... | c_last c_last | M paired up).
+// A lane runs four chains back to back -- state 0 of key l, 1 of key 63-l,
+// 2 of key l^32, 3 of key (63-l)^32 in the chunk's length order -- so its
+// work is a sum over a short and a long key, not one key's trip count and
+// trail branches: a chunk of 64 sorted zipf 8-256 B keys costs 1.23x the
+// ideal lane-rounds (simulated), k_var6's one key per lane 1.68x.  The four
+// states of key l then return to lane l by lane shuffles for Compress and
+// the final round (per key, in-lane).
+// MEASURED AND REJECTED (experiments build, knob 7 = 18/19; C2 on one
+// MI355X, outputs equal to k_var6): 4.92 ms (one unit per step, loads at
+// use), 4.88 ms (loads one unit ahead, conditional), 9.85 ms (this version:
+// unconditional buffer loads, double-buffered) against k_var6's 3.02 ms.
+// LDS instructions fell only 10 % (F folds at every chain start, the state
+// exchange and the tail add back most of the saved lookups), VALU rose
+// 44-80 % (slot bookkeeping, chunk extraction) and the per-unit gathers
+// doubled the wait time.
+__device__ __forceinline__ uint32_t chain_deal(uint32_t l, int s) {
+  return s == 0 ? l : s == 1 ? 63u - l : s == 2 ? l ^ 32u : (63u - l) ^ 32u;
+}
+// units of state s's chain for a key of L bytes: one per full block, plus
+// its trail chunk (s < 3: the full chunk at 16 s when L & 48 > 16 s; s = 3:
+// the partial tail)
+__device__ __forceinline__ uint32_t chain_units(uint32_t L, int s) {
+  const uint32_t C = L & 48u, t = L & 15u;
+  return (L >> 6) + (s < 3 ? (C > 16u * (uint32_t)s ? 1u : 0u) : (t ? 1u : 0u));
+}
+// A chain chunk as loaded: the 5 dwords from the dword-aligned address at or
+// below it (a buffer load off the window's base), with its byte shift and
+// valid byte count; extracted only where it is used, so the load stays in
+// flight until then.  Chunk u of state s's chain: the state's column of block
+// u, or its trail chunk (s = 3: the t-byte tail at 64 nb + C, zero padded).
+struct RawChunk {
+  uint32_t d[5], sn;  // sn = byte shift | valid bytes << 8
+};
+__device__ __forceinline__ RawChunk chain_ld(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t L, uint32_t s,
+                                             uint32_t u) {
+  const bool tail3 = s == 3 && u == (L >> 6);
+  const uint32_t a = off + 64u * u + (tail3 ? (L & 48u) : 16u * s);
+  const uint32_t q = a & ~3u;
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, q, 0, 0);
+  RawChunk c;
+  c.d[0] = v[0]; c.d[1] = v[1]; c.d[2] = v[2]; c.d[3] = v[3];
+  c.d[4] = __builtin_amdgcn_raw_buffer_load_b32(r, q + 16, 0, 0);
+  c.sn = (a & 3u) | ((tail3 ? (L & 15u) : 16u) << 8);
+  return c;
+}
+__device__ __forceinline__ Blk chain_fix(const RawChunk& c) {
+  const uint32_t sh = c.sn & 3u, nbytes = c.sn >> 8;
+  // bytes [nbytes, 16) are zero: 64-bit masks of the low and high halves
+  const uint64_t mlo = nbytes >= 8 ? ~0ull : (1ull << (8 * nbytes)) - 1;
+  const uint64_t mhi = nbytes >= 16 ? ~0ull : nbytes <= 8 ? 0ull : (1ull << (8 * (nbytes - 8))) - 1;
+  Blk x;
+  x.w[0] = __builtin_amdgcn_alignbyte(c.d[1], c.d[0], sh) & (uint32_t)mlo;
+  x.w[1] = __builtin_amdgcn_alignbyte(c.d[2], c.d[1], sh) & (uint32_t)(mlo >> 32);
+  x.w[2] = __builtin_amdgcn_alignbyte(c.d[3], c.d[2], sh) & (uint32_t)mhi;
+  x.w[3] = __builtin_amdgcn_alignbyte(c.d[4], c.d[3], sh) & (uint32_t)(mhi >> 32);
+  return x;
+}
+
+// A lane's chains, compacted: slot 0 is the running chain, slot 1 the next.
+struct ChainSlot {
+  uint32_t off, len, st, nu;  // key offset in the window, key length, state, units
+};
+__device__ __forceinline__ void slot_shift(ChainSlot (&q)[4], bool go) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    q[i].off = go ? q[i + 1].off : q[i].off;
+    q[i].len = go ? q[i + 1].len : q[i].len;
+    q[i].st = go ? q[i + 1].st : q[i].st;
+    q[i].nu = go ? q[i + 1].nu : q[i].nu;
+  }
+  q[3].nu = go ? 0u : q[3].nu;
+}
+
+// The chunks of the lane's next unit, requested one unit ahead: chunk 0 of
+// the next chain (used when the running chain ends with this unit) and the
+// next unit's second-round chunk.  Unconditional loads (addresses clamped to
+// the chain's own chunks): no branch splits the wait counters.
+struct UnitLoads {
+  RawChunk c0, c1;
+};
+__device__ __forceinline__ UnitLoads chain_prefetch(__amdgpu_buffer_rsrc_t r, const ChainSlot (&q)[4], uint32_t u,
+                                                    bool last) {
+  const uint32_t o2 = last ? q[1].off : q[0].off, L2 = last ? q[1].len : q[0].len,
+                 s2 = last ? q[1].st : q[0].st, n2 = last ? q[1].nu : q[0].nu, u2 = last ? 0u : u + 1;
+  UnitLoads n;  // chunk 0 of the chain after the one the next unit runs
+  n.c0 = chain_ld(r, last ? q[2].off : q[1].off, last ? q[2].len : q[1].len, last ? q[2].st : q[1].st, 0);
+  n.c1 = chain_ld(r, o2, L2, s2, u2 + 1 < n2 ? u2 + 1 : 0u);
+  return n;
+}
+
+// One unit of the lane's running chain (slot 0, unit u): two rounds, with
+// the chunks loaded one unit earlier (cur); then the lane advances.
+template <int NT>
+__device__ __forceinline__ void chain_unit(ChainSlot (&q)[4], uint32_t& u, bool act, Blk& X, Blk& K1,
+                                           const UnitLoads& cur, Blk (&Q)[4], uint64_t s1, uint64_t s2,
+                                           const LdsTab<NT>& T, const VConst* kfull, const Blk* ftab) {
+  const uint32_t L = q[0].len, st = q[0].st;
+  const bool last = u + 1 >= q[0].nu;
+  const Blk Mx = mixer(s1, s2, L);
+  if (u == 0) {  // chain start: the folded first absorb
+    Blk F;
+    if (L < (uint32_t)kLT) F = kfull[L].F[st];
+    else if (ftab && L < (uint32_t)(kLT + kNF)) F = ftab[(L - kLT) * 4 + st];
+    else F = aesT(bxor(ramp((int)st), Mx), T);
+    X = bxor(F, K1);
+  }
+  const Blk D = last ? Mx : chain_fix(cur.c1);
+  X = aesdec(aesdec(X, K1, T), D, T);
+  if (act && last) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (st == (uint32_t)i) Q[i] = X;
+  }
+  K1 = last ? chain_fix(cur.c0) : D;
+  slot_shift(q, act && last);
+  u = last ? 0u : u + 1;
+}
+
+// One chunk of 64 length-sorted keys (records [c0, c0 + 64) of the wave's
+// window, k valid): returns the hash of key c0 + lane (garbage past k).
+template <int NT>
+__device__ __forceinline__ Blk chain_hash_chunk(__amdgpu_buffer_rsrc_t rs, const uint32_t* r_off,
+                                                const uint32_t* r_len, uint32_t c0, uint32_t k, uint64_t s1,
+                                                uint64_t s2, const LdsTab<NT>& T, const VConst* kfull,
+                                                const Blk* ftab) {
+  const uint32_t lane = threadIdx.x & 63;
+  ChainSlot q[4];
+  uint32_t total = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = ChainSlot{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int s = 3; s >= 0; s--) {  // push the non-empty chains to the front, state order
+    const uint32_t pos = c0 + chain_deal(lane, s);
+    const bool v = pos < k;
+    const uint32_t L = v ? r_len[pos] : 0u, o = v ? r_off[pos] : 0u;
+    const uint32_t nu = v ? chain_units(L, s) : 0u;
+    total += nu;
+    const bool push = nu != 0;
+#pragma unroll
+    for (int i = 3; i > 0; i--) {
+      q[i].off = push ? q[i - 1].off : q[i].off;
+      q[i].len = push ? q[i - 1].len : q[i].len;
+      q[i].st = push ? q[i - 1].st : q[i].st;
+      q[i].nu = push ? q[i - 1].nu : q[i].nu;
+    }
+    q[0].off = push ? o : q[0].off;
+    q[0].len = push ? L : q[0].len;
+    q[0].st = push ? (uint32_t)s : q[0].st;
+    q[0].nu = push ? nu : q[0].nu;
+  }
+  uint32_t umax = total;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) umax = max(umax, (uint32_t)__shfl_xor((int)umax, o, 64));
+  Blk Q[4], X = bzero();
+#pragma unroll
+  for (int i = 0; i < 4; i++) Q[i] = bzero();
+  // the first unit's chunks: chunk 0 (K1) and chunk 1 of the first chain
+  Blk K1 = chain_fix(chain_ld(rs, q[0].off, q[0].len, q[0].st, 0));
+  UnitLoads A, B;
+  A.c0 = chain_ld(rs, q[1].off, q[1].len, q[1].st, 0);
+  A.c1 = chain_ld(rs, q[0].off, q[0].len, q[0].st, q[0].nu > 1 ? 1u : 0u);
+  uint32_t u = 0;
+  // two units per trip with alternating load sets: the loads for unit i + 1
+  // are issued before unit i's rounds and consumed after them
+  for (uint32_t step = 0; step < umax; step += 2) {
+    B = chain_prefetch(rs, q, u, u + 1 >= q[0].nu);
+    chain_unit<NT>(q, u, step < total, X, K1, A, Q, s1, s2, T, kfull, ftab);
+    if (step + 1 < umax) {
+      A = chain_prefetch(rs, q, u, u + 1 >= q[0].nu);
+      chain_unit<NT>(q, u, step + 1 < total, X, K1, B, Q, s1, s2, T, kfull, ftab);
+    }
+  }
+  // key c0 + lane: its states from the lanes that ran them
+  Blk S[4];
+  S[0] = Q[0];
+#pragma unroll
+  for (int s = 1; s < 4; s++) {
+    const int src = (int)chain_deal(lane, s);
+#pragma unroll
+    for (int w = 0; w < 4; w++) S[s].w[w] = (uint32_t)__shfl((int)Q[s].w[w], src, 64);
+  }
+  const uint32_t pos = c0 + lane;
+  const uint32_t L = pos < k ? r_len[pos] : 0u;
+  const Blk M = mixer(s1, s2, L);
+  const VConst& kc = kfull[L < (uint32_t)kLT ? L : (uint32_t)kLT - 1];
+  const bool T0 = chain_units(L, 0) != 0, T1 = chain_units(L, 1) != 0, T2 = chain_units(L, 2) != 0,
+             T3 = chain_units(L, 3) != 0;
+  const Blk S0 = T0 ? S[0] : kc.G[0], S1 = T1 ? S[1] : kc.G[1], S2 = T2 ? S[2] : kc.G[2],
+            S3 = T3 ? S[3] : kc.G[3];
+  Blk S2b;
+  if (T2) S2b = aesdec(aesdec(S2, S3, T), M, T);
+  else if (T3) S2b = aesdec(bxor(kc.TG2, S3), M, T);
+  else S2b = kc.CS2b;
+  Blk S0b;
+  if (T0) S0b = aesdec(aesdec(S0, S1, T), S2b, T);
+  else S0b = bxor(kc.TCS0a, S2b);
+  return aesdec(S0b, M, T);
+}
+
+template <int NT, int WIN, int SH = 4>
+__global__ void __launch_bounds__(kBlock)
+k_var8(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+       uint64_t* __restrict__ out, uint32_t flags) {
+  using C = Var6Cfg<WIN>;
+  constexpr int M = WIN / 64;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ VConst kfull[kLT];
+  __shared__ Blk kf[C::kWaves * C::kPerWave + LdsTab<NT>::kWords * 4 + kLT * sizeof(VConst) + kNF * 64 <= 163840
+                    ? kNF * 4 : 1];
+  constexpr bool kHaveF = sizeof(kf) == kNF * 4 * sizeof(Blk);
+  __shared__ __attribute__((aligned(16))) uint8_t wavemem[C::kWaves * C::kPerWave];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + (kHaveF ? kNF : 0)); l += blockDim.x) {
+    if (l >= (uint32_t)kLT) {
+      const Blk Mx = mixer(s1, s2, l);
+#pragma unroll
+      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), Mx), T);
+      continue;
+    }
+    const MeowConst kc = make_const(s1, s2, l, T);
+    VConst v;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { v.F[q] = kc.F[q]; v.G[q] = kc.G[q]; }
+    v.TG2 = kc.TG2; v.CS2b = kc.CS2b; v.TCS0a = kc.TCS0a;
+    kfull[l] = v;
+  }
+  const Blk* ftab = kHaveF ? kf : nullptr;
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* hist = (uint32_t*)(wavemem + wv * C::kPerWave);
+  uint32_t* r_off = hist + 256;
+  uint32_t* r_len = r_off + WIN;
+  uint32_t* r_idx = r_len + WIN;
+  const uint64_t kend_off = offs[n];
+  const uint64_t nwin = (n + WIN - 1) / WIN;
+  const uint64_t gw = (uint64_t)blockIdx.x * C::kWaves + wv, tw = (uint64_t)gridDim.x * C::kWaves;
+  for (uint64_t w = gw; w < nwin; w += tw) {
+    const uint64_t i0 = w * WIN;
+    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    const uint64_t ws = offs[i0];
+    uint64_t o[M];
+    uint32_t L[M], b[M], r[M];
+    bool wide = false;
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
+      o[m] = a - ws;
+      L[m] = (uint32_t)(e - a);
+      wide |= e - ws >= (1ull << 32);
+    }
+    // a window of >= 4 GiB (u32 records), or one within 64 bytes of the
+    // batch's last key byte (the chunk loads read whole dwords past a key's
+    // end): u64 offsets, input order, byte-exact loads (see k_var6)
+    const uint64_t we = offs[i0 + k];
+    if (__ballot(wide) != 0 || we + 64 > kend_off) {
+      wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds);
+      continue;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      b[m] = (L[m] >> SH) < 255u ? (L[m] >> SH) : 255u;
+      r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
+    }
+    wave_sync();
+    {
+      uint32_t v[4], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
+      uint32_t inc = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+      uint32_t run = inc - sum;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
+    }
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      if (j < k) {
+        const uint32_t pos = hist[b[m]] + r[m];
+        r_off[pos] = (uint32_t)o[m];
+        r_len[pos] = L[m];
+        r_idx[pos] = j;
+      }
+    }
+    wave_sync();
+    // the window's bytes as a buffer: 32-bit offsets, no 64-bit address math
+    const uint64_t span = kend_off - ws;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(keys + ws), (short)0, (int)(span < 0xffffffffull ? span : 0xffffffffull), 0x00020000);
+    Blk hs[M];
+    uint32_t ix[M];
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t pos = 64 * c + lane;
+      hs[c] = chain_hash_chunk<NT>(rs, r_off, r_len, 64 * c, k, s1, s2, T, kfull, ftab);
+      if (fix) hs[c] = fixup(hs[c]);
+      ix[c] = pos < k ? r_idx[pos] : (uint32_t)WIN;
+    }
+    wave_sync();
+    Blk* stage = (Blk*)hist;
+#pragma unroll
+    for (int c = 0; c < M; c++)
+      if (ix[c] < (uint32_t)WIN) stage[ix[c]] = hs[c];
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t j = 64 * c + lane;
+      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
+    }
+    wave_sync();
+  }
+}
+
+#endif  // KVH_EXPERIMENTS
+
+#ifdef KVH_EXPERIMENTS
+// ---------------------------------------------------------------------
 // k_var7: k_var6's per-wave length-class windows with the LDS traffic that
 // the round-1 counters charged to it removed:
 //  * ranking without LDS atomics on shared addresses: a key's class c =
@@ -2011,11 +2350,20 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
       hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
       return launch_done();
+
     default:
       break;
   }
 #ifdef KVH_EXPERIMENTS
   switch (var) {
+    case 18:
+      hipLaunchKernelGGL((k_var8<2, 256, 4>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1,
+                         seed2, out, flags);
+      return launch_done();
+    case 19:
+      hipLaunchKernelGGL((k_var8<2, 256, 0>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1,
+                         seed2, out, flags);
+      return launch_done();
     case 14:
       hipLaunchKernelGGL((k_var7<2>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out,
                          flags);
@@ -2420,7 +2768,7 @@ int kvh_set_tuning(int k, int value) {
             return set(g_tune_kpl, value);
     case 7: if (value != 0 && value != 7 && value != 13) {
 #ifdef KVH_EXPERIMENTS
-              if (value < 2 || value > 17) return KVH_EINVAL;
+              if (value < 2 || value > 19) return KVH_EINVAL;
 #else
               return KVH_EINVAL;
 #endif
