@@ -355,9 +355,10 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   const uint32_t lo = 64u - nb;
   int cus = 0;
   if ((rc = device_cus(&cus))) return rc;
-  // one element per lane: the run-start test is three coalesced key reads, and a
-  // capped grid-stride grid made it latency-bound (0.8 ms at 100M keys)
-  const uint32_t fgrid = grid;
+  // grid-stride, one duplicate-count atomic per workgroup (one element per
+  // lane made 390K same-address atomics at 100M keys: 11.5 ms for the whole
+  // sort against 7.9; 8 or 32 workgroups per CU measure the same)
+  const uint32_t fgrid = (uint32_t)std::min<uint64_t>(grid, (uint64_t)cus * 8);
   const uint32_t lgrid = (uint32_t)cus * 2;  // long runs: one workgroup each, grid-stride
   size_t tb = L.tmp_bytes;
   hipError_t e;
