@@ -12,11 +12,13 @@ HOT = ("k_fixed", "k_var", "k_generic", "k_fixed_ms")
 HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",), "f4": ("k_crc_fixed",), "f4v": ("k_crc_var",),
               "c2": ("k_var6",), "c3": ("k_fixed_lanes",)}
 # configs whose unit of work is one call of several kernels: (kernel name parts,
-# calls in the PMC run (run_kernel.py --reps), calls in the traced bench run (W + K))
-MULTI = {"f2": (("k_sort", "onesweep", "radix", "rocprim"), 5, 200),
-         "f3": (("k_tok", "k_spans"), 5, 200)}
+# a kernel that runs once per call: its dispatch counts give the calls in the
+# PMC run and in the traced bench run).  f2's rocPRIM kernels are the
+# library's trampoline kernels (torch's own rocPRIM sorts use other names).
+MULTI = {"f2": (("k_sort", "trampoline_kernel"), "k_sort_keys"),
+         "f3": (("k_tok", "k_spans"), "k_spans")}
 # configs whose hot kernel gathers 16-byte key pieces in length-sorted windows: keys per launch
-GATHER = {"c2": 100_000_000}
+GATHER = {"c2": 100_000_000, "f4v": 100_000_000}
 calib = os.path.join(src, "calib", "fetch_calib.json")
 GATHER_FACTOR = 1.0
 if os.path.exists(calib):
@@ -24,6 +26,10 @@ if os.path.exists(calib):
         if "k_gather<16>" in k:
             GATHER_FACTOR = (4 << 30) / (v["FETCH_SIZE"] * 1024)
     shutil.copy(calib, os.path.join(dst, "fetch_calib.json"))
+elif os.path.exists(os.path.join(dst, "fetch_calib.json")):  # the round's calibration, collected earlier
+    for k, v in json.load(open(os.path.join(dst, "fetch_calib.json"))).items():
+        if "k_gather<16>" in k:
+            GATHER_FACTOR = (4 << 30) / (v["FETCH_SIZE"] * 1024)
 tpath = os.path.join(root, "profiles", "pmc_traffic.json")
 spath = os.path.join(dst, "summary.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
@@ -39,8 +45,10 @@ for c in sorted(os.listdir(src)):
         shutil.copy(os.path.join(d, "bench.json"), os.path.join(dst, f"{c}_bench_under_rocprof.json"))
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
     if c in MULTI:  # one call = several kernels: per-call sums over the call's kernels
-        names, reps, calls = MULTI[c]
+        names, marker = MULTI[c]
         pmc = json.load(open(os.path.join(d, "pmc_summary.json")))
+        reps = max(v["_dispatches"] for k, v in pmc.items() if marker in k)
+        calls = max(int(r["Calls"]) for r in stats if marker in r["Name"])
         hbm = sum((v["FETCH_SIZE"] * 2 + v["WRITE_SIZE"]) * 1024 * v["_dispatches"] / reps
                   for k, v in pmc.items() if any(h in k for h in names) and "FETCH_SIZE" in v)
         traffic[c] = {"hbm_bytes_per_launch": hbm, "kernel": "+".join(names),
