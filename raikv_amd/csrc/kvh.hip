@@ -925,7 +925,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int NT, int WIN, bool PF = false, int NW = kBlock / 64, int SH = 0>
+template <int NT, int WIN, bool PF = false, int NW = kBlock / 64, int SH = 0, bool PFS = false>
 __global__ void __launch_bounds__(NW * 64)
 k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -984,7 +984,7 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     // this window is hashed in input order with u64 offsets and lengths
     // instead (wave-uniform), through the same hash call site.
     const bool wwin = __ballot(wide) != 0;
-    if constexpr (PF) {
+    if constexpr (PF || PFS) {
       if (wwin) { wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds); continue; }
     }
     if (!wwin) {
@@ -1058,10 +1058,34 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       // scattered 16-byte stores in sorted order inflated HBM writes 1.76x
       Blk hs[M];
       uint32_t ix[M];
+      Blk pre[4];
+      if constexpr (PFS) {  // experiments: the first 64 bytes of the next chunk's key one chunk ahead
+        const uint32_t p0 = lane < k ? lane : k - 1;
+        prefetch_first(base + r_off[p0], r_len[p0], pre);
+      }
 #pragma unroll
       for (int c = 0; c < M; c++) {
         const uint32_t pos = 64 * c + lane;
         ix[c] = WIN;
+        if constexpr (PFS) {
+          Blk nxt[4];
+          if (c + 1 < M) {
+            const uint32_t pn = pos + 64 < k ? pos + 64 : k - 1;
+            prefetch_first(base + r_off[pn], r_len[pn], nxt);
+          }
+          if (pos < k) {
+            const uint32_t kl = r_len[pos];
+            ix[c] = r_idx[pos];
+            const LdsKV5<LdsTab<NT>> K(kfull, kl, s1, s2, T, ftab);
+            hs[c] = meow_var_pre(base + r_off[pos], kl, pre, K, T);
+            if (fix) hs[c] = fixup(hs[c]);
+          }
+          if (c + 1 < M) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) pre[q] = nxt[q];
+          }
+          continue;
+        }
         if (pos < k) {
           const uint8_t* p;
           uint64_t kl;
@@ -2384,6 +2408,9 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
     case 12: hipLaunchKernelGGL((k_var6<2, 512, false, 10>), dim3(cus), dim3(640), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     case 8: hipLaunchKernelGGL((k_var6<2, 128>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     case 9: hipLaunchKernelGGL((k_var6<2, 256, true>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 20: hipLaunchKernelGGL((k_var6<2, 256, false, 12, 4, true>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 21: hipLaunchKernelGGL((k_var6<2, 256, false, 12, 4>), dim3(cus), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 22: hipLaunchKernelGGL((k_var6<2, 256, false, kBlock / 64, 4, true>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     case 10: hipLaunchKernelGGL((k_var6<2, 128, true>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     default: break;
   }
@@ -2768,7 +2795,7 @@ int kvh_set_tuning(int k, int value) {
             return set(g_tune_kpl, value);
     case 7: if (value != 0 && value != 7 && value != 13) {
 #ifdef KVH_EXPERIMENTS
-              if (value < 2 || value > 19) return KVH_EINVAL;
+              if (value < 2 || value > 22) return KVH_EINVAL;
 #else
               return KVH_EINVAL;
 #endif

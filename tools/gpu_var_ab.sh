@@ -7,7 +7,7 @@ if [ -n "$K" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$K" > $O/tests.txt 2>&1
   rc=$?; echo "pytest rc=$rc" >> $O/tests.txt; tail -2 $O/tests.txt; [ $rc -ne 0 ] && exit $rc
 fi
-KVH_LIB=$PWD/raikv_amd/libkvh.so timeout -k 10 300 python3 tools/tune_var.py --variants $V --rounds 5 > $O/ab.json 2> $O/ab.log || exit 1
+KVH_LIB=${KVH_LIB:-$PWD/raikv_amd/libkvh.so} timeout -k 10 300 python3 tools/tune_var.py --variants $V --rounds 5 > $O/ab.json 2> $O/ab.log || exit 1
 cat $O/ab.json
 for v in ${V//,/ }; do
   timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t$v -o run -- python3 tools/run_kernel.py --config c2 --reps 3 --var $v > $O/t$v.log 2>&1 || exit 1
