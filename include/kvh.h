@@ -448,10 +448,13 @@ int         kvh_device_synchronize(void);
  *  14 = variable-length CRC32C kernel (3 length-sorted windows, 16 waves on
  *       16-copy tables; 1 the same with 10 waves on 32-copy tables; 2 with 8
  *       waves; 0 input order),
- *  15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort key bits (0 auto),
+ *  15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort radix key bits
+ *       (0 auto; nonzero also selects the radix engine),
  *  18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
  *       long queues, two / one spans per lane per step; 0 lane per span),
- *  19 = tokenizer (1 wave-chunked, 0 workgroup-chunked).
+ *  19 = tokenizer (1 wave-chunked, 0 workgroup-chunked),
+ *  20 = ht_sort engine (0 bucketed when the batch fits it, up to ~147M
+ *       elements, else radix; 1 radix always).
  * Returns the previous value or KVH_EINVAL.  (Research kernels and ablation
  * builds whose outputs are not hashes exist only in the experiments build,
  * tools/libkvh_exp.so, never in libkvh.so.) */

@@ -114,12 +114,13 @@ k_sort_place(const uint64_t* __restrict__ h, const Rec* __restrict__ rec, const 
   if (items_out) items_out[j] = it;
 }
 
+template <int NT = kSB>
 __device__ __forceinline__ uint32_t block_sum(uint32_t d, uint32_t* wsum) {
   for (int o = 32; o >= 1; o >>= 1) d += __shfl_xor(d, o, 64);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = d;
   __syncthreads();
   uint32_t t = 0;
-  for (int w = 0; w < kSB / 64; w++) t += wsum[w];
+  for (int w = 0; w < NT / 64; w++) t += wsum[w];
   __syncthreads();
   return t;
 }
@@ -269,6 +270,329 @@ k_sort_long(const K* __restrict__ key, uint64_t n, uint64_t* __restrict__ h, uin
   }
 }
 
+// ---------------------------------------------------------------------
+// Bucketed path (the default when the batch fits it): slot order without a
+// library sort and without the random gather of k_sort_place.
+//   B0. k_bk_hist     per 64K-element tile, a histogram of the top B bits of
+//                     key64 (B <= 14: ~6K elements per bucket), tile-major
+//   B1. k_bk_colsum / k_bk_colscan / k_bk_scan / k_bk_tileoff
+//                     column scans of the tile x bucket table -> each tile's
+//                     first output position in each bucket
+//   B2. k_bk_scatter  (h1, h2, item, index) records to their bucket, ranked
+//                     by LDS atomics (a tile's elements of one bucket land
+//                     together: ~4 per bucket per tile, 128-byte runs)
+//   B3. k_bk_sort     one workgroup per bucket, in LDS: a counting sort on
+//                     the next 13 bits of key64, runs of equal bits put in
+//                     the full order (key64, h1 << 1, h1, h2, input index) by
+//                     insertion sort, then the records gathered into the
+//                     outputs with the dedup marks -- the order of the radix
+//                     path exactly (the input index is its stable tie-break)
+//   B4. k_bk_long     buckets over the LDS capacity or with a run over 64
+//                     (non-uniform input) sorted by a bitonic network in
+//                     global memory, one workgroup each (as k_sort_long)
+constexpr int kBkMaxB = 14;
+constexpr uint32_t kBkTile = 65536;  // elements per B0/B2 tile
+constexpr uint32_t kBkChunk = 64;    // tiles per column-scan chunk
+constexpr uint32_t kBkCap = 12288;   // B3 bucket capacity (LDS)
+constexpr int kBkD = 13;             // B3 counting-sort bits
+constexpr uint32_t kBkRun = 64;      // B3 longest run of equal bits
+constexpr int kBkT = 1024;           // threads per workgroup
+
+__device__ __forceinline__ uint64_t sort_key64(const HtGeom& g, uint32_t sb, uint64_t h1) {
+  const uint64_t slot = ht_mod(g, h1);
+  return sb >= 64 ? slot : (slot << (64 - sb)) | ((h1 << 1) >> sb);
+}
+__device__ __forceinline__ uint32_t bk_of(uint64_t k64, uint32_t B) { return B ? (uint32_t)(k64 >> (64 - B)) : 0u; }
+
+// the full order: key64, then (h1 << 1, h1, h2), then the input index
+__device__ __forceinline__ bool bk_less(const HtGeom& g, uint32_t sb, const Rec& a, const Rec& b) {
+  const uint64_t ka = sort_key64(g, sb, a.h1), kb = sort_key64(g, sb, b.h1);
+  if (ka != kb) return ka < kb;
+  if (a.h1 != b.h1 || a.h2 != b.h2) return rec_less(a.h1, a.h2, b.h1, b.h2);
+  return a.pad < b.pad;
+}
+
+__global__ void __launch_bounds__(kBkT)
+k_bk_hist(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sb, uint32_t B, uint32_t* __restrict__ H,
+          uint32_t* __restrict__ novf) {
+  __shared__ uint32_t hist[1u << kBkMaxB];
+  const uint32_t nb = 1u << B, tile = blockIdx.x;
+  if (tile == 0 && threadIdx.x == 0) *novf = 0;  // B3's overflow list, empty per call
+  for (uint32_t b = threadIdx.x; b < nb; b += kBkT) hist[b] = 0;
+  __syncthreads();
+  const uint64_t i0 = (uint64_t)tile * kBkTile;
+  for (uint32_t t = threadIdx.x; t < kBkTile; t += kBkT) {
+    const uint64_t i = i0 + t;
+    if (i < n) atomicAdd(&hist[bk_of(sort_key64(g, sb, h[2 * i]), B)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += kBkT) H[(uint64_t)tile * nb + b] = hist[b];
+}
+
+// S[c][b] = sum of H[t][b] over the tiles t of chunk c
+__global__ void __launch_bounds__(256)
+k_bk_colsum(const uint32_t* __restrict__ H, uint32_t ntiles, uint32_t nb, uint32_t* __restrict__ S) {
+  const uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t nch = (ntiles + kBkChunk - 1) / kBkChunk;
+  if (x >= (uint64_t)nch * nb) return;
+  const uint32_t c = (uint32_t)(x / nb), b = (uint32_t)(x % nb);
+  const uint32_t t1 = min(ntiles, (c + 1) * kBkChunk);
+  uint32_t s = 0;
+  for (uint32_t t = c * kBkChunk; t < t1; t++) s += H[(uint64_t)t * nb + b];
+  S[x] = s;
+}
+
+// per bucket: S[c][b] -> exclusive prefix over chunks, cnt[b] = the total
+__global__ void __launch_bounds__(256)
+k_bk_colscan(uint32_t* __restrict__ S, uint32_t nch, uint32_t nb, uint32_t* __restrict__ cnt) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= nb) return;
+  uint32_t run = 0;
+  for (uint32_t c = 0; c < nch; c++) {
+    const uint32_t v = S[(uint64_t)c * nb + b];
+    S[(uint64_t)c * nb + b] = run;
+    run += v;
+  }
+  cnt[b] = run;
+}
+
+// exclusive scan of the bucket sizes (nb <= 16384, one workgroup)
+__global__ void __launch_bounds__(kBkT)
+k_bk_scan(const uint32_t* __restrict__ cnt, uint32_t nb, uint32_t* __restrict__ start) {
+  __shared__ uint32_t wsum[kBkT / 64];
+  constexpr uint32_t per = (1u << kBkMaxB) / kBkT;  // 16 buckets per thread
+  uint32_t v[per], s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < per; j++) {
+    const uint32_t b = threadIdx.x * per + j;
+    v[j] = b < nb ? cnt[b] : 0u;
+    s += v[j];
+  }
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t wo = 0;
+  for (uint32_t q = 0; q < w; q++) wo += wsum[q];
+  uint32_t run = wo + inc - s;
+#pragma unroll
+  for (uint32_t j = 0; j < per; j++) {
+    const uint32_t b = threadIdx.x * per + j;
+    if (b < nb) start[b] = run;
+    run += v[j];
+  }
+}
+
+// H[t][b] -> the absolute output position of tile t's first element of bucket b
+__global__ void __launch_bounds__(256)
+k_bk_tileoff(uint32_t* __restrict__ H, const uint32_t* __restrict__ S, const uint32_t* __restrict__ start,
+             uint32_t ntiles, uint32_t nb) {
+  const uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint32_t nch = (ntiles + kBkChunk - 1) / kBkChunk;
+  if (x >= (uint64_t)nch * nb) return;
+  const uint32_t c = (uint32_t)(x / nb), b = (uint32_t)(x % nb);
+  const uint32_t t1 = min(ntiles, (c + 1) * kBkChunk);
+  uint32_t run = start[b] + S[x];
+  for (uint32_t t = c * kBkChunk; t < t1; t++) {
+    const uint32_t v = H[(uint64_t)t * nb + b];
+    H[(uint64_t)t * nb + b] = run;
+    run += v;
+  }
+}
+
+__global__ void __launch_bounds__(kBkT)
+k_bk_scatter(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, HtGeom g, uint32_t sb,
+             uint32_t B, const uint32_t* __restrict__ H, Rec* __restrict__ recs) {
+  __shared__ uint32_t pos[1u << kBkMaxB];
+  const uint32_t nb = 1u << B, tile = blockIdx.x;
+  for (uint32_t b = threadIdx.x; b < nb; b += kBkT) pos[b] = H[(uint64_t)tile * nb + b];
+  __syncthreads();
+  const uint64_t i0 = (uint64_t)tile * kBkTile;
+  for (uint32_t t = threadIdx.x; t < kBkTile; t += kBkT) {
+    const uint64_t i = i0 + t;
+    if (i >= n) break;
+    Rec r;
+    r.h1 = h[2 * i];
+    r.h2 = h[2 * i + 1];
+    r.item = items ? items[i] : i;
+    r.pad = i;
+    recs[atomicAdd(&pos[bk_of(sort_key64(g, sb, r.h1), B)], 1u)] = r;
+  }
+}
+
+// outputs for sorted position p of a bucket whose record for p is r, next
+// the record at p + 1 (when has_next): dedup marks as ctest.c:96-104
+__device__ __forceinline__ uint32_t bk_emit(uint64_t j, const Rec& r, bool has_next, uint64_t n1, uint64_t n2,
+                                            uint32_t dedup, uint64_t* __restrict__ h_out,
+                                            uint64_t* __restrict__ items_out) {
+  const bool dup = dedup && has_next && r.h1 == n1 && r.h2 == n2;
+  h_out[2 * j] = dup ? 0 : r.h1;
+  h_out[2 * j + 1] = r.h2;
+  if (items_out) items_out[j] = r.item;
+  return dup ? 1u : 0u;
+}
+
+__global__ void __launch_bounds__(kBkT)
+k_bk_sort(const Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
+          uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
+          uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
+          uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
+  __shared__ uint32_t K[kBkCap];         // key64 bits [B, B + 32) of each record
+  __shared__ uint16_t dig[kBkCap];       // its top kBkD bits
+  __shared__ uint16_t ord[kBkCap];       // sorted position -> record
+  __shared__ uint32_t hist[1u << kBkD];  // digit counts -> starts -> ends
+  __shared__ uint32_t wsum[kBkT / 64], wmax[kBkT / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr uint32_t nd = 1u << kBkD, per = nd / kBkT;  // 8 digits per thread
+  uint32_t d_total = 0;
+  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t R = cnt[b], base = start[b];
+    if (R == 0) continue;
+    if (R > kBkCap) {
+      if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+      continue;
+    }
+    const Rec* rb = recs + base;
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
+    __syncthreads();
+    for (uint32_t t = tid; t < R; t += kBkT) {
+      const uint32_t k32 = (uint32_t)((sort_key64(g, sb, rb[t].h1) << B) >> 32);
+      K[t] = k32;
+      dig[t] = (uint16_t)(k32 >> (32 - kBkD));
+      atomicAdd(&hist[k32 >> (32 - kBkD)], 1u);
+    }
+    __syncthreads();
+    {  // exclusive scan of the digit counts, and the longest run
+      uint32_t v[per], s = 0, mx = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { v[j] = hist[tid * per + j]; s += v[j]; mx = max(mx, v[j]); }
+      uint32_t inc = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+      if (lane == 63) wsum[w] = inc;
+      if (lane == 0) wmax[w] = mx;
+      __syncthreads();
+      uint32_t wo = 0, bm = 0;
+      for (uint32_t q = 0; q < kBkT / 64; q++) {
+        if (q < w) wo += wsum[q];
+        bm = max(bm, wmax[q]);
+      }
+      if (bm > kBkRun) {  // a run too long for insertion sort: the bitonic path
+        if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+        __syncthreads();
+        continue;
+      }
+      uint32_t run = wo + inc - s;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < R; t += kBkT) ord[atomicAdd(&hist[dig[t]], 1u)] = (uint16_t)t;
+    __syncthreads();
+    // runs of equal digit (hist[d] is now the end of digit d): full order
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) {
+      const uint32_t d = tid * per + j;
+      const uint32_t e = hist[d], s0 = d ? hist[d - 1] : 0u;
+      for (uint32_t a = s0 + 1; a < e; a++) {
+        const uint16_t x = ord[a];
+        const uint32_t kx = K[x];
+        uint32_t c = a;
+        while (c > s0) {
+          const uint16_t y = ord[c - 1];
+          const uint32_t ky = K[y];
+          const bool lt = kx != ky ? kx < ky : bk_less(g, sb, rb[x], rb[y]);
+          if (!lt) break;
+          ord[c] = y;
+          c--;
+        }
+        ord[c] = x;
+      }
+    }
+    __syncthreads();
+    for (uint32_t p0 = 0; p0 < R; p0 += kBkT) {
+      const uint32_t p = p0 + tid;
+      Rec r;
+      if (p < R) r = rb[ord[p]];
+      // the successor's pair: the next lane's record, or a load at a wave's edge
+      uint64_t n1 = (uint64_t)__shfl_down((unsigned long long)r.h1, 1, 64),
+               n2 = (uint64_t)__shfl_down((unsigned long long)r.h2, 1, 64);
+      const bool has_next = p + 1 < R;
+      if (lane == 63 && has_next) {
+        const Rec& q = rb[ord[p + 1]];
+        n1 = q.h1;
+        n2 = q.h2;
+      }
+      if (p < R) d_total += bk_emit((uint64_t)base + p, r, has_next, n1, n2, dedup, h_out, items_out);
+    }
+    __syncthreads();
+  }
+  if (dedup && dups) {
+    const uint32_t t = block_sum<kBkT>(d_total, wsum);
+    if (tid == 0 && t) atomicAdd(dups, (unsigned long long)t);
+  }
+}
+
+// buckets B3 could not sort in LDS: a bitonic network over their records in
+// place (as k_sort_long), then the outputs.  One workgroup per bucket.
+__global__ void __launch_bounds__(kSB)
+k_bk_long(Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start, HtGeom g,
+          uint32_t sb, uint64_t* __restrict__ h_out, uint64_t* __restrict__ items_out, uint32_t dedup,
+          unsigned long long* __restrict__ dups, const uint32_t* __restrict__ novf, const uint32_t* __restrict__ ovf) {
+  __shared__ uint32_t wsum[kSB / 64];
+  const uint32_t count = *novf, tid = threadIdx.x;
+  uint32_t d = 0;
+  for (uint32_t r = blockIdx.x; r < count; r += gridDim.x) {
+    const uint32_t b = ovf[r];
+    const uint64_t len = cnt[b];
+    Rec* R = recs + start[b];
+    uint64_t P = 1;
+    while (P < len) P <<= 1;
+    for (uint64_t k = 2; k <= P; k <<= 1) {
+      for (uint64_t jj = k >> 1; jj > 0; jj >>= 1) {
+        for (uint64_t t = tid; t < P / 2; t += kSB) {
+          const uint64_t off = t & (jj - 1);
+          uint64_t a, c;
+          if (jj == (k >> 1)) {
+            a = (t / jj) * k + off;
+            c = (t / jj) * k + k - 1 - off;
+          } else {
+            a = (t / jj) * 2 * jj + off;
+            c = a + jj;
+          }
+          if (c >= len) continue;
+          const Rec x = R[a], y = R[c];
+          if (bk_less(g, sb, y, x)) { R[a] = y; R[c] = x; }
+        }
+        __syncthreads();
+      }
+    }
+    for (uint64_t t = tid; t < len; t += kSB) {
+      const Rec v = R[t];
+      const bool has_next = t + 1 < len;
+      uint64_t n1 = 0, n2 = 0;
+      if (has_next) { n1 = R[t + 1].h1; n2 = R[t + 1].h2; }
+      d += bk_emit(start[b] + t, v, has_next, n1, n2, dedup, h_out, items_out);
+    }
+    __syncthreads();
+  }
+  if (dedup && dups) {
+    const uint32_t t = block_sum(d, wsum);
+    if (tid == 0 && t) atomicAdd(dups, (unsigned long long)t);
+  }
+}
+
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct SortLayout {
@@ -341,9 +665,57 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   // k_sort_fixup orders them by the full comparator.  100M keys into a
   // 64 GiB table: 32 bits, 4 radix passes instead of 8.
   const uint32_t sb = slot_bits(geom->ht_size);
+  const int tsb = g_tune_sort_bits.load(std::memory_order_relaxed);
+  int cus = 0;
+  if ((rc = device_cus(&cus))) return rc;
+  if (!tsb && g_tune_sort_engine.load(std::memory_order_relaxed) == 0) {
+    // the bucketed path: ~6K elements per bucket, B <= 14 bucket bits, so up
+    // to ~147M elements per call (a mean bucket of <= 9000 under the 12288
+    // LDS capacity); larger batches take the radix path below
+    uint32_t B = 0;
+    while (B < (uint32_t)kBkMaxB && ((uint64_t)n >> B) > 6144) B++;
+    if (((uint64_t)n >> B) <= 9000) {
+      const uint32_t nb = 1u << B;
+      const uint32_t ntiles = (uint32_t)((n + kBkTile - 1) / kBkTile);
+      const uint32_t nch = (ntiles + kBkChunk - 1) / kBkChunk;
+      // scratch: records in L.rec; the tile x bucket table in the key areas;
+      // chunk sums, bucket sizes, starts and the overflow list in the index areas
+      if ((uint64_t)ntiles * nb * 4 > L.idx_in - L.key_in || (uint64_t)nch * nb * 4 > L.idx_out - L.idx_in ||
+          (uint64_t)(3 * nb + 1) * 4 > L.rec - L.idx_out)
+        return set_err(KVH_EINVAL);  // cannot happen for the B chosen above
+      uint32_t* H = (uint32_t*)(s + L.key_in);
+      uint32_t* S = (uint32_t*)(s + L.idx_in);
+      uint32_t* cnt = (uint32_t*)(s + L.idx_out);
+      uint32_t* start = cnt + nb;
+      uint32_t* ovf = start + nb;
+      uint32_t* novf = ovf + nb;
+      const uint32_t cgrid = (uint32_t)(((uint64_t)nch * nb + 255) / 256);
+      hipLaunchKernelGGL(k_bk_hist, dim3(ntiles), dim3(kBkT), 0, st, hashes, (uint64_t)n, g, sb, B, H, novf);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_colsum, dim3(cgrid), dim3(256), 0, st, (const uint32_t*)H, ntiles, nb, S);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_colscan, dim3((nb + 255) / 256), dim3(256), 0, st, S, nch, nb, cnt);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(kBkT), 0, st, (const uint32_t*)cnt, nb, start);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_tileoff, dim3(cgrid), dim3(256), 0, st, H, (const uint32_t*)S, (const uint32_t*)start,
+                         ntiles, nb);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(kBkT), 0, st, hashes, items, (uint64_t)n, g, sb, B,
+                         (const uint32_t*)H, rec);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_sort, dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st, (const Rec*)rec,
+                         (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out,
+                         dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_long, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st, rec,
+                         (const uint32_t*)cnt, (const uint32_t*)start, g, sb, h_out, items_out, dedup ? 1u : 0u,
+                         (unsigned long long*)dup_count, (const uint32_t*)novf, (const uint32_t*)ovf);
+      return launch_done();
+    }
+  }
   uint32_t lg = 0;
   while (lg < 63 && (1ull << lg) < (uint64_t)n) lg++;
-  const int tsb = g_tune_sort_bits.load(std::memory_order_relaxed);
   uint32_t nb = tsb ? sb + (uint32_t)tsb : std::max(sb + 1, lg + 5);
   if (nb > 64) nb = 64;
   // u32 keys halve the key bytes every radix pass moves (16 instead of 24 per
@@ -353,8 +725,6 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   const bool k32 = !tsb && sb <= 31;
   if (k32) nb = std::min(nb, 31u);
   const uint32_t lo = 64u - nb;
-  int cus = 0;
-  if ((rc = device_cus(&cus))) return rc;
   // grid-stride, one duplicate-count atomic per workgroup (one element per
   // lane made 390K same-address atomics at 100M keys: 11.5 ms for the whole
   // sort against 7.9; 8 or 32 workgroups per CU measure the same)
@@ -406,7 +776,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
 
 }  // namespace
 
-namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; } }
 
 extern "C" {
 

@@ -2814,6 +2814,7 @@ int kvh_set_tuning(int k, int value) {
 #endif
       return set(g_tune_spans, value);
     case 19: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_tok, value);
+    case 20: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_engine, value);
 #ifdef KVH_EXPERIMENTS
     case 5: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_ablate, value);
     case 6: if (value != 0 && value != 2 && value != 3 && value != 4 && value != 6) return KVH_EINVAL;

@@ -34,16 +34,32 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
 
 
-@pytest.mark.parametrize("sort_bits", [0, 33], ids=["auto_u32", "u64_33"])
+ENGINES = [(0, 0), (0, 1), (33, 0)]
+ENGINE_IDS = ["bucketed", "radix_u32", "radix_u64"]
+
+
+class _engine:
+    """knob 20 = 0 bucketed (the default), 1 radix; knob 17 = 33 forces the
+    radix engine on u64 keys over slot + 33 h1 bits (0: u32 keys when the
+    prefix fits 31 bits)."""
+
+    def __init__(self, kvh, sort_bits, engine):
+        self.kvh, self.v = kvh, (sort_bits, engine)
+
+    def __enter__(self):
+        self.prev = (self.kvh.lib.kvh_set_tuning(17, self.v[0]), self.kvh.lib.kvh_set_tuning(20, self.v[1]))
+
+    def __exit__(self, *a):
+        self.kvh.lib.kvh_set_tuning(17, self.prev[0])
+        self.kvh.lib.kvh_set_tuning(20, self.prev[1])
+
+
+@pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
 @pytest.mark.parametrize("f", FIX, ids=[f["name"] for f in FIX])
-def test_sort_golden(kvh, f, sort_bits):
-    """Golden sets, both key widths: knob 17 = 0 sorts u32 keys when the
-    prefix fits 31 bits; 33 forces u64 keys over slot + 33 h1 bits."""
-    prev = kvh.lib.kvh_set_tuning(17, sort_bits)
-    try:
+def test_sort_golden(kvh, f, eng):
+    """Golden sets on each engine: bucketed, radix on u32 keys, radix on u64 keys."""
+    with _engine(kvh, *eng):
         _sort_golden(kvh, f)
-    finally:
-        kvh.lib.kvh_set_tuning(17, prev)
 
 
 def _sort_golden(kvh, f):
@@ -97,8 +113,8 @@ def test_edges(kvh):
     assert np.all(host(oh)[:-1, 0] == 0) and host(oh)[-1, 0] == 12345
 
 
-@pytest.mark.parametrize("sort_bits", [0, 33], ids=["auto_u32", "u64_33"])
-def test_long_runs(kvh, sort_bits):
+@pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
+def test_long_runs(kvh, eng):
     """Runs of equal sort prefix longer than k_sort_fixup's insertion-sort
     limit (64) go to k_sort_long's bitonic network: one 30000-element run
     (one h1, random h2 with duplicates), 60 runs of ~500 (60 h1 values), a
@@ -118,8 +134,7 @@ def test_long_runs(kvh, sort_bits):
     h = np.concatenate([one, many, ordered, rand])
     h = h[rng.permutation(len(h))]
     items = rng.integers(0, 2 ** 63, len(h), dtype=np.uint64)
-    prev = kvh.lib.kvh_set_tuning(17, sort_bits)
-    try:
+    with _engine(kvh, *eng):
         srt = kvh.HtSorter(g, len(h))
         for dedup in (False, True):
             oh, oi = srt.sort(dev(h), items=dev(items), dedup=dedup)
@@ -132,8 +147,34 @@ def test_long_runs(kvh, sort_bits):
         wh, wi, wd = np_ht_sort(og, h, dedup=True)
         np.testing.assert_array_equal(host(oh), wh)
         np.testing.assert_array_equal(host(oi), wi)
-    finally:
-        kvh.lib.kvh_set_tuning(17, prev)
+
+
+@pytest.mark.parametrize("n", [1, 2, 6144, 6145, 65536, 65537, 1_000_003, 20_000_000])
+def test_engines_agree(kvh, n):
+    """The bucketed engine against the radix engine, word for word, across
+    bucket counts (1 .. 4096 buckets, ragged last tiles), with items and
+    dedup; the oracle on the smaller sizes."""
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(n)
+    h = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda", generator=gen)
+    if n > 100:
+        k = n // 100  # 1 % duplicates
+        h[torch.randint(0, n, (k,), device="cuda", generator=gen)] = h[torch.randint(0, n, (k,), device="cuda", generator=gen)]
+    items = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=gen)
+    g = kvh.HtGeom.from_map(1 << 30, 64, 1.0, 4, 4)
+    srt = kvh.HtSorter(g, n)
+    res = {}
+    for e in (0, 1):
+        with _engine(kvh, 0, e):
+            oh, oi = srt.sort(h, items=items, dedup=True)
+            res[e] = (oh.clone(), oi.clone(), int(srt.dups.item()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]
+    if n <= 65537:
+        og = orc_geom(ORC, 1 << 30, 64, 1.0, 4, 4)
+        wh, wi, wd = np_ht_sort(og, host(h), items=host(items), dedup=True)
+        np.testing.assert_array_equal(host(res[0][0]), wh)
+        np.testing.assert_array_equal(host(res[0][1]), wi)
+        assert res[0][2] == wd
 
 
 def test_long_run_bound(kvh):
