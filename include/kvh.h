@@ -297,8 +297,9 @@ int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
  * the duplicate count differ.  The reference's in-place bit-pivot sort
  * (include/raikv/radix_sort.h:31-33) leaves equal slots in an input-dependent
  * order, so ctest's adjacent-pair scan finds only the duplicates that land
- * next to each other; here equal slots are ordered by (h1 << 1, h1, h2), all
- * duplicates are adjacent and the count is the true one (reference fixtures:
+ * next to each other; here equal slots are ordered by (h1 << 1, h1, h2) and
+ * then input order, all duplicates are adjacent and the count is the true
+ * one (reference fixtures:
  * 99 vs 500 on the 600-entry table, 992 vs 1000 on a 64 MiB one; tests/golden/
  * sort_*.npz).  Not a bit-identical drop-in for kv_ht_radix_sort.
  * ------------------------------------------------------------------- */
@@ -314,7 +315,13 @@ typedef struct {
 size_t kvh_ht_sort_scratch_bytes(size_t n);
 /* n < 2^32 device (h1,h2) pairs (+ optional u64 items, NULL = carry the
  * input index) -> hashes_out / items_out in table order; with KVH_DEDUP
- * the duplicate count is written to *dup_count (device u64, optional). */
+ * the duplicate count is written to *dup_count (device u64, optional).
+ * Asynchronous on stream.  Two engines give the same output word for word
+ * (kvh_set_tuning knob 20): a bucketed one (tile histograms, a record
+ * scatter into ~6K-element buckets, an LDS sort per bucket; the default up
+ * to ~147M elements per call) and a radix one (rocPRIM onesweep on a
+ * key prefix + gather; beyond that size).  Non-uniform input (many pairs
+ * sharing a slot and h1) is bounded at O(R log^2 R) per such group. */
 int kvh_ht_sort(const uint64_t *hashes, const uint64_t *items, size_t n,
                 const kvh_ht_geom_t *geom, uint64_t *hashes_out,
                 uint64_t *items_out, uint64_t *dup_count, uint32_t flags,
