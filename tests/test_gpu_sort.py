@@ -149,11 +149,16 @@ def test_long_runs(kvh, eng):
         np.testing.assert_array_equal(host(oi), wi)
 
 
-@pytest.mark.parametrize("n", [1, 2, 6144, 6145, 65536, 65537, 1_000_003, 20_000_000])
-def test_engines_agree(kvh, n):
+@pytest.mark.parametrize("n,map_size", [(1, 1 << 30), (2, 1 << 30), (6144, 1 << 30), (6145, 1 << 30),
+                                        (65536, 1 << 30), (65537, 1 << 30), (1_000_003, 1 << 30),
+                                        (20_000_000, 1 << 30), (65537, (448 << 10) + 64 * 600), (1_000_003, (448 << 10) + 64 * 600),
+                                        (65537, 1 << 40), (1_000_003, 1 << 40)])
+def test_engines_agree(kvh, n, map_size):
     """The bucketed engine against the radix engine, word for word, across
-    bucket counts (1 .. 4096 buckets, ragged last tiles), with items and
-    dedup; the oracle on the smaller sizes."""
+    bucket counts (1 .. 4096 buckets, ragged last tiles) and table sizes (a
+    600-entry table: most elements share a slot; a 1 TiB table: 35 slot
+    bits, past the radix engine's u32 keys), with items and dedup; the
+    oracle on the smaller sizes."""
     gen = torch.Generator(device="cuda")
     gen.manual_seed(n)
     h = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda", generator=gen)
@@ -161,7 +166,7 @@ def test_engines_agree(kvh, n):
         k = n // 100  # 1 % duplicates
         h[torch.randint(0, n, (k,), device="cuda", generator=gen)] = h[torch.randint(0, n, (k,), device="cuda", generator=gen)]
     items = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=gen)
-    g = kvh.HtGeom.from_map(1 << 30, 64, 1.0, 4, 4)
+    g = kvh.HtGeom.from_map(map_size, 64, 1.0, 4, 4)
     srt = kvh.HtSorter(g, n)
     res = {}
     for e in (0, 1):
@@ -170,7 +175,7 @@ def test_engines_agree(kvh, n):
             res[e] = (oh.clone(), oi.clone(), int(srt.dups.item()))
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]
     if n <= 65537:
-        og = orc_geom(ORC, 1 << 30, 64, 1.0, 4, 4)
+        og = orc_geom(ORC, map_size, 64, 1.0, 4, 4)
         wh, wi, wd = np_ht_sort(og, host(h), items=host(items), dedup=True)
         np.testing.assert_array_equal(host(res[0][0]), wh)
         np.testing.assert_array_equal(host(res[0][1]), wi)
