@@ -1860,6 +1860,140 @@ int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t
   return launch_done();
 }
 
+// Fixed-length keys of any length 1-63 (k_fixed<L> covers the multiples of
+// 8 at 8-byte aligned bases): the same wave-chunked streaming and U keys per
+// lane as k_fixed, with the length a kernel argument.  Every lane of the
+// launch has the same length, so every branch of the Meow plan below is
+// wave-uniform (scalar branches, each body U independent rounds: the ILP
+// k_generic's one key per lane lacks, which ran these lengths at half the
+// neighbouring multiples of 8).  NC = ceil(L / 16) 16-byte chunks per key,
+// each read as the dword-aligned 16 bytes at or below it plus one dword,
+// funnelled by the byte offset (v_alignbyte), then masked past the key.  A
+// chunk of keys within 32 bytes of the batch's last byte reads byte-exact
+// (load_bytes) instead: wave-uniform, the last chunk only.
+template <int NC, int U, class Tab>
+__device__ __forceinline__ void meow_small(Blk (&D)[U][NC], uint32_t L, const MeowConst& K, const Tab& T,
+                                           Blk (&h)[U]) {
+  // nb = 0: the trail only (key_hash.c:1200-1210); every state's first
+  // absorb is folded (F_s ^ k, one round)
+  const uint32_t C = L & 48u, t = L & 15u;
+  const bool T0 = C >= 16, T1 = C >= 32, T2 = C >= 48, T3 = t != 0;
+  Blk S0[U], S1[U], S2[U], S3[U];
+  if (T3) {  // the partial chunk is the last one
+#pragma unroll
+    for (int u = 0; u < U; u++) S3[u] = aesdec(aesdec(bxor(K.F[3], D[u][NC - 1]), D[u][NC - 1], T), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S3[u] = K.G[3];
+  }
+  if constexpr (NC >= 3) {
+    if (T2) {
+#pragma unroll
+      for (int u = 0; u < U; u++) S2[u] = aesdec(aesdec(bxor(K.F[2], D[u][2]), D[u][2], T), K.M, T);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) S2[u] = K.G[2];
+    }
+  }
+  if constexpr (NC >= 2) {
+    if (T1) {
+#pragma unroll
+      for (int u = 0; u < U; u++) S1[u] = aesdec(aesdec(bxor(K.F[1], D[u][1]), D[u][1], T), K.M, T);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) S1[u] = K.G[1];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S1[u] = K.G[1];
+  }
+  if (T0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) S0[u] = aesdec(aesdec(bxor(K.F[0], D[u][0]), D[u][0], T), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S0[u] = K.G[0];
+  }
+  // Compress_Meow2 / Compress_Meow and the final round, as meow_ct
+  Blk S2b[U];
+  if (NC >= 3 && T2) {
+    if constexpr (NC >= 3) {
+#pragma unroll
+      for (int u = 0; u < U; u++) S2b[u] = aesdec(aesdec(S2[u], S3[u], T), K.M, T);
+    }
+  } else if (T3) {
+#pragma unroll
+    for (int u = 0; u < U; u++) S2b[u] = aesdec(bxor(K.TG2, S3[u]), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S2b[u] = K.CS2b;
+  }
+  if (T0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = aesdec(aesdec(aesdec(S0[u], S1[u], T), S2b[u], T), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = aesdec(bxor(K.TCS0a, S2b[u]), K.M, T);
+  }
+}
+
+template <int NC, int NT, int U>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_rt(const uint8_t* __restrict__ keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2,
+           uint64_t* __restrict__ out, uint32_t flags) {
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  const uint64_t last = n - 1, total = n * (uint64_t)L;
+  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
+    const bool exact = (b + 64 * U) * (uint64_t)L + 32 > total;  // this chunk reaches the batch's end
+    Blk D[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      const uint8_t* p = keys + (j < last ? j : last) * (uint64_t)L;
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        const int left = (int)L - 16 * c;
+        const uint32_t nv = left >= 16 ? 16u : (uint32_t)left;
+        if (exact) {
+          D[u][c] = load_bytes(p + 16 * c, nv);
+        } else {
+          D[u][c] = load16_full(p + 16 * c);
+          if (c == NC - 1 && nv < 16) {
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+              const int keep = (int)nv - 4 * w;
+              D[u][c].w[w] &= keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+            }
+          }
+        }
+      }
+    }
+    Blk h[U];
+    meow_small<NC, U>(D, L, K, T, h);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      store_h<true>(out, j < last ? j : last, h[u], fix);
+    }
+  }
+}
+
+template <int NC, int NT, int U>
+int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2, uint64_t* out,
+                    uint32_t flags, hipStream_t st, int cus) {
+  const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
+  hipLaunchKernelGGL((k_fixed_rt<NC, NT, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, L, s1, s2, out, flags);
+  return launch_done();
+}
+
 // Default (NT, U) per length from tools/tune.py sweeps; the tuning knobs
 // override them for the benchmark lengths (16, 32) only.
 template <int L>
@@ -2345,6 +2479,20 @@ int kvh_meow128_fixed(const void* keys, uint32_t key_len, size_t n, uint64_t see
       case 56: return launch_fixed_nt<56>(k, n, seed1, seed2, out, flags, st, cus);
       case 64: return launch_fixed_nt<64>(k, n, seed1, seed2, out, flags, st, cus);
       default: break;
+    }
+  }
+  if (!knob(g_tune_generic) && key_len >= 1 && key_len < 64) {  // any other length below one block
+    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
+    const int nc = (int)(key_len + 15) / 16, nt = tnt ? tnt : 4, kpl = tkpl ? tkpl : (nc == 1 ? 4 : 2);
+    switch (nc * 1000 + nt * 10 + kpl) {
+#define KVH_RT(NCv, NTv, Uv) \
+  case NCv * 1000 + NTv * 10 + Uv: return launch_fixed_rt<NCv, NTv, Uv>(k, n, key_len, seed1, seed2, out, flags, st, cus);
+      KVH_RT(1, 4, 4) KVH_RT(1, 4, 2) KVH_RT(1, 4, 8) KVH_RT(1, 2, 4) KVH_RT(1, 2, 8)
+      KVH_RT(2, 4, 2) KVH_RT(2, 4, 4) KVH_RT(2, 2, 2) KVH_RT(2, 2, 4)
+      KVH_RT(3, 4, 2) KVH_RT(3, 4, 4) KVH_RT(3, 2, 2) KVH_RT(3, 2, 4)
+      KVH_RT(4, 4, 2) KVH_RT(4, 4, 4) KVH_RT(4, 2, 2) KVH_RT(4, 2, 4)
+#undef KVH_RT
+      default: break;  // a knob pair without an instance: the generic kernel
     }
   }
   uint64_t s[16] = {seed1, seed2};

@@ -90,6 +90,22 @@ def test_all_lengths_0_300_all_paths(kvh):
         np.testing.assert_array_equal(got1[0], out[L, 3], err_msg=f"fixed L={L}")
 
 
+def test_fixed_every_length_batched(kvh):
+    """Every length 1..70 as a batch of a few thousand keys (the runtime-length
+    kernel for 1..63 outside the multiples of 8, its byte-exact last chunk, the
+    specialised kernels, k_generic past 63), at an aligned and an odd base,
+    against the oracle."""
+    rng = np.random.default_rng(70)
+    for L in range(1, 71):
+        n = 2000 + 37 * L
+        for shift in (0, 3):
+            raw = rng.integers(0, 256, n * L + shift, dtype=np.uint8)
+            t = dev(raw)
+            got = u64(kvh.meow128_fixed(t[shift:], L, STATIC, n=n))
+            np.testing.assert_array_equal(got, orc_fixed(ORC, raw[shift:].copy(), L, STATIC),
+                                          err_msg=f"L={L} shift={shift}")
+
+
 def test_var_zipf_golden(kvh):
     g = golden("var_zipf.npz")
     out = kvh.meow128_var(dev(g["keys"]), dev_u64(g["offsets"]), STATIC)
