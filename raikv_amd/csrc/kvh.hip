@@ -1121,6 +1121,185 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
   }
 }
 
+// ---------------------------------------------------------------------
+// k_var9: k_var6's per-wave windows, sorted by 16-byte length class, with
+// the two costs its counters name removed:
+//  * L2 requests.  The L1 does not merge misses of different load
+//    instructions, so k_var6's byte-aligned pieces (dwordx4 + dword each)
+//    and dword-by-dword tails cost ~7 L2 requests per key, and the L1->L2
+//    queue (46 requests in flight per CU at ~430 cycles) sets its time.
+//    meow_a reads 16-byte aligned chunks: one request per 16 bytes;
+//  * serial latency.  meow_rt's per-lane branches run one after the other
+//    in a wave (each trail chunk's load, each Mix state, each Compress half);
+//    meow_a runs, per chunk of 64 sorted keys, one straight-line variant
+//    chosen by two wave-uniform facts (some key has a full block; the
+//    largest trail), so the state chains interleave and every short key's
+//    loads are issued before its first round.
+// The variants need ~165 VGPRs, so 12 waves per CU; hashes go straight to
+// the wave's LDS stage at their input slot, records are 8 bytes
+// (window offset, length << 8 | slot), and no per-window value lives in a
+// register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
+// more take wide_window (input order, u64 offsets and lengths).
+struct VConst9 {  // VConst minus CS2b (meow_a never needs it)
+  Blk F[4], G[4], TG2, TCS0a;
+};
+template <class Tab, int NF>
+struct LdsKV9 {
+  const VConst9* full;
+  const Blk* ftab;  // first-absorb folds F[0..3] for kLT <= L < kLT + NF
+  uint32_t L;
+  Blk m;
+  const Tab& T;
+  __device__ __forceinline__ LdsKV9(const VConst9* f, const Blk* ft, uint32_t len, uint64_t s1, uint64_t s2,
+                                    const Tab& t)
+      : full(f), ftab(ft), L(len), m(mixer(s1, s2, len)), T(t) {}
+  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ Blk M() const { return m; }
+  __device__ __forceinline__ Blk F(int i) const {
+    if (L < (uint32_t)kLT) return full[L].F[i];
+    if (L < (uint32_t)(kLT + NF)) return ftab[(L - kLT) * 4 + i];
+    return aesT(bxor(ramp(i), m), T);
+  }
+  // F of a key shorter than kLT, read branch-free (unused lanes read any record)
+  __device__ __forceinline__ Blk F0(int i) const { return full[L & (kLT - 1)].F[i]; }
+  __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
+  __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
+  __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
+};
+
+template <int NT, int NW, int KF>
+__global__ void __launch_bounds__(NW * 64)
+k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+       uint64_t* __restrict__ out, uint32_t flags) {
+  // per wave: the hash stage (4 KiB); while sorting it holds the bucket counts
+  // (first KiB) and the sorted records (last 2 KiB), which each lane then
+  // takes into registers (its four sorted positions) before hashes land
+  constexpr int WIN = 256, M = WIN / 64, AREA = WIN * 16;
+  // one LDS object, tables first: a lookup address is then the v_perm result
+  // itself (a table at a nonzero base costs one v_add per lookup)
+  constexpr int kTabB = LdsTab<NT>::kWords * 4, kFullB = kLT * (int)sizeof(VConst9), kKfB = KF * 64;
+  constexpr int kBytes = kTabB + kFullB + kKfB + NW * AREA;
+  static_assert(kBytes <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint32_t smem[kBytes / 4];
+  uint32_t* lds = smem;
+  VConst9* kfull = (VConst9*)((uint8_t*)smem + kTabB);
+  Blk* kf = (Blk*)((uint8_t*)smem + kTabB + kFullB);
+  uint8_t* wavemem = (uint8_t*)smem + kTabB + kFullB + kKfB;
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + KF); l += blockDim.x) {
+    if (l >= (uint32_t)kLT) {
+      const Blk Mx = mixer(s1, s2, l);
+#pragma unroll
+      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), Mx), T);
+      continue;
+    }
+    const MeowConst k = make_const(s1, s2, l, T);
+    VConst9 v;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { v.F[q] = k.F[q]; v.G[q] = k.G[q]; }
+    v.TG2 = k.TG2; v.TCS0a = k.TCS0a;
+    kfull[l] = v;
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Blk* stage = (Blk*)(wavemem + wv * AREA);
+  uint32_t* hist = (uint32_t*)stage;
+  uint2* rec = (uint2*)(wavemem + wv * AREA + WIN * 8);
+  const uint64_t nwin = (n + WIN - 1) / WIN;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
+  const uint64_t kend = offs[n];  // the buffer holds every byte up to the last key's end
+  for (uint64_t w = gw; w < nwin; w += tw) {
+    const uint64_t i0 = w * WIN;
+    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    const uint64_t ws = offs[i0];
+    const uint64_t wend = kend - ws;  // window-relative
+    uint32_t o[M], L[M], r[M], b[M];
+    bool wide = false;
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
+      o[m] = (uint32_t)(a - ws);
+      L[m] = (uint32_t)(e - a);
+      wide |= e - ws >= (1ull << 32) || e - a >= (1ull << 24);
+    }
+    if (__ballot(wide) != 0) {  // wave-uniform
+      wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds);
+      continue;
+    }
+    // counting sort of the window by 16-byte length class
+#pragma unroll
+    for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      b[m] = (L[m] >> 4) < 255u ? (L[m] >> 4) : 255u;
+      r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
+    }
+    wave_sync();
+    {
+      uint32_t v[4], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
+      uint32_t inc = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+      uint32_t run = inc - sum;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
+    }
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      if (j < k) rec[hist[b[m]] + r[m]] = make_uint2(o[m], (L[m] << 8) | j);
+    }
+    wave_sync();
+    // this lane's sorted positions lane, 64 + lane, ... (rotated through
+    // scalars below: a register array indexed in a rolled loop is scratch)
+    uint2 rc0 = rec[lane], rc1 = rec[64 + lane], rc2 = rec[128 + lane], rc3 = rec[192 + lane];
+    wave_sync();  // the stage takes hashes from here on
+    const uint8_t* base = keys + ws;
+#pragma unroll 1
+    for (int c = 0; c < M; c++) {
+      const uint32_t pos = 64 * c + lane;
+      const bool valid = pos < k;
+      const uint2 rc = rc0;
+      rc0 = rc1; rc1 = rc2; rc2 = rc3;
+      const uint32_t kl = valid ? rc.y >> 8 : 0u;
+      const bool al = __ballot(kl >= 64u) != 0;
+      const int cm = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
+                   : __ballot((kl & 48u) >= 16u) ? 16 : 0;
+      if (valid) {
+        const uint8_t* p = base + rc.x;
+        const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
+        const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
+        Blk h;
+        if (al) h = meow_a<true, 48>(p, kl, safe, K, T);
+        else if (cm == 48) h = meow_a<false, 48>(p, kl, safe, K, T);
+        else if (cm == 32) h = meow_a<false, 32>(p, kl, safe, K, T);
+        else if (cm == 16) h = meow_a<false, 16>(p, kl, safe, K, T);
+        else h = meow_a<false, 0>(p, kl, safe, K, T);
+        stage[rc.y & 255u] = fix ? fixup(h) : h;
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t j = 64 * c + lane;
+      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
+    }
+    wave_sync();  // stage and records reused by the next window
+  }
+}
+
 #ifdef KVH_EXPERIMENTS
 // ---------------------------------------------------------------------
 // k_var8: k_var6's length-sorted per-wave windows, hashed as balanced
@@ -2522,6 +2701,14 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
       hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
       return launch_done();
+    case 23:
+      hipLaunchKernelGGL((k_var9<2, 16, 192>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
+                         out, flags);
+      return launch_done();
+    case 24:
+      hipLaunchKernelGGL((k_var9<2, 12, 192>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
+                         out, flags);
+      return launch_done();
 
     default:
       break;
@@ -2941,7 +3128,7 @@ int kvh_set_tuning(int k, int value) {
     case 2: return set(g_tune_generic, value ? 1 : 0);
     case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13) {
+    case 7: if (value != 0 && value != 7 && value != 13 && value != 23 && value != 24) {
 #ifdef KVH_EXPERIMENTS
               if (value < 2 || value > 22) return KVH_EINVAL;
 #else

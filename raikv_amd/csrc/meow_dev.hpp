@@ -521,6 +521,248 @@ __device__ __forceinline__ Blk meow_var_pre(const uint8_t* p, uint32_t L, const 
   return aesdec(S0b, M, T);
 }
 
+// Variable-length Meow written for a WAVE of keys whose shapes are bounded by
+// two wave-uniform facts: AL = some lane's key has a full 64-byte block, CM =
+// the largest trail-chunk count (L & 48) of any lane.  meow_rt's per-lane
+// branches (one per trail chunk, one per Mix state, two in Compress) make the
+// wave run every taken branch anyway, one after the other: each branch's
+// load and each of its rounds is a separately exposed latency.  Here every
+// trail load is issued before the first round, and the work any lane of the
+// wave needs is done by all lanes in one basic block, so the (up to) four
+// state chains of the trail and the Mix, and the two halves of Compress,
+// interleave.  The LDS work is the same as the divergent code's (a round
+// runs for the whole wave as soon as one lane needs it); lanes that do not
+// need a state keep it at its init value ramp_i ^ M, for which the unfolded
+// rounds give exactly the folded constants (AESDEC(init_i, M) = G_i,
+// AESDEC(G2, S3) = TG2 ^ S3, T(AESDEC(G0, G1)) = TCS0a), so no lane needs a
+// select after the trail.  Same dataflow as key_hash.c:1155-1226.
+template <bool AL, int CM, class Tab, class KGet, class LenT = uint32_t>
+__device__ __forceinline__ Blk meow_u(const uint8_t* p, LenT L, const KGet& K, const Tab& T) {
+  constexpr bool P0 = AL || CM >= 16, P1 = AL || CM >= 32, P2 = AL || CM >= 48;  // state touched by some lane
+  const LenT nb = L >> 6;
+  const uint32_t C = (uint32_t)L & 48, t = (uint32_t)L & 15;
+  const bool first = nb == 0;
+  const uint8_t* q = p + (LenT)64 * nb;
+  const Blk z = bzero();
+  // short keys: every load before the first round; long keys: the trail's
+  // loads together after the blocks (live across the block loop they spill)
+#define KVH_TRAIL_LOADS                                                      \
+  const Blk r3 = t ? load_bytes(q + C, t) : z;                               \
+  const Blk r2 = (CM >= 48 && C >= 48) ? load16_full(q + 32) : z;            \
+  const Blk r1 = (CM >= 32 && C >= 32) ? load16_full(q + 16) : z;            \
+  const Blk r0 = (CM >= 16 && C >= 16) ? load16_full(q) : z;
+  const Blk M = K.M();
+  Blk S0 = bxor(ramp(0), M), S1 = bxor(ramp(1), M), S2 = bxor(ramp(2), M), S3 = bxor(ramp(3), M);
+  if constexpr (AL) {
+    if (!first) {
+      const Blk k0 = load16_full(p), k1 = load16_full(p + 16), k2 = load16_full(p + 32), k3 = load16_full(p + 48);
+      S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
+      S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
+      for (LenT b = 1; b < nb; b++) {
+        const uint8_t* r = p + (LenT)64 * b;
+        const Blk k0 = load16_full(r), k1 = load16_full(r + 16), k2 = load16_full(r + 32), k3 = load16_full(r + 48);
+        S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+        S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+      }
+    }
+    KVH_TRAIL_LOADS
+    // trail: a block-absorbed state takes two rounds, an init state the folded one
+    {
+      const Blk Y = aesdec(first ? bxor(K.F(3), r3) : aesdec(S3, r3, T), r3, T);
+      if (t) S3 = Y;
+    }
+    if constexpr (CM >= 48) {
+      const Blk Y = aesdec(first ? bxor(K.F(2), r2) : aesdec(S2, r2, T), r2, T);
+      if (C >= 48) S2 = Y;
+    }
+    if constexpr (CM >= 32) {
+      const Blk Y = aesdec(first ? bxor(K.F(1), r1) : aesdec(S1, r1, T), r1, T);
+      if (C >= 32) S1 = Y;
+    }
+    if constexpr (CM >= 16) {
+      const Blk Y = aesdec(first ? bxor(K.F(0), r0) : aesdec(S0, r0, T), r0, T);
+      if (C >= 16) S0 = Y;
+    }
+  } else {
+    KVH_TRAIL_LOADS
+    {
+      const Blk Y = aesdec(bxor(K.F(3), r3), r3, T);
+      if (t) S3 = Y;
+    }
+    if constexpr (CM >= 48) { const Blk Y = aesdec(bxor(K.F(2), r2), r2, T); if (C >= 48) S2 = Y; }
+    if constexpr (CM >= 32) { const Blk Y = aesdec(bxor(K.F(1), r1), r1, T); if (C >= 32) S1 = Y; }
+    if constexpr (CM >= 16) { const Blk Y = aesdec(bxor(K.F(0), r0), r0, T); if (C >= 16) S0 = Y; }
+  }
+#undef KVH_TRAIL_LOADS
+  // Mix_Meow: states no lane touched are the folded constants
+  S3 = aesdec(S3, M, T);
+  if constexpr (P2) S2 = aesdec(S2, M, T); else S2 = K.G(2);
+  if constexpr (P1) S1 = aesdec(S1, M, T); else S1 = K.G(1);
+  if constexpr (P0) S0 = aesdec(S0, M, T); else S0 = K.G(0);
+  // Compress_Meow2 / Compress_Meow: the S2 chain and T(AESDEC(S0, S1)) are independent
+  Blk S2b;
+  if constexpr (P2) S2b = aesdec(aesdec(S2, S3, T), M, T);
+  else S2b = aesdec(bxor(K.TG2(), S3), M, T);
+  Blk S0b;
+  if constexpr (P0) S0b = bxor(aesT(aesdec(S0, S1, T), T), S2b);
+  else S0b = bxor(K.TCS0a(), S2b);
+  return aesdec(S0b, M, T);
+}
+
+// A key's bytes read as dwordx4 GROUPS from the dword-aligned address at or
+// below it: group i = dwords 4i..4i+3.  The L1 does not merge the misses of
+// different load instructions, so every load instruction of a gather is one
+// L2 request per lane (two when it straddles a line): meow_rt's pieces
+// (dwordx4 + one more dword each) and dword-by-dword tails cost ~7 requests
+// per C2 key, and the L1->L2 queue sets k_var6's time.  Here a key costs
+// ceil((s + L) / 16) loads (s = p & 3), and piece k (bytes 16k..16k+15) is
+// group k plus the first dword of group k+1, funnel-shifted by s: four
+// v_alignbyte.  A group may run up to 12 bytes past the key's last dword
+// (into the next key); `safe` says the caller's buffer holds those bytes,
+// otherwise the group is read dword by dword, never past the key.
+struct AChunks {
+  const u32x4_a4* g;  // dword-aligned address at or below the key
+  uint64_t lim;       // s + L: group i holds key bytes iff 16 i < lim
+  uint32_t bs;        // s
+  bool safe;
+  __device__ __forceinline__ AChunks(const uint8_t* p, uint64_t L, bool sf) {
+    const uint32_t s = (uint32_t)((uintptr_t)p & 3);
+    g = (const u32x4_a4*)(p - s);  // pointer arithmetic keeps the global address space
+    lim = s + L;
+    bs = s;
+    safe = sf;
+  }
+  __device__ __forceinline__ Blk chunk(uint64_t i) const {
+    Blk r = bzero();
+    if (16 * i < lim) {
+      if (safe) {
+        const u32x4_a4 v = g[i];
+        r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
+      } else {
+        const uint32_t* d = (const uint32_t*)(g + i);
+#pragma unroll
+        for (int j = 0; j < 4; j++) r.w[j] = 16 * i + 4 * j < lim ? d[j] : 0u;
+      }
+    }
+    return r;
+  }
+  __device__ __forceinline__ Blk piece(const Blk& A, const Blk& B) const {
+    Blk r;
+    r.w[0] = __builtin_amdgcn_alignbyte(A.w[1], A.w[0], bs);
+    r.w[1] = __builtin_amdgcn_alignbyte(A.w[2], A.w[1], bs);
+    r.w[2] = __builtin_amdgcn_alignbyte(A.w[3], A.w[2], bs);
+    r.w[3] = __builtin_amdgcn_alignbyte(B.w[0], A.w[3], bs);
+    return r;
+  }
+};
+// per-word select (a ?: on the struct can become a select of addresses,
+// i.e. a scratch copy)
+__device__ __forceinline__ Blk bsel(bool c, const Blk& a, const Blk& b) {
+  Blk r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.w[i] = c ? a.w[i] : b.w[i];
+  return r;
+}
+// the first n bytes of b (n < 16), zero padded
+__device__ __forceinline__ Blk mask_bytes(Blk b, uint32_t n) {
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int keep = (int)n - 4 * c;
+    b.w[c] &= keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+  }
+  return b;
+}
+
+// meow_u over dwordx4 groups (AChunks): same rounds, fewer load
+// instructions.  All chunks of a short key, and each block's four new chunks
+// of a long key, are requested before the rounds that use them.
+template <bool AL, int CM, class Tab, class KGet, class LenT = uint32_t>
+__device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const KGet& K, const Tab& T) {
+  constexpr bool P0 = AL || CM >= 16, P1 = AL || CM >= 32, P2 = AL || CM >= 48;  // state touched by some lane
+  const LenT nb = L >> 6;
+  const uint32_t C = (uint32_t)L & 48, t = (uint32_t)L & 15;
+  const bool first = nb == 0;
+  const AChunks A(p, L, safe);
+  const Blk M = K.M();
+  Blk S0 = bxor(ramp(0), M), S1 = bxor(ramp(1), M), S2 = bxor(ramp(2), M), S3 = bxor(ramp(3), M);
+  Blk c0 = A.chunk(0);  // chunk 4 nb (the trail's first) once the blocks are absorbed
+  if constexpr (AL) {
+    if (!first) {
+      {
+        const Blk c1 = A.chunk(1), c2 = A.chunk(2), c3 = A.chunk(3), c4 = A.chunk(4);
+        const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
+        c0 = c4;
+        S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
+        S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
+      }
+      for (LenT b = 1; b < nb; b++) {
+        const uint64_t i = 4 * (uint64_t)b;
+        const Blk c1 = A.chunk(i + 1), c2 = A.chunk(i + 2), c3 = A.chunk(i + 3), c4 = A.chunk(i + 4);
+        const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
+        c0 = c4;
+        S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+        S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+      }
+    }
+  }
+  // trail pieces: chunks 4nb .. 4nb + CM/16 + 1; piece j feeds state j, the
+  // partial piece C/16 (t bytes) state 3
+  const uint64_t i0 = 4 * (uint64_t)nb;
+  const Blk c1 = A.chunk(i0 + 1);
+  Blk c2 = bzero(), c3 = bzero(), c4 = bzero();
+  if constexpr (CM >= 16) c2 = A.chunk(i0 + 2);
+  if constexpr (CM >= 32) c3 = A.chunk(i0 + 3);
+  if constexpr (CM >= 48) c4 = A.chunk(i0 + 4);
+  const Blk q0 = A.piece(c0, c1);
+  Blk q1 = bzero(), q2 = bzero(), q3 = bzero();
+  if constexpr (CM >= 16) q1 = A.piece(c1, c2);
+  if constexpr (CM >= 32) q2 = A.piece(c2, c3);
+  if constexpr (CM >= 48) q3 = A.piece(c3, c4);
+  Blk r3 = q0;
+  if constexpr (CM >= 16) r3 = bsel(C >= 16, q1, r3);
+  if constexpr (CM >= 32) r3 = bsel(C >= 32, q2, r3);
+  if constexpr (CM >= 48) r3 = bsel(C >= 48, q3, r3);
+  r3 = mask_bytes(r3, t);
+  if constexpr (AL) {
+    // a block-absorbed state takes two rounds, an init state the folded one
+    {
+      const Blk Y = aesdec(bsel(first, bxor(K.F0(3), r3), aesdec(S3, r3, T)), r3, T);
+      S3 = bsel(t != 0, Y, S3);
+    }
+    if constexpr (CM >= 48) {
+      const Blk Y = aesdec(bsel(first, bxor(K.F0(2), q2), aesdec(S2, q2, T)), q2, T);
+      S2 = bsel(C >= 48, Y, S2);
+    }
+    if constexpr (CM >= 32) {
+      const Blk Y = aesdec(bsel(first, bxor(K.F0(1), q1), aesdec(S1, q1, T)), q1, T);
+      S1 = bsel(C >= 32, Y, S1);
+    }
+    if constexpr (CM >= 16) {
+      const Blk Y = aesdec(bsel(first, bxor(K.F0(0), q0), aesdec(S0, q0, T)), q0, T);
+      S0 = bsel(C >= 16, Y, S0);
+    }
+  } else {
+    {
+      const Blk Y = aesdec(bxor(K.F(3), r3), r3, T);
+      S3 = bsel(t != 0, Y, S3);
+    }
+    if constexpr (CM >= 48) { const Blk Y = aesdec(bxor(K.F(2), q2), q2, T); S2 = bsel(C >= 48, Y, S2); }
+    if constexpr (CM >= 32) { const Blk Y = aesdec(bxor(K.F(1), q1), q1, T); S1 = bsel(C >= 32, Y, S1); }
+    if constexpr (CM >= 16) { const Blk Y = aesdec(bxor(K.F(0), q0), q0, T); S0 = bsel(C >= 16, Y, S0); }
+  }
+  S3 = aesdec(S3, M, T);
+  if constexpr (P2) S2 = aesdec(S2, M, T); else S2 = K.G(2);
+  if constexpr (P1) S1 = aesdec(S1, M, T); else S1 = K.G(1);
+  if constexpr (P0) S0 = aesdec(S0, M, T); else S0 = K.G(0);
+  Blk S2b;
+  if constexpr (P2) S2b = aesdec(aesdec(S2, S3, T), M, T);
+  else S2b = aesdec(bxor(K.TG2(), S3), M, T);
+  Blk S0b;
+  if constexpr (P0) S0b = bxor(aesT(aesdec(S0, S1, T), T), S2b);
+  else S0b = bxor(K.TCS0a(), S2b);
+  return aesdec(S0b, M, T);
+}
+
 // constants held in registers (uniform length)
 struct RegK {
   const MeowConst& k;

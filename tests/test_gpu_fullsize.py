@@ -170,7 +170,7 @@ def test_var_windows_spanning_4gib(kvh):
     doff = dev_u64(offs)
     sd = torch.tensor(np.array(STATIC, dtype=np.uint64).view(np.int64), device="cuda").repeat(n, 1)
     lit = kvh.meow128_var_seeded(keys, doff, sd)
-    for variant in (13, 7, 0):
+    for variant in (13, 7, 0, 23):
         prev = kvh.lib.kvh_set_tuning(7, variant)
         try:
             got = kvh.meow128_var(keys, doff, STATIC)

@@ -315,7 +315,7 @@ def test_cpp_hash_test_program(kvh):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("variant", [0, 7, 13])
+@pytest.mark.parametrize("variant", [0, 7, 13, 23, 24])
 def test_var_kernel_variants_vs_oracle(kvh, variant):
     """The variable-length kernels (kvh_set_tuning(7, v): 0 unsorted, 7
     length-sorted windows, 13 windows sorted by 16-byte length class) against
@@ -356,7 +356,7 @@ def _digest(d: np.ndarray) -> int:
         return int(np.sum(w * (2 * np.arange(w.size, dtype=np.uint64) + np.uint64(1)), dtype=np.uint64))
 
 
-@pytest.mark.parametrize("variant", [13, 7, 0])
+@pytest.mark.parametrize("variant", [13, 7, 0, 23])
 def test_partition_vectors_against_reference(kvh, variant):
     """hash_test.cpp:404-442 on the device, pinned to the REFERENCE's outputs
     (tests/golden/partition2.npz, partition4.npz; make_golden.py): bytes
