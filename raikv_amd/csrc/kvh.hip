@@ -1167,7 +1167,7 @@ struct LdsKV9 {
   __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
 };
 
-template <int NT, int NW, int KF>
+template <int NT, int NW, int KF, bool PF = false>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -1282,11 +1282,11 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
         const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
         const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
         Blk h;
-        if (al) h = meow_a<true, 48>(p, kl, safe, K, T);
-        else if (cm == 48) h = meow_a<false, 48>(p, kl, safe, K, T);
-        else if (cm == 32) h = meow_a<false, 32>(p, kl, safe, K, T);
-        else if (cm == 16) h = meow_a<false, 16>(p, kl, safe, K, T);
-        else h = meow_a<false, 0>(p, kl, safe, K, T);
+        if (al) h = meow_a<true, 48, PF>(p, kl, safe, K, T);
+        else if (cm == 48) h = meow_a<false, 48, PF>(p, kl, safe, K, T);
+        else if (cm == 32) h = meow_a<false, 32, PF>(p, kl, safe, K, T);
+        else if (cm == 16) h = meow_a<false, 16, PF>(p, kl, safe, K, T);
+        else h = meow_a<false, 0, PF>(p, kl, safe, K, T);
         stage[rc.y & 255u] = fix ? fixup(h) : h;
       }
     }
@@ -2709,6 +2709,10 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
       hipLaunchKernelGGL((k_var9<2, 12, 192>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
       return launch_done();
+    case 25:
+      hipLaunchKernelGGL((k_var9<2, 12, 192, true>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1,
+                         seed2, out, flags);
+      return launch_done();
 
     default:
       break;
@@ -3128,7 +3132,7 @@ int kvh_set_tuning(int k, int value) {
     case 2: return set(g_tune_generic, value ? 1 : 0);
     case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13 && value != 23 && value != 24) {
+    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25)) {
 #ifdef KVH_EXPERIMENTS
               if (value < 2 || value > 22) return KVH_EINVAL;
 #else

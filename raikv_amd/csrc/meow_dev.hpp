@@ -676,7 +676,7 @@ __device__ __forceinline__ Blk mask_bytes(Blk b, uint32_t n) {
 // meow_u over dwordx4 groups (AChunks): same rounds, fewer load
 // instructions.  All chunks of a short key, and each block's four new chunks
 // of a long key, are requested before the rounds that use them.
-template <bool AL, int CM, class Tab, class KGet, class LenT = uint32_t>
+template <bool AL, int CM, bool PF, class Tab, class KGet, class LenT = uint32_t>
 __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const KGet& K, const Tab& T) {
   constexpr bool P0 = AL || CM >= 16, P1 = AL || CM >= 32, P2 = AL || CM >= 48;  // state touched by some lane
   const LenT nb = L >> 6;
@@ -685,34 +685,64 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
   const AChunks A(p, L, safe);
   const Blk M = K.M();
   Blk S0 = bxor(ramp(0), M), S1 = bxor(ramp(1), M), S2 = bxor(ramp(2), M), S3 = bxor(ramp(3), M);
-  Blk c0 = A.chunk(0);  // chunk 4 nb (the trail's first) once the blocks are absorbed
-  if constexpr (AL) {
+  // groups 4nb .. 4nb+4 (the trail's) once the blocks are absorbed
+  Blk c0 = A.chunk(0), c1, c2 = bzero(), c3 = bzero(), c4 = bzero();
+  if constexpr (AL && PF) {
+    // one block ahead: block b's rounds run while block b+1's groups (and,
+    // in the last block, the trail's) are in flight
+    c1 = A.chunk(1); c2 = A.chunk(2); c3 = A.chunk(3); c4 = A.chunk(4);
     if (!first) {
+#define KVH_BLOCK(FIRST)                                                                                   \
+  {                                                                                                        \
+    const Blk n1 = A.chunk(i + 5), n2 = A.chunk(i + 6), n3 = A.chunk(i + 7), n4 = A.chunk(i + 8);         \
+    const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);     \
+    if (FIRST) {                                                                                           \
+      S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);                           \
+      S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);                           \
+    } else {                                                                                               \
+      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);                         \
+      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);                         \
+    }                                                                                                      \
+    c0 = c4; c1 = n1; c2 = n2; c3 = n3; c4 = n4;                                                           \
+  }
       {
-        const Blk c1 = A.chunk(1), c2 = A.chunk(2), c3 = A.chunk(3), c4 = A.chunk(4);
-        const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
-        c0 = c4;
-        S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
-        S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
+        const uint64_t i = 0;
+        KVH_BLOCK(true)
       }
       for (LenT b = 1; b < nb; b++) {
         const uint64_t i = 4 * (uint64_t)b;
-        const Blk c1 = A.chunk(i + 1), c2 = A.chunk(i + 2), c3 = A.chunk(i + 3), c4 = A.chunk(i + 4);
-        const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
-        c0 = c4;
-        S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
-        S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+        KVH_BLOCK(false)
+      }
+#undef KVH_BLOCK
+    }
+  } else {
+    if constexpr (AL) {
+      if (!first) {
+        {
+          const Blk c1 = A.chunk(1), c2 = A.chunk(2), c3 = A.chunk(3), c4 = A.chunk(4);
+          const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
+          c0 = c4;
+          S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
+          S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);
+        }
+        for (LenT b = 1; b < nb; b++) {
+          const uint64_t i = 4 * (uint64_t)b;
+          const Blk c1 = A.chunk(i + 1), c2 = A.chunk(i + 2), c3 = A.chunk(i + 3), c4 = A.chunk(i + 4);
+          const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
+          c0 = c4;
+          S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+          S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+        }
       }
     }
+    // trail pieces: groups 4nb .. 4nb + CM/16 + 1; piece j feeds state j,
+    // the partial piece C/16 (t bytes) state 3
+    const uint64_t i0 = 4 * (uint64_t)nb;
+    c1 = A.chunk(i0 + 1);
+    if constexpr (CM >= 16) c2 = A.chunk(i0 + 2);
+    if constexpr (CM >= 32) c3 = A.chunk(i0 + 3);
+    if constexpr (CM >= 48) c4 = A.chunk(i0 + 4);
   }
-  // trail pieces: chunks 4nb .. 4nb + CM/16 + 1; piece j feeds state j, the
-  // partial piece C/16 (t bytes) state 3
-  const uint64_t i0 = 4 * (uint64_t)nb;
-  const Blk c1 = A.chunk(i0 + 1);
-  Blk c2 = bzero(), c3 = bzero(), c4 = bzero();
-  if constexpr (CM >= 16) c2 = A.chunk(i0 + 2);
-  if constexpr (CM >= 32) c3 = A.chunk(i0 + 3);
-  if constexpr (CM >= 48) c4 = A.chunk(i0 + 4);
   const Blk q0 = A.piece(c0, c1);
   Blk q1 = bzero(), q2 = bzero(), q3 = bzero();
   if constexpr (CM >= 16) q1 = A.piece(c1, c2);
