@@ -2007,7 +2007,7 @@ Knob g_tune_wgmul{1};     // workgroups per CU multiplier
 Knob g_tune_generic{0};   // force the generic kernel
 Knob g_tune_kpl{0};       // keys per lane per chunk in k_fixed (1, 2, 4 or 8; 0 = per-length default)
 Knob g_tune_ms_lanes{1};  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
-Knob g_tune_var{13};      // var-length kernel: 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic
+Knob g_tune_var{23};      // var-length kernel: 23 = k_var9 (16 waves; 24 = 12 waves, 25 = 12 waves + block prefetch); 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic
 #ifdef KVH_EXPERIMENTS
 Knob g_tune_pf{0};        // k_fixed: 1 = register prefetch of the next chunk
 Knob g_tune_bs{0};        // hybrid kernel: bitsliced share of the keys in per mille (0 = k_fixed)

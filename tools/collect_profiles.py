@@ -10,7 +10,7 @@ dst = os.path.join(root, "profiles", rnd)
 os.makedirs(dst, exist_ok=True)
 HOT = ("k_fixed", "k_var", "k_generic", "k_fixed_ms")
 HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",), "f4": ("k_crc_fixed",), "f4v": ("k_crc_var",),
-              "c2": ("k_var6",), "c3": ("k_fixed_lanes",)}
+              "c2": ("k_var9", "k_var6"), "c3": ("k_fixed_lanes",)}
 # configs whose unit of work is one call of several kernels: (kernel name parts,
 # a kernel that runs once per call: its dispatch counts give the calls in the
 # PMC run and in the traced bench run).  f2's rocPRIM kernels are the
