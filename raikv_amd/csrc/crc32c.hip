@@ -257,6 +257,37 @@ __device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, u
   return r;
 }
 
+// kv_crc_c over one key read as dwordx4 groups of its dword-aligned span
+// (AChunks, meow_dev.hpp): one load instruction, so one L2 request, per 16
+// bytes, where crc_key_pf's byte-aligned pieces cost two and its tail up to
+// five.  Two groups are in flight ahead of the piece being stepped.
+template <class Tab>
+__device__ __forceinline__ uint32_t crc_key_g(const uint8_t* p, uint32_t len, bool safe, uint32_t r,
+                                              const Tab& T) {
+  const AChunks A(p, len, safe);
+  Blk cur = A.chunk(0), nxt = A.chunk(1);
+  uint32_t k = 0;
+  for (; 16 * k + 16 <= len; k++) {
+    const Blk nn = A.chunk(k + 2);
+    const Blk b = A.piece(cur, nxt);
+    r = T.word(r, b.w[0]); r = T.word(r, b.w[1]);
+    r = T.word(r, b.w[2]); r = T.word(r, b.w[3]);
+    cur = nxt;
+    nxt = nn;
+  }
+  const uint32_t t = len - 16 * k;
+  if (t) {
+    const Blk b = A.piece(cur, nxt);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int left = (int)t - 4 * c;
+      if (left >= 4) r = T.word(r, b.w[c]);
+      else if (left > 0) r = T.tail(r, b.w[c], (uint32_t)left);
+    }
+  }
+  return r;
+}
+
 // Variable length, length-sorted per-wave windows (the k_var6 scheme of
 // kvh.hip): one lane per key in input order runs each wave as long as its
 // longest key (zipf 8-256 B: ~25 % of the lane-steps do work).  Each wave
@@ -281,7 +312,7 @@ __device__ __attribute__((noinline)) void crc_wide_window(const uint8_t* __restr
   }
 }
 
-template <int WIN, int NW, int SH = 0, int R = 32>
+template <int WIN, int NW, int SH = 0, int R = 32, bool G = false>
 __global__ void __launch_bounds__(NW * 64)
 k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
                  const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out
@@ -298,6 +329,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* hist = hist_s[wv];
   const uint64_t nwin = (n + WIN - 1) / WIN;
+  const uint64_t kend = offs[n];  // the buffer holds every byte up to the last key's end
   for (uint64_t w = (uint64_t)blockIdx.x * NW + wv; w < nwin; w += (uint64_t)gridDim.x * NW) {
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
@@ -324,7 +356,16 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
         const uint32_t j = ridx_s[wv][pos];
         uint64_t len = rlen_s[wv][pos];
         if (len == 65535u) len = offs[i0 + j + 1] - offs[i0 + j];
-        crc[c] = crc_key_pf(keys + ws + roff_s[wv][pos], len, seeds ? seeds[i0 + j] : seed, T);
+        if constexpr (G) {
+          if (len < (1u << 31)) {  // whole groups stay inside the buffer unless the key ends within 16 bytes of it
+            const uint64_t a = ws + roff_s[wv][pos];
+            crc[c] = crc_key_g(keys + a, (uint32_t)len, a + len + 16 <= kend, seeds ? seeds[i0 + j] : seed, T);
+          } else {
+            crc[c] = crc_key_pf(keys + ws + roff_s[wv][pos], len, seeds ? seeds[i0 + j] : seed, T);
+          }
+        } else {
+          crc[c] = crc_key_pf(keys + ws + roff_s[wv][pos], len, seeds ? seeds[i0 + j] : seed, T);
+        }
         ix[c] = j;
       }
     }
@@ -343,7 +384,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
 }
 
 }  // namespace
-namespace kvh { namespace rt { std::atomic<int> g_tune_crc_var{3}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_crc_var{4}; } }
 namespace {
 
 uint32_t grid_crc(uint64_t n, int cus) {
@@ -452,6 +493,9 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 3)  // tables with 16 copies (64 KiB): 16 waves per CU
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
+                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  else if (v == 4)  // as 3, keys read as dwordx4 groups (crc_key_g)
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, true>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 2)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 8>), dim3(cus), dim3(512), 0, (hipStream_t)stream,
