@@ -449,12 +449,16 @@ int         kvh_device_synchronize(void);
  *   0 = tables per LDS (0 per-length default, 2 or 4),
  *   1 = workgroups per CU multiplier (1-8), 2 = force the generic kernel (0/1),
  *   3 = keys per lane per step in the fixed-length kernel (0 default, 1, 2, 4, 8),
- *   7 = variable-length kernel (13 default: per-wave windows sorted by 16-byte
- *       length class; 7 by exact length; 0 lane per key in input order),
+ *   7 = variable-length kernel (23 default: per-wave windows sorted by 16-byte
+ *       length class, keys read as dwordx4 groups, one straight-line variant
+ *       per chunk shape, 16 waves; 24 / 25 the same at 12 waves, 25 with the
+ *       next block's groups in flight; 13 the round-2 sorted-window kernel;
+ *       7 sorted by exact length; 0 lane per key in input order),
  *   8 = multi-seed kernel (1 lanes per key, 0 one lane per key),
- *  14 = variable-length CRC32C kernel (3 length-sorted windows, 16 waves on
- *       16-copy tables; 1 the same with 10 waves on 32-copy tables; 2 with 8
- *       waves; 0 input order),
+ *  14 = variable-length CRC32C kernel (4 default: length-sorted windows, 16
+ *       waves on 16-copy tables, keys read as dwordx4 groups; 3 the same with
+ *       byte-aligned pieces; 1 10 waves on 32-copy tables; 2 8 waves; 0 input
+ *       order),
  *  15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort radix key bits
  *       (0 auto; nonzero also selects the radix engine),
  *  18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
