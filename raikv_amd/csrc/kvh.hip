@@ -1140,8 +1140,8 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 // (window offset, length << 8 | slot), and no per-window value lives in a
 // register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
 // more take wide_window (input order, u64 offsets and lengths).
-struct VConst9 {  // VConst minus CS2b (meow_a never needs it)
-  Blk F[4], G[4], TG2, TCS0a;
+struct VConst9 {  // VConst minus CS2b (meow_a never needs it), padded to 13 blocks:
+  Blk F[4], G[4], TG2, TCS0a, pad;  // a 52-dword stride puts the 16 lengths of a class on distinct banks
 };
 template <class Tab, int NF>
 struct LdsKV9 {
@@ -2702,7 +2702,7 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
                          out, flags);
       return launch_done();
     case 23:
-      hipLaunchKernelGGL((k_var9<2, 16, 192>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
+      hipLaunchKernelGGL((k_var9<2, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
       return launch_done();
     case 24:
