@@ -1237,7 +1237,9 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 #pragma unroll
     for (int m = 0; m < M; m++) {
       const uint32_t j = lane + 64 * m;
-      b[m] = (L[m] >> 4) < 255u ? (L[m] >> 4) : 255u;
+      // 64 length classes x 4 sub-counters by lane & 3: a quarter of the
+      // same-address atomics (a class's keys in one instruction serialise)
+      b[m] = ((L[m] >> 4) < 63u ? (L[m] >> 4) : 63u) * 4u + (lane & 3u);
       r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
     }
     wave_sync();
