@@ -312,14 +312,14 @@ __device__ __attribute__((noinline)) void crc_wide_window(const uint8_t* __restr
   }
 }
 
-template <int WIN, int NW, int SH = 0, int R = 32, bool G = false>
+template <int WIN, int NW, int SH = 0, int R = 32, bool G = false, int SUB = 1>
 __global__ void __launch_bounds__(NW * 64)
 k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
                  const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out
   constexpr int M = WIN / 64;
   static_assert(WIN <= 256 * 4, "hist slice doubles as the CRC staging area");
   __shared__ uint32_t lds[R == 32 ? kWords : kWords / 2];
-  __shared__ uint32_t hist_s[NW][WIN > 256 ? WIN : 256];
+  __shared__ uint32_t hist_s[NW][(WIN > 256 ? WIN : 256) * SUB];
   __shared__ uint32_t roff_s[NW][WIN];
   __shared__ uint16_t rlen_s[NW][WIN];
   __shared__ uint16_t ridx_s[NW][WIN];
@@ -344,7 +344,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
       crc_wide_window<R>(keys, offs, i0, k, M, seeds, seed, out, lds);
       continue;
     }
-    const uint64_t ws = wave_sort_from<WIN, SH>(W, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
+    const uint64_t ws = wave_sort_from<WIN, SH, SUB>(W, k, hist, roff_s[wv], rlen_s[wv], ridx_s[wv]);
     // (running the lane's M keys as interleaved chains was slower: each
     // lane then steps as long as its longest key, chunk M-1's)
     uint32_t crc[M], ix[M];
@@ -496,6 +496,9 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 4)  // as 3, keys read as dwordx4 groups (crc_key_g)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, true>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
+                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  else if (v == 5)  // as 4, two sub-counters per length bucket in the window sort
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, true, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 2)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 8>), dim3(cus), dim3(512), 0, (hipStream_t)stream,

@@ -119,11 +119,14 @@ __device__ __forceinline__ WinOffs<WIN> win_load(const uint64_t* __restrict__ of
 // SH: bucket = min(len >> SH, 255).  SH = 0 sorts by exact length; SH = 4 by
 // 16-byte class (same full-block count, so the same trip counts), which keeps
 // a class in address order (the counting sort is stable) and so coalesces
-// the chunk's key gathers.
-template <int WIN, int SH = 0>
+// the chunk's key gathers.  SUB sub-counters per bucket (by lane % SUB; hist
+// holds 256 * SUB words) divide the same-address LDS atomics of one
+// instruction -- a bucket's keys in one instruction serialise -- by SUB.
+template <int WIN, int SH = 0, int SUB = 1>
 __device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32_t k, uint32_t* hist,
                                                    uint32_t* r_off, uint16_t* r_len, uint16_t* r_idx) {
-  constexpr int M = WIN / 64;
+  constexpr int M = WIN / 64, HQ = 4 * SUB;  // hist words per lane
+  static_assert(SUB == 1 || SUB == 2 || SUB == 4, "sub-counters");
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t ws = W.ws;
   uint32_t o[M], L[M], r[M];
@@ -132,19 +135,22 @@ __device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32
     o[m] = (uint32_t)(W.a[m] - ws);
     L[m] = W.e[m] - W.a[m] < 65535 ? (uint32_t)(W.e[m] - W.a[m]) : 65535u;
   }
+  uint32_t bk[M];
 #pragma unroll
-  for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
+  for (int m = 0; m < M; m++) bk[m] = ((L[m] >> SH) < 255u ? (L[m] >> SH) : 255u) * SUB + (lane % SUB);
+#pragma unroll
+  for (int q = 0; q < HQ; q++) hist[lane * HQ + q] = 0;
   wave_lds_sync();
 #pragma unroll
   for (int m = 0; m < M; m++) {
     const uint32_t j = lane + 64 * m;
-    r[m] = j < k ? atomicAdd(&hist[(L[m] >> SH) < 255u ? (L[m] >> SH) : 255u], 1u) : 0u;
+    r[m] = j < k ? atomicAdd(&hist[bk[m]], 1u) : 0u;
   }
   wave_lds_sync();
   {
-    uint32_t v[4], sum = 0;
+    uint32_t v[HQ], sum = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
+    for (int q = 0; q < HQ; q++) { v[q] = hist[lane * HQ + q]; sum += v[q]; }
     uint32_t inc = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -153,14 +159,14 @@ __device__ __forceinline__ uint64_t wave_sort_from(const WinOffs<WIN>& W, uint32
     }
     uint32_t run = inc - sum;
 #pragma unroll
-    for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
+    for (int q = 0; q < HQ; q++) { hist[lane * HQ + q] = run; run += v[q]; }
   }
   wave_lds_sync();
 #pragma unroll
   for (int m = 0; m < M; m++) {
     const uint32_t j = lane + 64 * m;
     if (j < k) {
-      const uint32_t pos = hist[(L[m] >> SH) < 255u ? (L[m] >> SH) : 255u] + r[m];
+      const uint32_t pos = hist[bk[m]] + r[m];
       r_off[pos] = o[m];
       r_len[pos] = (uint16_t)L[m];
       r_idx[pos] = (uint16_t)j;
