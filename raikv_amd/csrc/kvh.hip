@@ -1167,7 +1167,7 @@ struct LdsKV9 {
   __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
 };
 
-template <int NT, int NW, int KF, bool PF = false>
+template <int NT, int NW, int KF, bool PF = false, bool PR = false>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -1279,6 +1279,23 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       const bool al = __ballot(kl >= 64u) != 0;
       const int cm = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
                    : __ballot((kl & 48u) >= 16u) ? 16 : 0;
+      if constexpr (PR) {  // experiments: long keys two lanes per key (meow_pair), the chunk as two 32-key halves
+      if (al) {
+        const auto sx = __builtin_amdgcn_permlane32_swap(rc.x, rc.x, false, false);
+        const auto sy = __builtin_amdgcn_permlane32_swap(rc.y, rc.y, false, false);
+        const uint32_t hh = lane >> 5;
+#pragma unroll 1
+        for (int ps = 0; ps < 2; ps++) {
+          const uint32_t px = ps ? sx[1] : sx[0], py = ps ? sy[1] : sy[0];
+          const bool v2 = 64 * c + 32 * ps + (lane & 31) < k;
+          const uint32_t o2 = v2 ? px : 0u, kl2 = v2 ? py >> 8 : 0u;
+          const LdsKV9<LdsTab<NT>, KF> K2(kfull, kf, kl2, s1, s2, T);
+          const Blk h2 = meow_pair(base + o2, kl2, hh, (uint64_t)o2 + kl2 + 16 <= wend, K2, T);
+          if (v2 && hh == 0) stage[py & 255u] = fix ? fixup(h2) : h2;
+        }
+        continue;
+      }
+      }
       if (valid) {
         const uint8_t* p = base + rc.x;
         const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
@@ -2721,6 +2738,14 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
   }
 #ifdef KVH_EXPERIMENTS
   switch (var) {
+    case 26:  // k_var9 with long keys two lanes per key (meow_pair), 16 waves: spills, 3.75 ms
+      hipLaunchKernelGGL((k_var9<2, 16, 256, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n,
+                         seed1, seed2, out, flags);
+      return launch_done();
+    case 27:  // the same at 12 waves: 10 % fewer LDS instructions, 3.14 vs 3.03 ms (two serial passes)
+      hipLaunchKernelGGL((k_var9<2, 12, 192, true, true>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n,
+                         seed1, seed2, out, flags);
+      return launch_done();
     case 18:
       hipLaunchKernelGGL((k_var8<2, 256, 4>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1,
                          seed2, out, flags);
@@ -3136,7 +3161,7 @@ int kvh_set_tuning(int k, int value) {
             return set(g_tune_kpl, value);
     case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25)) {
 #ifdef KVH_EXPERIMENTS
-              if (value < 2 || value > 22) return KVH_EINVAL;
+              if (value < 2 || value > 27) return KVH_EINVAL;
 #else
               return KVH_EINVAL;
 #endif

@@ -793,6 +793,77 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
   return aesdec(S0b, M, T);
 }
 
+// Long keys, two lanes per key.  Until Compress a Meow state only ever meets
+// its own 16-byte column of each block and its own trail chunk
+// (key_hash.c:1155-1226), so lane half h (lane >> 5) carries states 2h and
+// 2h+1 of the key both lanes of a pair were given: each lane loads the three
+// dwordx4 groups its two columns need per block and runs two chains.  Mix is
+// per state; Compress splits evenly: both halves form W = AESDEC(X, Y) and
+// Z = T(W), which is T(AESDEC(S0, S1)) in the low half and, XORed with M,
+// Compress_Meow2's AESDEC(AESDEC(S2, S3), M) in the high half; one
+// v_permlane32_swap hands the high half's value down, and the low half runs
+// the last round.  Against one lane per key this halves the lanes a chunk of
+// long keys waits on its longest key for: a 64-key chunk is two 32-key
+// halves, each as long as its own longest key (simulated over the C2 lengths:
+// 1.60x -> 1.38x the ideal rounds).  Every lane must be active (permlane);
+// a lane without a key passes L = 0.  The hash is valid in the low half.
+template <class Tab, class KGet>
+__device__ __forceinline__ Blk meow_pair(const uint8_t* p, uint32_t L, uint32_t h, bool safe, const KGet& K,
+                                         const Tab& T) {
+  const uint32_t nb = L >> 6, C = L & 48, t = L & 15;
+  const bool first = nb == 0;
+  const bool hi = h != 0;
+  const int ix = 2 * (int)h, iy = ix + 1;
+  const AChunks A(p, L, safe);
+  const Blk M = K.M();
+  Blk X = bxor(ramp(ix), M), Y = bxor(ramp(iy), M);
+  if (!first) {
+    {
+      const Blk G0 = A.chunk(ix), G1 = A.chunk(ix + 1), G2 = A.chunk(ix + 2);
+      const Blk kx = A.piece(G0, G1), ky = A.piece(G1, G2);
+      X = aesdec(bxor(K.F(ix), kx), kx, T);
+      Y = aesdec(bxor(K.F(iy), ky), ky, T);
+    }
+    for (uint32_t b = 1; b < nb; b++) {
+      const uint64_t g = 4 * (uint64_t)b + ix;
+      const Blk G0 = A.chunk(g), G1 = A.chunk(g + 1), G2 = A.chunk(g + 2);
+      const Blk kx = A.piece(G0, G1), ky = A.piece(G1, G2);
+      X = aesdec(aesdec(X, kx, T), kx, T);
+      Y = aesdec(aesdec(Y, ky, T), ky, T);
+    }
+  }
+  // trail: X takes piece 2h (state 0: C >= 16; state 2: C >= 48), Y piece 1
+  // (state 1: C >= 32) or the partial piece C/16 of t bytes (state 3)
+  const uint64_t i0 = 4 * (uint64_t)nb;
+  const Blk z = bzero();
+  const Blk g0 = A.chunk(i0), g1 = A.chunk(i0 + 1), g2 = A.chunk(i0 + 2);
+  const Blk g3 = hi ? A.chunk(i0 + 3) : z, g4 = hi ? A.chunk(i0 + 4) : z;
+  const Blk kx = A.piece(bsel(hi, g2, g0), bsel(hi, g3, g1));
+  const uint32_t j = C >> 4;
+  const Blk ya = bsel(j == 0, g0, bsel(j == 1, g1, bsel(j == 2, g2, g3)));
+  const Blk yb = bsel(j == 0, g1, bsel(j == 1, g2, bsel(j == 2, g3, g4)));
+  Blk ky = A.piece(bsel(hi, ya, g1), bsel(hi, yb, g2));
+  ky = bsel(hi, mask_bytes(ky, t), ky);
+  const bool cx = hi ? C >= 48 : C >= 16, cy = hi ? t != 0 : C >= 32;
+  {
+    const Blk X2 = aesdec(bsel(first, bxor(K.F0(ix), kx), aesdec(X, kx, T)), kx, T);
+    const Blk Y2 = aesdec(bsel(first, bxor(K.F0(iy), ky), aesdec(Y, ky, T)), ky, T);
+    X = bsel(cx, X2, X);
+    Y = bsel(cy, Y2, Y);
+  }
+  X = aesdec(X, M, T);  // Mix_Meow (an untouched state holds its init value: this gives G)
+  Y = aesdec(Y, M, T);
+  const Blk Z = aesT(aesdec(X, Y, T), T);
+  const Blk V = bsel(hi, bxor(Z, M), Z);
+  Blk S0b;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const auto r = __builtin_amdgcn_permlane32_swap(V.w[w], V.w[w], false, false);
+    S0b.w[w] = Z.w[w] ^ r[1];  // low half: T(AESDEC(S0, S1)) ^ S2b
+  }
+  return aesdec(S0b, M, T);
+}
+
 // constants held in registers (uniform length)
 struct RegK {
   const MeowConst& k;
