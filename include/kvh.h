@@ -455,10 +455,11 @@ int         kvh_device_synchronize(void);
  *       next block's groups in flight; 13 the round-2 sorted-window kernel;
  *       7 sorted by exact length; 0 lane per key in input order),
  *   8 = multi-seed kernel (1 lanes per key, 0 one lane per key),
- *  14 = variable-length CRC32C kernel (4 default: length-sorted windows, 16
- *       waves on 16-copy tables, keys read as dwordx4 groups; 3 the same with
- *       byte-aligned pieces; 1 10 waves on 32-copy tables; 2 8 waves; 0 input
- *       order),
+ *  14 = variable-length CRC32C kernel (6 default: length-sorted windows, 16
+ *       waves on 16-copy tables, keys read as dwordx4 groups, the next key's
+ *       first groups in flight; 4 without that; 5 with split histogram
+ *       counters; 3 byte-aligned pieces; 1 10 waves on 32-copy tables; 2 8
+ *       waves; 0 input order),
  *  15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort radix key bits
  *       (0 auto; nonzero also selects the radix engine),
  *  18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and

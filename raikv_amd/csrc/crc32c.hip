@@ -262,6 +262,30 @@ __device__ __forceinline__ uint32_t crc_key_pf(const uint8_t* p, uint64_t len, u
 // bytes, where crc_key_pf's byte-aligned pieces cost two and its tail up to
 // five.  Two groups are in flight ahead of the piece being stepped.
 template <class Tab>
+__device__ __forceinline__ uint32_t crc_key_g2(const AChunks& A, uint32_t len, uint32_t r, const Tab& T, Blk cur,
+                                               Blk nxt) {
+  uint32_t k = 0;
+  for (; 16 * k + 16 <= len; k++) {
+    const Blk nn = A.chunk(k + 2);
+    const Blk b = A.piece(cur, nxt);
+    r = T.word(r, b.w[0]); r = T.word(r, b.w[1]);
+    r = T.word(r, b.w[2]); r = T.word(r, b.w[3]);
+    cur = nxt;
+    nxt = nn;
+  }
+  const uint32_t t = len - 16 * k;
+  if (t) {
+    const Blk b = A.piece(cur, nxt);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int left = (int)t - 4 * c;
+      if (left >= 4) r = T.word(r, b.w[c]);
+      else if (left > 0) r = T.tail(r, b.w[c], (uint32_t)left);
+    }
+  }
+  return r;
+}
+template <class Tab>
 __device__ __forceinline__ uint32_t crc_key_g(const uint8_t* p, uint32_t len, bool safe, uint32_t r,
                                               const Tab& T) {
   const AChunks A(p, len, safe);
@@ -312,7 +336,7 @@ __device__ __attribute__((noinline)) void crc_wide_window(const uint8_t* __restr
   }
 }
 
-template <int WIN, int NW, int SH = 0, int R = 32, bool G = false, int SUB = 1>
+template <int WIN, int NW, int SH = 0, int R = 32, int G = 0, int SUB = 1>
 __global__ void __launch_bounds__(NW * 64)
 k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
                  const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out
@@ -348,15 +372,48 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
     // (running the lane's M keys as interleaved chains was slower: each
     // lane then steps as long as its longest key, chunk M-1's)
     uint32_t crc[M], ix[M];
+    // G == 2: the first two groups of the lane's next key are in flight while
+    // it steps through the current one (keys of 64 KiB and more re-read theirs)
+    Blk pf0 = bzero(), pf1 = bzero();
+    auto pre = [&](uint32_t pos, Blk& g0, Blk& g1) {
+      g0 = bzero();
+      g1 = bzero();
+      if (pos < k) {
+        const uint32_t ln = rlen_s[wv][pos];
+        const uint64_t a = ws + roff_s[wv][pos];
+        const AChunks A(keys + a, ln, a + ln + 16 <= kend);
+        g0 = A.chunk(0);
+        g1 = A.chunk(1);
+      }
+    };
+    if constexpr (G == 2) pre(lane, pf0, pf1);
 #pragma unroll
     for (int c = 0; c < M; c++) {
       const uint32_t pos = 64 * c + lane;
       ix[c] = 0xffffffffu;
+      Blk nf0, nf1;
+      if constexpr (G == 2) {
+        if (c + 1 < M) pre(pos + 64, nf0, nf1);
+      }
       if (pos < k) {
         const uint32_t j = ridx_s[wv][pos];
         uint64_t len = rlen_s[wv][pos];
+        if constexpr (G == 2) {
+          const uint64_t a = ws + roff_s[wv][pos];
+          if (len < 65535u) {
+            const AChunks A(keys + a, len, a + len + 16 <= kend);
+            crc[c] = crc_key_g2(A, (uint32_t)len, seeds ? seeds[i0 + j] : seed, T, pf0, pf1);
+          } else {
+            len = offs[i0 + j + 1] - offs[i0 + j];
+            if (len < (1u << 31)) crc[c] = crc_key_g(keys + a, (uint32_t)len, a + len + 16 <= kend, seeds ? seeds[i0 + j] : seed, T);
+            else crc[c] = crc_key_pf(keys + a, len, seeds ? seeds[i0 + j] : seed, T);
+          }
+          ix[c] = j;
+          if (c + 1 < M) { pf0 = nf0; pf1 = nf1; }
+          continue;
+        }
         if (len == 65535u) len = offs[i0 + j + 1] - offs[i0 + j];
-        if constexpr (G) {
+        if constexpr (G != 0) {
           if (len < (1u << 31)) {  // whole groups stay inside the buffer unless the key ends within 16 bytes of it
             const uint64_t a = ws + roff_s[wv][pos];
             crc[c] = crc_key_g(keys + a, (uint32_t)len, a + len + 16 <= kend, seeds ? seeds[i0 + j] : seed, T);
@@ -367,6 +424,9 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
           crc[c] = crc_key_pf(keys + ws + roff_s[wv][pos], len, seeds ? seeds[i0 + j] : seed, T);
         }
         ix[c] = j;
+      }
+      if constexpr (G == 2) {
+        if (c + 1 < M) { pf0 = nf0; pf1 = nf1; }
       }
     }
     wave_lds_sync();  // the records are read; the hist slice becomes the staging area
@@ -384,7 +444,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
 }
 
 }  // namespace
-namespace kvh { namespace rt { std::atomic<int> g_tune_crc_var{4}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_crc_var{6}; } }
 namespace {
 
 uint32_t grid_crc(uint64_t n, int cus) {
@@ -495,10 +555,13 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 4)  // as 3, keys read as dwordx4 groups (crc_key_g)
-    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, true>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 1>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
+                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  else if (v == 6)  // as 4, the next key's first two groups in flight
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 5)  // as 4, two sub-counters per length bucket in the window sort
-    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, true, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 1, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 2)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 8>), dim3(cus), dim3(512), 0, (hipStream_t)stream,

@@ -131,7 +131,7 @@ def test_full_size_var_property(kvh):
     assert c == s
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("n", [1, 255, 257, 2561])
 def test_var_kernels_vs_oracle(kvh, kernel, n):
     """Both variable-length kernels (input order; length-sorted windows, knob
