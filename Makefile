@@ -10,9 +10,10 @@ SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/ht_pos.hip raikv_amd/csrc/crc3
 OBJS     := $(SRCS:.hip=.o)
 HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/csrc/kvh_internal.hpp \
             raikv_amd/csrc/ht_pos.hpp raikv_amd/csrc/bs_prelude.hpp raikv_amd/csrc/bs_aes.hpp \
-            raikv_amd/csrc/bs_meow.hpp include/kvh.h include/raikv_amd/key_hash.hpp
+            raikv_amd/csrc/bs_meow.hpp raikv_amd/csrc/kvh_var.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
-CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/paths_gpu tools/copy_peak tools/fetch_calib
+CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/host_latency tests/cpp/paths_gpu \
+             tools/copy_peak tools/fetch_calib
 
 KV_LIB   := raikv_amd/libkvh_kv.so
 
@@ -30,17 +31,19 @@ $(KV_LIB): raikv_amd/csrc/kv_compat.cpp raikv_amd/csrc/kv_compat.map include/kvh
 	g++ -O2 -std=c++17 -fPIC -shared $(INC) -Wl,--version-script=raikv_amd/csrc/kv_compat.map -o $@ $< \
 	    -L raikv_amd -lkvh -Wl,-rpath,'$$ORIGIN'
 
-# Research build (NOT the product): the same sources with -DKVH_EXPERIMENTS,
-# which adds the superseded kernels and the ablation builds (outputs that are
-# not hashes) behind extra kvh_set_tuning knobs.  Used by tools/*.py through
-# KVH_LIB=tools/libkvh_exp.so; never loaded by the tests of the product path.
+# Research build (NOT the product): the product objects plus the research
+# kernels of tools/exp/ (variants that lost their A/B, ablation builds whose
+# outputs are not hashes), which register themselves behind extra
+# kvh_set_tuning values (raikv_amd/csrc/kvh_internal.hpp: rt::g_exp).  Used by
+# tools/*.py through KVH_LIB=tools/libkvh_exp.so; never loaded by the tests
+# of the product path.
 EXP_LIB  := tools/libkvh_exp.so
-EXP_OBJS := $(SRCS:raikv_amd/csrc/%.hip=tools/exp/%.o)
-tools/exp/%.o: raikv_amd/csrc/%.hip $(HDRS)
-	@mkdir -p tools/exp
-	$(HIPCC) $(HIPFLAGS) -DKVH_EXPERIMENTS $(INC) -c -o $@ $<
-$(EXP_LIB): $(EXP_OBJS) raikv_amd/csrc/kvh.map
-	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(EXP_OBJS)
+EXP_SRCS := tools/exp/kvh_exp.hip
+EXP_OBJS := $(EXP_SRCS:.hip=.o)
+tools/exp/%.o: tools/exp/%.hip tools/exp/meow_exp.hpp $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(INC) -c -o $@ $<
+$(EXP_LIB): $(OBJS) $(EXP_OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(OBJS) $(EXP_OBJS)
 experiments: $(EXP_LIB)
 
 oracle:
@@ -63,6 +66,13 @@ tests/cpp/paths_gpu: tests/cpp/paths_gpu.cpp $(LIB) include/raikv_amd/key_hash.h
 tests/cpp/e2e_host: tests/cpp/e2e_host.cpp $(LIB) include/kvh.h
 	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
 	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
+
+# per-call latency of the host pipelines at raikv's batch sizes, beside the
+# reference CPU path (dlopen'ed from oracle/_ref at run time, test-only)
+tests/cpp/host_latency: tests/cpp/host_latency.cpp $(LIB) include/kvh.h
+	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 -ldl \
 	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
 
 # measurement: the box's achievable streaming rate for bench.py's roofline

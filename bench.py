@@ -1,14 +1,17 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident 128-bit Meow key-hash throughput on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4|c4g|c64|...]
 
 A "step" is one pass of the hot path (one kvh_meow128_* launch) over one
-batch of synthetic keys already resident in HBM.  Default workload is
-BASELINE.json configs[1] (C1: 100M fixed 16-byte keys per GPU).  For N>1
-(torch.distributed.run, one rank per GPU) every rank hashes its own batch:
-keys are independent, there is no data-path collective ("scaling": "weak");
-a CPU gloo group only carries the barrier and the max-over-ranks time.
+batch of synthetic keys already resident in HBM.  Default workload at N=1 is
+BASELINE.json configs[1] (C1: 100M fixed 16-byte keys); at N>1 it is
+configs[4] as stated (c4g: ONE global batch of 1B 32-byte keys, rank r
+hashing index range shard_range(1B, r, N), "scaling": "strong"; per-GPU and
+aggregate rates in the line).  Keys are independent: there is no data-path
+collective; a CPU gloo group only carries the barrier and the max-over-ranks
+time.  The other configs ("c1".."c4", "c64", the §8 f rows) keep a fixed
+per-GPU batch ("scaling": "weak").
 
 The JSON line carries
   roofline     : algorithmic bytes/launch / avg kernel time (HIP events on
@@ -42,7 +45,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 # (MI355X_MICROARCH.md §LDS, 128 B/clk), 256 CUs, 2.4 GHz peak engine clock
 LDS_PEAK_LOOKUPS = 32 * 256 * 2.4e9
 # T-table lookups per unit of work (16 per AES round; folded rounds)
-LOOKUPS_PER_UNIT = {"c1": 5 * 16, "c4": 7 * 16, "c3": 4 * 7 * 16, "f1": 5 * 16, "f4": 16}
+LOOKUPS_PER_UNIT = {"c1": 5 * 16, "c4": 7 * 16, "c4g": 7 * 16, "c64": 13 * 16, "c3": 4 * 7 * 16, "f1": 5 * 16,
+                    "f4": 16}
+# the float4 copy rate MI355X_MICROARCH.md records for this part (the guide's
+# achievable streaming figure, beside the box's own copy probe)
+GUIDE_COPY_GBS = 6290.0
 
 CONFIGS = {
     "c1": dict(workload="C1: 100M fixed 16-byte keys resident in HBM, one lane per key, bit-exact vs reference",
@@ -53,6 +60,13 @@ CONFIGS = {
                n=50_000_000, key_len=32, arity=4, var=False),
     "c4": dict(workload="C4: 32-byte keys, 125M per GPU (1B over 8 GPUs), sharded by index range",
                n=125_000_000, key_len=32, arity=1, var=False),
+    # BASELINE configs[4] as stated: one global 1B x 32 B batch, index-range shards (strong scaling)
+    "c4g": dict(workload="C4: 1B 32-byte keys, one global batch sharded by index range across the GPUs "
+                         "(per-GPU and aggregate hashes/s)",
+                n=1_000_000_000, key_len=32, arity=1, var=False, global_batch=True),
+    # the metric's top length: 100M x 64-byte keys (80 B/key: 64 in + 16 out)
+    "c64": dict(workload="C64: 100M fixed 64-byte keys resident in HBM (the 64 B end of the metric's 16-64 B range)",
+                n=100_000_000, key_len=64, arity=1, var=False),
     # SURVEY.md §8 f1 (next row): the consumer side of the hash
     "f1": dict(workload="F1: 100M fixed 16-byte keys -> Meow128 + fixup + cuckoo arity-4 table positions "
                         "(64 GiB map, 4 buckets), hashes and u64 positions stored; one fused kernel",
@@ -372,7 +386,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c1 at N=1, c4g (BASELINE configs[4], strong scaling) at N>1")
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -384,8 +399,6 @@ def main():
                          "power transient (DESIGN.md §4.5); 0 disables")
     ap.add_argument("--no-copy-peak", action="store_true", help="skip the achievable-peak copy probe")
     args = ap.parse_args()
-    if args.e2e is None:
-        args.e2e = args.config in ("c1", "c2")
 
     import torch
 
@@ -396,9 +409,19 @@ def main():
     import raikv_amd as kvh
     from raikv_amd.workload import STATIC_SEED, C3_SEEDS, zipf_lengths, offsets_from_lengths
 
+    if args.config is None:
+        args.config = "c1" if world == 1 else "c4g"
+    if args.e2e is None:
+        args.e2e = args.config in ("c1", "c2")
     cfg = dict(CONFIGS[args.config])
     if args.keys:
         cfg["n"] = args.keys
+    n_global = cfg["n"]
+    if cfg.get("global_batch"):  # this rank's index range of the one global batch
+        from raikv_amd.workload import shard_range
+        lo, hi = shard_range(n_global, rank, world)
+        cfg["n"] = hi - lo
+        cfg["shard"] = [lo, hi]
     n, L, arity = cfg["n"], cfg["key_len"], cfg["arity"]
     seed = STATIC_SEED
     gen = torch.Generator(device="cuda")
@@ -522,7 +545,8 @@ def main():
     wall = kdist.reduce_max(wall, world)
 
     units = cfg["tokens"] if cfg.get("ingest") else n * arity
-    n_hash = units * args.steps * world  # keys for the f1/f3/f4 configs
+    # keys for the f1/f3/f4 configs; a global batch counts its keys once
+    n_hash = (n_global * arity if cfg.get("global_batch") else units * world) * args.steps
     value = n_hash / wall
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic, tsrc = load_traffic(args.config)
@@ -537,12 +561,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if cfg.get("global_batch") else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (seeded uniform random key bytes generated on device; zipf lengths for C2)",
         "config": {"workload": cfg["workload"], "config": args.config,
                    "keys_per_gpu": cfg.get("tokens", n), **({"text_bytes": n} if cfg.get("ingest") else {}),
+                   **({"global_keys": n_global, "shard_rank0": cfg["shard"]} if cfg.get("global_batch") else {}),
                    "key_len": L if L else "zipf 8-256", "hashes_per_key": arity,
                    "seed": ["0x%016x" % seed[0], "0x%016x" % seed[1]],
                    "parallelism": f"shard x{world} (index ranges, no collective)"},
@@ -553,8 +578,11 @@ def main():
                      "traffic_source": tsrc},
         "settle": {"ms": args.settle_ms, "launches": settle_n},
         "hashes_per_s_per_gpu": n * arity / (kern_ms * 1e-3),
+        "hashes_per_s_aggregate": n_hash / wall,
         "lds_roofline": lds_line(args.config, units, kern_ms),
     }
+    res["roofline"]["guide_copy_peak"] = GUIDE_COPY_GBS
+    res["roofline"]["frac_vs_guide_copy"] = achieved / GUIDE_COPY_GBS
     if rank == 0 and world == 1 and not args.no_copy_peak:
         cp = copy_peak(alg_bytes)
         if cp.get("copy_GBps"):

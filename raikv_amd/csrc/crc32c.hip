@@ -57,7 +57,6 @@ static_assert(kCrc.t[0][1] == 0xF26B8303u, "CRC32C table");  // standard Castagn
 
 __constant__ CrcTabs c_crc = kCrc;
 
-constexpr int kBlock = 1024;
 constexpr int kWords = 4 * 8192;  // 4 tables x 256 entries x 32 copies
 
 // LDS slot s holds table T_{3-s}, so slot s is indexed by byte s of x.

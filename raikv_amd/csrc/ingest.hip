@@ -649,7 +649,7 @@ __device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, co
   }
 }
 
-template <int NT, int NH, int ABL = 0, int PD = 2>
+template <int NT, int NH, int PD = 2>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
@@ -727,7 +727,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
 #pragma unroll
     for (int h = 0; h < NH; h++) {  // text of chunk b + step
       const uint32_t D1 = mD[un][h];
-      tr[x ^ 1][h] = short_issue(buf + mo[un][h], D1, ABL < 2 && b + step + 64 * h + lane < n && D1 && is_short(D1));
+      tr[x ^ 1][h] = short_issue(buf + mo[un][h], D1, b + step + 64 * h + lane < n && D1 && is_short(D1));
       tr[x ^ 1][h].D = D1;
     }
     bool valid[NH], shrt[NH];
@@ -746,16 +746,12 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
         ShortRaw r = tr[x][h];
         r.D = D0;
         const Blk k0 = short_key(r, psel);
-        if constexpr (ABL != 0) {  // ablation: loads and stores only (2: no text loads either)
-          hh[h] = bxor(k0, kfull[D0 + nul].M);
-        } else {
         const MeowConst& c = kfull[D0 + nul];
         const Blk M = c.M;
         Blk S3 = aesdec(bxor(c.F[3], k0), k0, T);
         S3 = aesdec(S3, M, T);
         const Blk S2 = aesdec(bxor(c.TG2, S3), M, T);
         hh[h] = aesdec(bxor(c.TCS0a, S2), M, T);
-        }
       }
 #pragma unroll
       for (int h = 0; h < NH; h++)
@@ -778,7 +774,6 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
         ql += (uint32_t)__popcll(lm);
       }
     }
-    if (ABL == 3) qn = ql = 0;  // ablation: no medium / long path
     if (qn >= 64 || ql >= 64) {
       wave_lds_sync();
       while (qn >= 64) {
@@ -1045,15 +1040,6 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
   const int sk = g_tune_spans.load(std::memory_order_relaxed);
-#ifdef KVH_EXPERIMENTS
-  if (sk == 3)  // ablation: loads and stores, no table rounds (outputs are not hashes)
-    hipLaunchKernelGGL((k_spans<4, 2, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
-                       lens, (uint64_t)n, seed1, seed2, out, flags);
-  else if (sk == 4)  // ablation: offsets/lengths in, hashes out only (no text, no medium/long path)
-    hipLaunchKernelGGL((k_spans<4, 2, 3>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
-                       lens, (uint64_t)n, seed1, seed2, out, flags);
-  else
-#endif
   if (sk == 2)
     hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);

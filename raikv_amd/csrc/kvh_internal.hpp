@@ -10,6 +10,8 @@
 
 namespace kvh {
 
+constexpr int kBlock = 1024;  // threads per workgroup of the streaming kernels (16 waves)
+
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
@@ -205,6 +207,22 @@ extern std::atomic<int> g_tune_sort_engine;
 extern std::atomic<int> g_tune_spans;
 // tokenizer: 1 = wave-chunked (default), 0 = workgroup-chunked
 extern std::atomic<int> g_tune_tok;
+
+// Research-build hook table.  libkvh.so leaves it empty.  The experiments
+// library (`make experiments` -> tools/libkvh_exp.so: these objects plus
+// tools/exp/*.o) fills it from a static initialiser, so the research kernels
+// stay reachable through the same C-ABI calls and kvh_set_tuning knobs
+// without living in the product sources.  Each launcher returns false when
+// the knob value is not one of its own (the product path then runs).
+struct ExpHooks {
+  int (*set_tuning)(int k, int value);  // previous value, or KVH_EINVAL: not a research knob
+  bool (*var_knob)(int value);          // a research value of knob 7
+  bool (*fixed)(int L, const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,
+                hipStream_t st, int cus, int tune_nt, int tune_kpl, int* rc);
+  bool (*var)(int knob7, const uint8_t* keys, const uint64_t* offs, uint64_t n, uint64_t s1, uint64_t s2,
+              uint64_t* out, uint32_t flags, hipStream_t st, int cus, int* rc);
+};
+extern ExpHooks g_exp;
 }  // namespace rt
 
 }  // namespace kvh

@@ -9,7 +9,8 @@ batch against an independent device kernel (the straight-line per-key
 restatement k_seeded, or the generic runtime-length kernel); and
 determinism.  Configs (BASELINE.json `configs`): C2 = 100M zipf 8-256 B keys
 (4.87 GB of key bytes: offsets past 2^32), C3 = 50M x 32 B x 4 seeds,
-C4 = 125M x 32 B (one GPU's shard of 1B).  C1 is in test_gpu_parity.py.
+C4 = 125M x 32 B (one GPU's shard of 1B) and the whole 1B x 32 B global
+batch on one GPU.  C1 is in test_gpu_parity.py.
 
 Window spans >= 4 GiB: the length-sorted kernels keep u32 window-relative
 offsets; a window whose bytes span 4 GiB or more takes a u64 input-order
@@ -144,6 +145,41 @@ def test_c4_full_shard(kvh):
     lo, hi = shard_range(n, 3, 8)
     part = kvh.meow128_fixed(keys[lo * L:hi * L], L, STATIC)
     assert torch.equal(part, out[lo:hi])
+
+
+def test_c4g_one_global_batch_on_one_gpu(kvh):
+    """C4 as BASELINE configs[4] states it (bench.py --config c4g, the N>1
+    default): ONE global batch of 1B 32-byte keys (32 GB of keys, 16 GB of
+    hashes), hashed by one launch on one MI355X.  20k sampled keys + the
+    first/last keys == oracle; the whole batch == the generic runtime-length
+    kernel; the index-range shards that bench.py gives ranks 0..7 of N = 2, 4
+    and 8 hashed on their own == their slices of the one-launch result."""
+    n, L = 1_000_000_000, 32
+    g = torch.Generator(device="cuda")
+    g.manual_seed(404)
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    out = kvh.meow128_fixed(keys, L, STATIC)
+    prev = kvh.lib.kvh_set_tuning(2, 1)
+    try:
+        gen = kvh.meow128_fixed(keys, L, STATIC)
+    finally:
+        kvh.lib.kvh_set_tuning(2, prev)
+    assert torch.equal(out, gen), "k_fixed != k_generic on the 1B batch"
+    del gen
+    rng = np.random.default_rng(404)
+    idx = np.unique(np.concatenate([rng.choice(n, 20_000, replace=False), np.arange(0, 100), np.arange(n - 100, n)]))
+    ti = torch.from_numpy(idx).cuda()
+    kb = keys.view(n, L)[ti].cpu().numpy().reshape(-1)
+    h = out[ti].cpu().numpy().view(np.uint64)
+    loc = np.arange(0, (len(idx) + 1) * L, L, dtype=np.uint64)
+    np.testing.assert_array_equal(h, orc_sample(kb, loc, STATIC))
+    from raikv_amd.workload import shard_range
+    for world in (2, 4, 8):
+        for r in sorted({0, world // 2, world - 1}):
+            lo, hi = shard_range(n, r, world)
+            part = kvh.meow128_fixed(keys[lo * L:hi * L], L, STATIC)
+            assert torch.equal(part, out[lo:hi]), (world, r)
+            del part
 
 
 def _big_window_batch():
