@@ -88,8 +88,13 @@ int kvh_meow128_var_seeded(const void *keys, const uint64_t *offsets,
  * chunked H2D -> kernel -> D2H on the current device, one stream per
  * direction so both PCIe directions run at once.  Synchronous.  This is the
  * PCIe-inclusive path (keys arrive from a socket / shm segment, hashes feed
- * the cuckoo probe).  Pinned buffers from kvh_host_alloc are DMA'd directly;
- * pageable ones go through pinned bounce buffers (about half the rate).
+ * the cuckoo probe).  Pinned buffers from kvh_host_alloc (or a range
+ * page-locked by kvh_host_register whose first and last byte are) are
+ * DMA'd directly; pageable ones go through pinned bounce buffers (about
+ * half the rate).  Batches of <= 4096 keys (knob 21) are copied into a
+ * coherent pinned buffer that one kernel reads and writes across PCIe (no
+ * DMA, ~15 us per call).  Below ~16-32K 16-byte keys per call one CPU core
+ * running the reference hash is faster.
  * ------------------------------------------------------------------- */
 int kvh_meow128_fixed_host(const void *keys, uint32_t key_len, size_t n,
                            uint64_t seed1, uint64_t seed2, uint64_t *out,
@@ -317,11 +322,14 @@ size_t kvh_ht_sort_scratch_bytes(size_t n);
  * input index) -> hashes_out / items_out in table order; with KVH_DEDUP
  * the duplicate count is written to *dup_count (device u64, optional).
  * Asynchronous on stream.  Two engines give the same output word for word
- * (kvh_set_tuning knob 20): a bucketed one (tile histograms, a record
- * scatter into ~6K-element buckets, an LDS sort per bucket; the default up
- * to ~147M elements per call) and a radix one (rocPRIM onesweep on a
- * key prefix + gather; beyond that size).  Non-uniform input (many pairs
- * sharing a slot and h1) is bounded at O(R log^2 R) per such group. */
+ * (kvh_set_tuning knob 20): a bucketed one (~6K-element buckets filled by
+ * two tile-stable LDS-staged scatter passes of <= 7 bucket bits each, an
+ * LDS sort per bucket; the default up to ~75-147M elements per call, the
+ * bound scaled by the share of bucket ids the table's slots reach) and a
+ * radix one (rocPRIM onesweep on a key prefix + gather; beyond that size).
+ * Non-uniform input (many pairs sharing a slot and h1) is bounded at
+ * O(R log^2 R) per such group; a bucket of one repeated pair (the
+ * KVH_DEDUP hot key) arrives in order and costs one pass. */
 int kvh_ht_sort(const uint64_t *hashes, const uint64_t *items, size_t n,
                 const kvh_ht_geom_t *geom, uint64_t *hashes_out,
                 uint64_t *items_out, uint64_t *dup_count, uint32_t flags,
@@ -465,8 +473,11 @@ int         kvh_device_synchronize(void);
  *  18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
  *       long queues, two / one spans per lane per step; 0 lane per span),
  *  19 = tokenizer (1 wave-chunked, 0 workgroup-chunked),
- *  20 = ht_sort engine (0 bucketed when the batch fits it, up to ~147M
- *       elements, else radix; 1 radix always).
+ *  20 = ht_sort engine (0 two-pass bucketed when the batch fits it, else
+ *       radix; 1 radix always; 2 one-pass bucketed when the batch fits it),
+ *  21 = host batches of at most this many keys (and 256 KiB of key bytes)
+ *       take the zero-copy tiny path (default 4096; 0 off),
+ *   3 also takes 3 for the 40-64-byte fixed-length kernels.
  * Returns the previous value or KVH_EINVAL.  (Research kernels and ablation
  * builds whose outputs are not hashes exist only in the experiments build,
  * tools/libkvh_exp.so, never in libkvh.so.) */

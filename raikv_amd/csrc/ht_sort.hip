@@ -39,6 +39,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <vector>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -557,8 +558,15 @@ k_bk_long(Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32
     const uint32_t b = ovf[r];
     const uint64_t len = cnt[b];
     Rec* R = recs + start[b];
+    // a bucket already in the full order skips the network: with the
+    // tile-stable two-pass scatter a bucket's records arrive in input order,
+    // so a hot key repeated millions of times (the KVH_DEDUP case) costs one
+    // pass here instead of O(R log^2 R) on one workgroup
+    uint32_t unordered = 0;
+    for (uint64_t t = tid; t + 1 < len; t += kSB) unordered |= bk_less(g, sb, R[t + 1], R[t]) ? 1u : 0u;
     uint64_t P = 1;
     while (P < len) P <<= 1;
+    if (!block_sum(unordered, wsum)) P = 1;  // (the loop below then does nothing)
     for (uint64_t k = 2; k <= P; k <<= 1) {
       for (uint64_t jj = k >> 1; jj > 0; jj >>= 1) {
         for (uint64_t t = tid; t < P / 2; t += kSB) {
@@ -593,10 +601,329 @@ k_bk_long(Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32
   }
 }
 
+
+// ---------------------------------------------------------------------
+// Two-pass bucketed path (round 3): the B bucket bits of B2 (k_bk_scatter's
+// one pass into 2^B <= 16K bucket streams) split into a pass over the top
+// B1 = ceil(B / 2) bits and one over the low B2 = B - B1 bits, each <= 7
+// bits (<= 128 streams), each a TILE-STABLE, LDS-staged scatter: a tile of
+// kTwTile elements is ranked by digit in input order (wave ballots "match
+// any" on the 7 digit bits + per (round, wave, digit) counts), staged in LDS
+// in digit order and written out from there, so a store instruction's lanes
+// write one digit's consecutive records (16 per digit per tile on average)
+// instead of 64 different bucket streams (tools/scatter_probe.hip prices the
+// 16K-stream scatter at 2.4-4.5x a copy).  Tiles keep input order, so every
+// bucket's records arrive in input order: k_bk_sort's order is unchanged
+// (its comparator ends in the input index) and a bucket of one repeated key
+// is already ordered for k_bk_long.
+//   T0. k_tw_hist1     per tile, the counts of the top-B1 digit
+//   T1. k_bk_colsum / k_tw_scan1 / k_bk_scan / k_bk_tileoff (as B1 above,
+//                      over 2^B1 columns; the chunk scan one parallel
+//                      workgroup) -> each tile's first position per digit
+//   T2. k_tw_scatter1  records (h1, h2, item, index) -> recA by top digit,
+//                      with their full bucket id (u16) -> bA
+//   T3. k_tw_tiles     pass-2 tiles: each top-digit region cut into kTwTile runs
+//   T4. k_tw_hist2     per pass-2 tile, the counts of the low digit
+//   T5. k_tw_scan2 / k_tw_start2   per bucket: running offsets over its
+//                      region's tiles, the bucket sizes and starts
+//   T6. k_tw_scatter2  recA -> rec by low digit (stable)
+//   then B3 k_bk_sort / B4 k_bk_long as the one-pass path.
+constexpr uint32_t kTwTile = 2048;             // elements per tile
+constexpr int kTwT = 512;                      // threads per workgroup
+constexpr int kTwW = kTwT / 64;                // waves
+constexpr int kTwPer = (int)(kTwTile / kTwT);  // elements per thread
+constexpr int kTwD = 128;                      // digit values (<= 7 bits)
+
+struct TwShared {
+  Rec stage[kTwTile];                  // the tile in digit order
+  uint16_t cnt[kTwPer][kTwW][kTwD];    // per (round, wave, digit) counts -> offsets in the digit
+  uint16_t bkt[kTwTile];               // the full bucket id of each staged record
+  uint8_t dig[kTwTile];                // its digit
+  uint32_t lstart[kTwD], gofs[kTwD], wtot[2];
+};
+
+// Stable rank of the tile's elements by digit (element k*kTwT + tid holds
+// dg[k], valid v[k]): pos[k] = its position in the digit-sorted tile;
+// S.lstart[d] = digit d's first position.  Ends with a barrier.
+__device__ __forceinline__ void tw_rank(const uint32_t (&dg)[kTwPer], const bool (&v)[kTwPer], TwShared& S,
+                                        uint32_t (&pos)[kTwPer]) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint16_t* c = &S.cnt[0][0][0];
+  for (uint32_t i = tid; i < (uint32_t)(kTwPer * kTwW * kTwD); i += kTwT) c[i] = 0;
+  __syncthreads();
+  uint32_t below[kTwPer];
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++) {
+    uint64_t eq = __ballot(v[k]);
+#pragma unroll
+    for (int bit = 0; bit < 7; bit++) {
+      const uint64_t B = __ballot((dg[k] >> bit) & 1u);
+      eq &= ((dg[k] >> bit) & 1u) ? B : ~B;
+    }
+    below[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(eq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)eq, 0u));
+    if (v[k] && below[k] == 0) S.cnt[k][w][dg[k]] = (uint16_t)__popcll(eq);
+  }
+  __syncthreads();
+  if (tid < (uint32_t)kTwD) {  // per digit: running offsets over (round, wave), then the digit starts
+    uint32_t run = 0;
+#pragma unroll
+    for (int k = 0; k < kTwPer; k++)
+#pragma unroll
+      for (int q = 0; q < kTwW; q++) {
+        const uint32_t x = S.cnt[k][q][tid];
+        S.cnt[k][q][tid] = (uint16_t)run;
+        run += x;
+      }
+    uint32_t inc = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (lane >= (uint32_t)d) inc += y;
+    }
+    if (lane == 63) S.wtot[w] = inc;
+    S.lstart[tid] = inc - run;  // within this wave's 64 digits
+  }
+  __syncthreads();
+  if (tid >= 64 && tid < (uint32_t)kTwD) S.lstart[tid] += S.wtot[0];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++)
+    pos[k] = v[k] ? S.lstart[dg[k]] + S.cnt[k][w][dg[k]] + below[k] : 0u;
+}
+
+__global__ void __launch_bounds__(kTwT)
+k_tw_hist1(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sb, uint32_t B, uint32_t B2,
+           uint32_t* __restrict__ H, uint32_t* __restrict__ novf) {
+  __shared__ uint32_t hist[kTwD];
+  const uint32_t tid = threadIdx.x, tile = blockIdx.x, nb1 = 1u << (B - B2);
+  if (tile == 0 && tid == 0) *novf = 0;  // B4's overflow list, empty per call
+  if (tid < (uint32_t)kTwD) hist[tid] = 0;
+  __syncthreads();
+  const uint64_t i0 = (uint64_t)tile * kTwTile;
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++) {
+    const uint64_t i = i0 + (uint64_t)k * kTwT + tid;
+    if (i < n) atomicAdd(&hist[bk_of(sort_key64(g, sb, h[2 * i]), B) >> B2], 1u);
+  }
+  __syncthreads();
+  if (tid < nb1) H[(uint64_t)tile * nb1 + tid] = hist[tid];
+}
+
+__global__ void __launch_bounds__(kTwT)
+k_tw_scatter1(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, HtGeom g, uint32_t sb,
+              uint32_t B, uint32_t B2, const uint32_t* __restrict__ H, Rec* __restrict__ recA,
+              uint16_t* __restrict__ bA) {
+  __shared__ TwShared S;
+  const uint32_t tid = threadIdx.x, tile = blockIdx.x, nb1 = 1u << (B - B2);
+  const uint64_t i0 = (uint64_t)tile * kTwTile;
+  Rec r[kTwPer];
+  uint32_t dg[kTwPer], bk[kTwPer], pos[kTwPer];
+  bool v[kTwPer];
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++) {
+    const uint64_t i = i0 + (uint64_t)k * kTwT + tid;
+    v[k] = i < n;
+    if (v[k]) {
+      r[k].h1 = h[2 * i];
+      r[k].h2 = h[2 * i + 1];
+      r[k].item = items ? items[i] : i;
+      r[k].pad = i;
+      bk[k] = bk_of(sort_key64(g, sb, r[k].h1), B);
+    } else {
+      bk[k] = 0;
+    }
+    dg[k] = bk[k] >> B2;
+  }
+  if (tid < nb1) S.gofs[tid] = H[(uint64_t)tile * nb1 + tid];
+  tw_rank(dg, v, S, pos);
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++)
+    if (v[k]) {
+      S.stage[pos[k]] = r[k];
+      S.dig[pos[k]] = (uint8_t)dg[k];
+      S.bkt[pos[k]] = (uint16_t)bk[k];
+    }
+  __syncthreads();
+  const uint32_t total = (uint32_t)min<uint64_t>(kTwTile, n - i0);
+  for (uint32_t p = tid; p < total; p += kTwT) {
+    const uint32_t d = S.dig[p];
+    const uint64_t q = (uint64_t)S.gofs[d] + (p - S.lstart[d]);
+    recA[q] = S.stage[p];
+    bA[q] = S.bkt[p];
+  }
+}
+
+// pass-2 tiles: top digit d's records [start1[d], start1[d] + cnt1[d]) cut
+// into kTwTile runs; tbs[d] = the first tile of digit d, tbs[nb1] = all tiles
+__global__ void __launch_bounds__(kTwD)
+k_tw_tiles(const uint32_t* __restrict__ cnt1, uint32_t nb1, uint32_t* __restrict__ tbs) {
+  __shared__ uint32_t w0;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t t = tid < nb1 ? (cnt1[tid] + kTwTile - 1) / kTwTile : 0u;
+  uint32_t inc = t;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  if (tid == 63) w0 = inc;
+  __syncthreads();
+  if (tid >= 64) inc += w0;
+  if (tid < nb1) tbs[tid + 1] = inc;
+  if (tid == 0) tbs[0] = 0;
+}
+
+// pass-2 tile j -> its top digit and record range [*p0, *p1); false past the last tile
+__device__ __forceinline__ bool tw_tile2(uint32_t j, const uint32_t* __restrict__ tbs, uint32_t nb1,
+                                         const uint32_t* __restrict__ cnt1, const uint32_t* __restrict__ start1,
+                                         uint32_t* d1, uint32_t* p0, uint32_t* p1) {
+  if (j >= tbs[nb1]) return false;
+  uint32_t lo = 0, hi = nb1;  // the last d with tbs[d] <= j
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (tbs[mid] <= j) lo = mid; else hi = mid;
+  }
+  *d1 = lo;
+  *p0 = start1[lo] + (j - tbs[lo]) * kTwTile;
+  *p1 = min(*p0 + kTwTile, start1[lo] + cnt1[lo]);
+  return true;
+}
+
+__global__ void __launch_bounds__(kTwT)
+k_tw_hist2(const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs, const uint32_t* __restrict__ cnt1,
+           const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2, uint32_t* __restrict__ H2) {
+  __shared__ uint32_t hist[kTwD];
+  const uint32_t tid = threadIdx.x, nb2 = 1u << B2;
+  uint32_t d1, p0, p1;
+  if (!tw_tile2(blockIdx.x, tbs, nb1, cnt1, start1, &d1, &p0, &p1)) return;  // workgroup-uniform
+  if (tid < (uint32_t)kTwD) hist[tid] = 0;
+  __syncthreads();
+  for (uint32_t p = p0 + tid; p < p1; p += kTwT) atomicAdd(&hist[bA[p] & (nb2 - 1)], 1u);
+  __syncthreads();
+  if (tid < nb2) H2[(uint64_t)blockIdx.x * nb2 + tid] = hist[tid];
+}
+
+// Exclusive scan, in place, of the columns c < ncols (<= 128) of rows
+// [r0, r1) of a row-major table with `ncols` words per row, by one
+// 1024-thread workgroup: 8 groups of 128 threads, group g scans a
+// contiguous eighth of the rows (the 128 threads of a group read one row's
+// words together: coalesced), group sums combined in LDS.  *total[c] gets
+// the column sum when total != nullptr.
+__device__ __forceinline__ void tw_colscan(uint32_t* __restrict__ Tb, uint32_t r0, uint32_t r1, uint32_t ncols,
+                                           uint32_t* __restrict__ total, uint32_t (&part)[8][kTwD]) {
+  const uint32_t c = threadIdx.x & (kTwD - 1), grp = threadIdx.x >> 7;
+  const uint32_t rows = r1 - r0, per = (rows + 7) / 8;
+  const uint32_t a = r0 + min(rows, grp * per), b = r0 + min(rows, (grp + 1) * per);
+  uint32_t sum = 0;
+  if (c < ncols) {
+    uint32_t r = a;
+    for (; r + 8 <= b; r += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) v[q] = Tb[(uint64_t)(r + q) * ncols + c];
+#pragma unroll
+      for (int q = 0; q < 8; q++) sum += v[q];
+    }
+    for (; r < b; r++) sum += Tb[(uint64_t)r * ncols + c];
+  }
+  part[grp][c] = sum;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t g = 0; g < grp; g++) run += part[g][c];
+  if (c < ncols) {
+    if (grp == 0 && total) {
+      uint32_t t = 0;
+      for (uint32_t g = 0; g < 8; g++) t += part[g][c];
+      total[c] = t;
+    }
+    uint32_t r = a;
+    for (; r + 8 <= b; r += 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) v[q] = Tb[(uint64_t)(r + q) * ncols + c];
+#pragma unroll
+      for (int q = 0; q < 8; q++) { Tb[(uint64_t)(r + q) * ncols + c] = run; run += v[q]; }
+    }
+    for (; r < b; r++) {
+      const uint32_t v = Tb[(uint64_t)r * ncols + c];
+      Tb[(uint64_t)r * ncols + c] = run;
+      run += v;
+    }
+  }
+}
+
+// pass 1: the chunk sums S[nch][nb1] -> exclusive prefix per column, cnt1 = the column sums
+__global__ void __launch_bounds__(1024)
+k_tw_scan1(uint32_t* __restrict__ S, uint32_t nch, uint32_t nb1, uint32_t* __restrict__ cnt1) {
+  __shared__ uint32_t part[8][kTwD];
+  tw_colscan(S, 0, nch, nb1, cnt1, part);
+}
+
+// pass 2, one workgroup per top digit d1: H2 over d1's tiles -> running
+// offsets within each bucket (d1, d2); cnt[(d1, d2)] = the bucket's size
+__global__ void __launch_bounds__(1024)
+k_tw_scan2(uint32_t* __restrict__ H2, const uint32_t* __restrict__ tbs, uint32_t B2, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t part[8][kTwD];
+  const uint32_t d1 = blockIdx.x;
+  tw_colscan(H2, tbs[d1], tbs[d1 + 1], 1u << B2, cnt + (d1 << B2), part);
+}
+
+// start[b] = start1[d1] + the sizes of d1's earlier buckets
+__global__ void __launch_bounds__(kTwD)
+k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
+            uint32_t* __restrict__ start) {
+  const uint32_t d1 = threadIdx.x, nb2 = 1u << B2;
+  if (d1 >= nb1) return;
+  uint32_t run = start1[d1];
+  for (uint32_t d2 = 0; d2 < nb2; d2++) {
+    start[(d1 << B2) | d2] = run;
+    run += cnt[(d1 << B2) | d2];
+  }
+}
+
+__global__ void __launch_bounds__(kTwT)
+k_tw_scatter2(const Rec* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
+              const uint32_t* __restrict__ cnt1, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
+              const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, Rec* __restrict__ rec) {
+  __shared__ TwShared S;
+  const uint32_t tid = threadIdx.x, nb2 = 1u << B2, j = blockIdx.x;
+  uint32_t d1, p0, p1;
+  if (!tw_tile2(j, tbs, nb1, cnt1, start1, &d1, &p0, &p1)) return;  // workgroup-uniform
+  Rec r[kTwPer];
+  uint32_t dg[kTwPer], pos[kTwPer];
+  bool v[kTwPer];
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++) {
+    const uint32_t p = p0 + (uint32_t)k * kTwT + tid;
+    v[k] = p < p1;
+    dg[k] = 0;
+    if (v[k]) {
+      r[k] = recA[p];
+      dg[k] = bA[p] & (nb2 - 1);
+    }
+  }
+  if (tid < nb2) S.gofs[tid] = start[(d1 << B2) | tid] + H2[(uint64_t)j * nb2 + tid];
+  tw_rank(dg, v, S, pos);
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++)
+    if (v[k]) {
+      S.stage[pos[k]] = r[k];
+      S.dig[pos[k]] = (uint8_t)dg[k];
+    }
+  __syncthreads();
+  for (uint32_t p = tid; p < p1 - p0; p += kTwT) {
+    const uint32_t d = S.dig[p];
+    rec[(uint64_t)S.gofs[d] + (p - S.lstart[d])] = S.stage[p];
+  }
+}
+
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct SortLayout {
-  size_t key_in, key_out, idx_in, idx_out, rec, runs, tmp, tmp_bytes, total;
+  size_t key_in, key_out, idx_in, idx_out, rec, runs, tmp, tmp_bytes;
+  // the two-pass bucketed path (its own offsets from 0)
+  size_t tw_recA, tw_rec, tw_bA, tw_H1, tw_S1, tw_small, tw_H2, tw_bk;
+  size_t total;
 };
 
 int sort_layout(size_t n, SortLayout* L) {
@@ -618,7 +945,18 @@ int sort_layout(size_t n, SortLayout* L) {
   L->runs = o; o += al256(4 * (n / (kShortRun + 1) + 2));  // count, then run starts
   L->tmp = o; o += al256(tmp);
   L->tmp_bytes = tmp;
-  L->total = o;
+  const size_t radix_total = o;
+  const size_t ntiles = (n + kTwTile - 1) / kTwTile, nch = (ntiles + kBkChunk - 1) / kBkChunk;
+  o = 0;
+  L->tw_recA = o; o += al256(sizeof(Rec) * n);
+  L->tw_rec = o; o += al256(sizeof(Rec) * n);
+  L->tw_bA = o; o += al256(2 * n);
+  L->tw_H1 = o; o += al256(4 * ntiles * kTwD);
+  L->tw_S1 = o; o += al256(4 * nch * kTwD);
+  L->tw_small = o; o += al256(4 * (3 * kTwD + 2));  // cnt1, start1, tbs
+  L->tw_H2 = o; o += al256(4 * (ntiles + kTwD) * kTwD);
+  L->tw_bk = o; o += al256(4 * (3 * (1u << kBkMaxB) + 1));  // cnt, start, ovf, novf
+  L->total = std::max(radix_total, o);
   return 0;
 }
 
@@ -668,13 +1006,76 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   const int tsb = g_tune_sort_bits.load(std::memory_order_relaxed);
   int cus = 0;
   if ((rc = device_cus(&cus))) return rc;
-  if (!tsb && g_tune_sort_engine.load(std::memory_order_relaxed) == 0) {
-    // the bucketed path: ~6K elements per bucket, B <= 14 bucket bits, so up
-    // to ~147M elements per call (a mean bucket of <= 9000 under the 12288
+  const int engine = g_tune_sort_engine.load(std::memory_order_relaxed);
+  if (!tsb && engine != 1) {
+    // the bucketed paths: ~6K elements per bucket over the buckets the
+    // table's slots reach (slot < ht_size: a share ht_size / 2^sb of the 2^B
+    // top-bit buckets, 1/2 to 1), B <= 14 bucket bits, so up to
+    // ~75-147M elements per call (a mean bucket of <= 9000 under the 12288
     // LDS capacity); larger batches take the radix path below
+    const double reach = (double)geom->ht_size / std::ldexp(1.0, (int)std::min<uint32_t>(sb, 64));
+    auto mean_of = [&](uint32_t B) { return (double)n / (reach * std::ldexp(1.0, (int)B)); };
     uint32_t B = 0;
-    while (B < (uint32_t)kBkMaxB && ((uint64_t)n >> B) > 6144) B++;
-    if (((uint64_t)n >> B) <= 9000) {
+    while (B < (uint32_t)kBkMaxB && mean_of(B) > 6144.0) B++;
+    if (mean_of(B) <= 9000.0 && engine != 2 && B >= 2) {
+      // two passes of <= 7 bits, tile-stable LDS-staged scatters
+      const uint32_t B2 = B / 2, B1 = B - B2, nb1 = 1u << B1, nb = 1u << B;
+      const uint32_t ntiles = (uint32_t)((n + kTwTile - 1) / kTwTile);
+      const uint32_t nch = (ntiles + kBkChunk - 1) / kBkChunk;
+      Rec* recA = (Rec*)(s + L.tw_recA);
+      Rec* recB = (Rec*)(s + L.tw_rec);
+      uint16_t* bA = (uint16_t*)(s + L.tw_bA);
+      uint32_t* H1 = (uint32_t*)(s + L.tw_H1);
+      uint32_t* S1 = (uint32_t*)(s + L.tw_S1);
+      uint32_t* cnt1 = (uint32_t*)(s + L.tw_small);
+      uint32_t* start1 = cnt1 + kTwD;
+      uint32_t* tbs = start1 + kTwD;
+      uint32_t* H2 = (uint32_t*)(s + L.tw_H2);
+      uint32_t* cnt = (uint32_t*)(s + L.tw_bk);
+      uint32_t* start = cnt + nb;
+      uint32_t* ovf = start + nb;
+      uint32_t* novf = ovf + nb;
+      const uint32_t cgrid = (uint32_t)(((uint64_t)nch * nb1 + 255) / 256);
+      hipLaunchKernelGGL(k_tw_hist1, dim3(ntiles), dim3(kTwT), 0, st, hashes, (uint64_t)n, g, sb, B, B2, H1, novf);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_colsum, dim3(cgrid), dim3(256), 0, st, (const uint32_t*)H1, ntiles, nb1, S1);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_tw_scan1, dim3(1), dim3(1024), 0, st, S1, nch, nb1, cnt1);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_scan, dim3(1), dim3(kBkT), 0, st, (const uint32_t*)cnt1, nb1, start1);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_tileoff, dim3(cgrid), dim3(256), 0, st, H1, (const uint32_t*)S1,
+                         (const uint32_t*)start1, ntiles, nb1);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_tw_scatter1, dim3(ntiles), dim3(kTwT), 0, st, hashes, items, (uint64_t)n, g, sb, B, B2,
+                         (const uint32_t*)H1, recA, bA);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_tw_tiles, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt1, nb1, tbs);
+      if ((rc = launch_done())) return rc;
+      const uint32_t ntB = ntiles + nb1;  // an upper bound: the tiles past tbs[nb1] return at once
+      hipLaunchKernelGGL(k_tw_hist2, dim3(ntB), dim3(kTwT), 0, st, (const uint16_t*)bA, (const uint32_t*)tbs,
+                         (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2, H2);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_tw_scan2, dim3(nb1), dim3(1024), 0, st, H2, (const uint32_t*)tbs, B2, cnt);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_tw_start2, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
+                         nb1, B2, start);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_tw_scatter2, dim3(ntB), dim3(kTwT), 0, st, (const Rec*)recA, (const uint16_t*)bA,
+                         (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
+                         (const uint32_t*)H2, (const uint32_t*)start, recB);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_sort, dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
+                         (const Rec*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
+                         items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_long, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st, recB,
+                         (const uint32_t*)cnt, (const uint32_t*)start, g, sb, h_out, items_out, dedup ? 1u : 0u,
+                         (unsigned long long*)dup_count, (const uint32_t*)novf, (const uint32_t*)ovf);
+      return launch_done();
+    }
+    if (mean_of(B) <= 9000.0) {
+      // one pass: LDS-atomic-ranked scatter into 2^B bucket streams (knob 20 = 2; small B)
       const uint32_t nb = 1u << B;
       const uint32_t ntiles = (uint32_t)((n + kBkTile - 1) / kBkTile);
       const uint32_t nch = (ntiles + kBkChunk - 1) / kBkChunk;

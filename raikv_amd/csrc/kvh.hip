@@ -25,6 +25,9 @@
 #include <atomic>
 #include <mutex>
 #include <thread>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <vector>
 #include <algorithm>
 #include "meow_dev.hpp"
@@ -84,6 +87,66 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
       const uint64_t j = b + 64 * u + lane;
       store_h<true>(out, j < last ? j : last, h[u], fix);
     }
+  }
+}
+
+// k_fixed software-pipelined across chunks: while chunk c+1's key loads are
+// in flight, chunk c's TAIL (three serial rounds, meow_tail) runs; then
+// chunk c+1's HEAD (the absorb/Mix/Compress rounds whose chains run side by
+// side, meow_head) -- so the serial end of one chunk overlaps the loads and
+// the parallel start of the next instead of exposing its LDS latency.
+// Same chunking, clamping and stores as k_fixed.
+template <int L, int NT, bool A16, int U>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_pl(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
+           uint64_t* __restrict__ out, uint32_t flags) {
+  constexpr int NC = Plan<L>::NC;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  const uint64_t last = n - 1;
+  uint64_t pb = wave * 64 * U;
+  if (pb >= n) return;  // wave-uniform
+  Blk X[U], Y[U];
+  {
+    Blk D[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = pb + 64 * u + lane;
+      load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) meow_head<L>(D[u], K, T, X[u], Y[u]);
+  }
+  for (uint64_t b = pb + step; b < n; b += step) {  // wave-uniform trip count
+    Blk D[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
+    }
+    Blk h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = meow_tail<L>(X[u], Y[u], K, T);
+#pragma unroll
+    for (int u = 0; u < U; u++) meow_head<L>(D[u], K, T, X[u], Y[u]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = pb + 64 * u + lane;
+      store_h<true>(out, j < last ? j : last, h[u], fix);
+    }
+    pb = b;
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t j = pb + 64 * u + lane;
+    store_h<true>(out, j < last ? j : last, meow_tail<L>(X[u], Y[u], K, T), fix);
   }
 }
 
@@ -552,6 +615,29 @@ k_seeded(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, ui
   store_h(out, i, h, (flags & KVH_FIXUP) != 0);
 }
 
+// Tiny host batches (raikv's 8-key prefetch pipes, ev_net.h:442; a ctest
+// batch of a few thousand frags, ctest.c:34): keys, offsets and hashes stay
+// in coherent pinned host memory and the kernel reads and writes them
+// across PCIe itself -- one launch and one synchronize, no DMA copies, no
+// LDS table fill (constant-memory tables, the literal restatement).  Key i
+// is keys[offs[i] - offs[0] ..) (variable length) or keys[i * key_len ..).
+__global__ void __launch_bounds__(256)
+k_tiny(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t key_len, uint64_t n, uint64_t s1,
+       uint64_t s2, uint64_t* __restrict__ out, uint32_t flags) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const ConstTab T;
+  uint64_t a, L;
+  if (offs) {
+    a = offs[i] - offs[0];
+    L = offs[i + 1] - offs[i];
+  } else {
+    a = i * key_len;
+    L = key_len;
+  }
+  store_h(out, i, meow_literal(keys + a, L, s1, s2, T), (flags & KVH_FIXUP) != 0);
+}
+
 // streaming: state[16 words] in/out; absorb nblk full 64-byte blocks
 __global__ void k_stream_absorb(uint32_t* st, const uint8_t* data, uint64_t nblk) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -631,6 +717,7 @@ Knob g_tune_wgmul{1};     // workgroups per CU multiplier
 Knob g_tune_generic{0};   // force the generic kernel
 Knob g_tune_kpl{0};       // keys per lane per chunk in k_fixed (1, 2, 4 or 8; 0 = per-length default)
 Knob g_tune_ms_lanes{1};  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
+Knob g_tune_pl{0};        // fixed-length kernel: 1 = software-pipelined across chunks (k_fixed_pl)
 Knob g_tune_var{23};      // var-length kernel: 23 = k_var9 (16 waves; 24 = 12 waves, 25 = 12 waves + block prefetch); 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic
 inline int knob(const Knob& k) { return k.load(std::memory_order_relaxed); }
 
@@ -647,6 +734,13 @@ int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t
              hipStream_t st, int cus) {
   const bool a16 = ((uintptr_t)keys & 15) == 0;
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
+  if (knob(g_tune_pl)) {
+    if (a16)
+      hipLaunchKernelGGL((k_fixed_pl<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+    else
+      hipLaunchKernelGGL((k_fixed_pl<L, NT, false, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+    return launch_done();
+  }
   if (a16)
     hipLaunchKernelGGL((k_fixed<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
   else
@@ -821,8 +915,11 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
       case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
       case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
       case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
-      default: return set_err(KVH_EINVAL);
+      case 403: if constexpr (L >= 40) return launch_k<L, 4, 3>(keys, n, s1, s2, out, flags, st, cus); break;
+      case 203: if constexpr (L >= 40) return launch_k<L, 2, 3>(keys, n, s1, s2, out, flags, st, cus); break;
+      default: break;
     }
+    return set_err(KVH_EINVAL);
   }
 }
 
@@ -997,6 +1094,8 @@ constexpr int kMaxDev = 64;
 constexpr int kPipesPerDev = 4;
 Knob g_tune_pipe_mib{16};   // key bytes per pipeline chunk, MiB (knob 15)
 Knob g_tune_pipe_slots{4};  // chunks in flight (knob 16)
+Knob g_tune_tiny{4096};     // host batches of at most this many keys take the zero-copy tiny path (knob 21; 0 = off)
+constexpr size_t kTinyBytes = 256 << 10;  // ... and at most this many key bytes
 struct HostPipe {
   std::mutex mu;
   hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
@@ -1004,6 +1103,8 @@ struct HostPipe {
   uint8_t* dk[kPipeSlots] = {};      // key bytes (device)
   uint64_t* doff[kPipeSlots] = {};   // key offsets (device, variable length)
   uint64_t* dout[kPipeSlots] = {};   // hashes (device)
+  uint8_t* tiny = nullptr;           // coherent pinned keys | offsets | hashes of the tiny path
+  size_t tinycap = 0;
   uint8_t* hk[kPipeSlots] = {};      // pinned bounce buffers for pageable callers
   uint64_t* hoff[kPipeSlots] = {};
   uint64_t* ho[kPipeSlots] = {};
@@ -1056,11 +1157,19 @@ std::unique_lock<std::mutex> pick_pipe(int dev, HostPipe** P) {
   return std::unique_lock<std::mutex>(g_pipe[dev][0].mu);
 }
 
-bool is_pinned(const void* p) {
+// [p, p + bytes) is page-locked host memory (kvh_host_alloc, hipHostMalloc,
+// or kvh_host_register of a range holding it): its first AND last byte are
+// (a range registered only in part takes the bounce buffers, never a DMA
+// past the registered extent).
+bool pinned_byte(const void* p) {
   hipPointerAttribute_t a;
   const bool pin = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
   (void)hipGetLastError();
   return pin;
+}
+bool is_pinned(const void* p, size_t bytes) {
+  if (!bytes) return true;
+  return pinned_byte(p) && (bytes == 1 || pinned_byte((const uint8_t*)p + bytes - 1));
 }
 
 // One host batch through H2D -> kernel -> D2H on the current device.
@@ -1083,6 +1192,32 @@ int host_pipeline(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, s
   HostPipe* P = nullptr;
   std::unique_lock<std::mutex> lk = pick_pipe(dev, &P);
   const bool var = offs != nullptr;
+  if (n <= (size_t)knob(g_tune_tiny) && (var ? offs[n] - offs[0] : (uint64_t)n * key_len) <= kTinyBytes) {
+    // tiny batch: copy into the pipeline's coherent pinned buffer, one
+    // kernel reading and writing host memory, one synchronize
+    const size_t kb = var ? (size_t)(offs[n] - offs[0]) : n * (size_t)key_len;
+    const size_t o_off = al16(kb), o_out = o_off + al16(var ? 8 * (n + 1) : 0), need = o_out + 16 * n;
+    if (P->tinycap < need) {
+      if (P->tiny) (void)hipHostFree(P->tiny);
+      P->tiny = nullptr;
+      P->tinycap = 0;
+      const size_t cap = std::max<size_t>(need, kTinyBytes + 16 * 4096 + 8 * 4097 + 64);
+      if ((e = hipHostMalloc((void**)&P->tiny, cap, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
+        return hip_err(e);
+      P->tinycap = cap;
+    }
+    if (!P->s_k && (e = hipStreamCreateWithFlags(&P->s_k, hipStreamNonBlocking)) != hipSuccess) return hip_err(e);
+    if (kb) memcpy(P->tiny, keys + (var ? offs[0] : 0), kb);
+    if (var) memcpy(P->tiny + o_off, offs, 8 * (n + 1));
+    hipLaunchKernelGGL(k_tiny, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, P->s_k, (const uint8_t*)P->tiny,
+                       var ? (const uint64_t*)(P->tiny + o_off) : (const uint64_t*)nullptr, key_len, (uint64_t)n, s1,
+                       s2, (uint64_t*)(P->tiny + o_out), flags);
+    int rc = launch_done();
+    if ((e = hipStreamSynchronize(P->s_k)) != hipSuccess && !rc) rc = hip_err(e);
+    if (rc) return rc;
+    memcpy(out, P->tiny + o_out, 16 * n);
+    return set_err(0);
+  }
   const size_t budget = (size_t)knob(g_tune_pipe_mib) << 20;
   const size_t chunk_keys = var ? std::max<size_t>(1, budget / 8) : std::max<size_t>(1, budget / key_len);
   // chunk boundaries; the largest chunk sizes the buffers
@@ -1101,10 +1236,35 @@ int host_pipeline(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, s
     max_keys = std::max(max_keys, hi - lo);
     bounds.push_back(hi);
   }
-  const bool pin_k = is_pinned(keys), pin_o = is_pinned(out), pin_f = var && is_pinned(offs);
+  const uint64_t kb0 = var ? offs[0] : 0, kb1 = var ? offs[n] : (uint64_t)n * key_len;
+  const bool pin_k = is_pinned(keys + kb0, kb1 - kb0), pin_o = is_pinned(out, 16 * n),
+             pin_f = var && is_pinned(offs, 8 * (n + 1));
   const int slots = std::min(std::max(knob(g_tune_pipe_slots), 2), kPipeSlots);
   int rc = P->reserve(slots, max_bytes, var ? 8 * (max_keys + 1) : 0, 16 * max_keys, !pin_k, var && !pin_f, !pin_o);
   if (rc) return rc;
+  if (bounds.size() == 2) {
+    // one chunk (raikv's batches: 8 keys per prefetch pipe, ev_net.h:442; up
+    // to 16K frags per ctest batch, ctest.c:34): H2D, kernel and D2H in order
+    // on one stream and one synchronize, no cross-stream events
+    const uint8_t* src = keys + kb0;
+    const size_t nbytes = (size_t)(kb1 - kb0);
+    if (!pin_k && nbytes) { memcpy(P->hk[0], src, nbytes); src = P->hk[0]; }
+    const uint64_t* fsrc = offs;
+    if (var && !pin_f) { memcpy(P->hoff[0], offs, 8 * (n + 1)); fsrc = P->hoff[0]; }
+    uint64_t* dst = pin_o ? out : P->ho[0];
+    if ((nbytes && (e = hipMemcpyAsync(P->dk[0], src, nbytes, hipMemcpyHostToDevice, P->s_k)) != hipSuccess) ||
+        (var && (e = hipMemcpyAsync(P->doff[0], fsrc, 8 * (n + 1), hipMemcpyHostToDevice, P->s_k)) != hipSuccess))
+      return hip_err(e);
+    rc = var ? kvh_meow128_var((const uint8_t*)((uintptr_t)P->dk[0] - (uintptr_t)kb0), P->doff[0], n, s1, s2,
+                               P->dout[0], flags, P->s_k)
+             : kvh_meow128_fixed(P->dk[0], key_len, n, s1, s2, P->dout[0], flags, P->s_k);
+    if (!rc && (e = hipMemcpyAsync(dst, P->dout[0], 16 * n, hipMemcpyDeviceToHost, P->s_k)) != hipSuccess)
+      rc = hip_err(e);
+    if ((e = hipStreamSynchronize(P->s_k)) != hipSuccess && !rc) rc = hip_err(e);
+    if (rc) return rc;
+    if (!pin_o) memcpy(out, P->ho[0], 16 * n);
+    return set_err(0);
+  }
   size_t pend_lo[kPipeSlots] = {}, pend_cnt[kPipeSlots] = {};
   auto drain = [&](int s) -> int {  // the slot's previous chunk has left the device
     if (!pend_cnt[s]) return 0;
@@ -1178,6 +1338,52 @@ void shard_bounds(const uint64_t* offs, size_t n, int ns, size_t* b) {
 // its disjoint slice of the caller's output, the same global layout as a
 // one-device call).  Fixed length: equal index ranges; variable length:
 // ranges of equal key BYTES (raikv_amd/workload.py: shard_var).
+// Persistent host workers for the _multi entries: a job queue served by
+// threads created on first use and kept for the process lifetime (grown to
+// the largest device list seen), instead of one new std::thread per device
+// per call.  Jobs are independent (a job never waits for another), so a
+// pool smaller than the jobs in flight only serialises them.
+struct WorkPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  int threads = 0;
+  void run(std::vector<std::function<void()>>& jobs) {
+    std::mutex dmu;
+    std::condition_variable dcv;
+    size_t left = jobs.size();
+    {
+      std::lock_guard<std::mutex> g(mu);
+      while (threads < (int)jobs.size()) {
+        std::thread([this]() { worker(); }).detach();
+        threads++;
+      }
+      for (auto& j : jobs)
+        q.push_back([&dmu, &dcv, &left, &j]() {
+          j();
+          std::lock_guard<std::mutex> g2(dmu);
+          if (--left == 0) dcv.notify_all();
+        });
+    }
+    cv.notify_all();
+    std::unique_lock<std::mutex> lk(dmu);
+    dcv.wait(lk, [&]() { return left == 0; });
+  }
+  void worker() {
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [this]() { return !q.empty(); });
+        job = std::move(q.front());
+        q.pop_front();
+      }
+      job();
+    }
+  }
+};
+WorkPool* g_pool = new WorkPool;  // never destroyed: its detached workers outlive static destructors
+
 int host_multi(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, size_t n, uint64_t s1, uint64_t s2,
                uint64_t* out, uint32_t flags, const int* devices, int ndev) {
   if (ndev < 1 || ndev > kMaxDev || !devices) return set_err(KVH_EINVAL);
@@ -1189,11 +1395,11 @@ int host_multi(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, size
   std::vector<size_t> lo(ndev + 1);
   shard_bounds(offs, n, ndev, lo.data());
   std::vector<int> rcs(ndev, 0);
-  std::vector<std::thread> th;
+  std::vector<std::function<void()>> jobs;
   for (int d = 0; d < ndev; d++) {
-    th.emplace_back([&, d]() {
-      const size_t a = lo[d], b = std::max(lo[d], lo[d + 1]);
-      if (b == a) return;
+    const size_t a = lo[d], b = std::max(lo[d], lo[d + 1]);
+    if (b == a) continue;
+    jobs.emplace_back([&, d, a, b]() {
       const hipError_t se = hipSetDevice(devices[d]);
       if (se != hipSuccess) { rcs[d] = hip_err(se); return; }
       // variable length: shard offsets stay absolute into `keys`;
@@ -1202,7 +1408,14 @@ int host_multi(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, size
                     : host_pipeline(keys + (uint64_t)a * key_len, key_len, nullptr, b - a, s1, s2, out + 2 * a, flags);
     });
   }
-  for (auto& t : th) t.join();
+  if (jobs.size() == 1) {  // one shard: on the calling thread, whose current device is restored
+    int cur = 0;
+    if ((e = hipGetDevice(&cur)) != hipSuccess) return hip_err(e);
+    jobs[0]();
+    (void)hipSetDevice(cur);
+  } else if (!jobs.empty()) {
+    g_pool->run(jobs);
+  }
   for (int d = 0; d < ndev; d++)
     if (rcs[d]) return set_err(rcs[d]);
   return set_err(0);
@@ -1627,7 +1840,7 @@ int kvh_set_tuning(int k, int value) {
     case 0: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL; return set(g_tune_nt, value);
     case 1: if (value < 1 || value > 8) return KVH_EINVAL; return set(g_tune_wgmul, value);
     case 2: return set(g_tune_generic, value ? 1 : 0);
-    case 3: if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8) return KVH_EINVAL;
+    case 3: if (value < 0 || value > 8 || value == 5 || value == 6 || value == 7) return KVH_EINVAL;
             return set(g_tune_kpl, value);
     case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) &&
                 !(g_exp.var_knob && g_exp.var_knob(value)))
@@ -1640,7 +1853,9 @@ int kvh_set_tuning(int k, int value) {
     case 17: if (value < 0 || value > 64) return KVH_EINVAL; return set(g_tune_sort_bits, value);
     case 18: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_spans, value);
     case 19: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_tok, value);
-    case 20: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_engine, value);
+    case 20: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_engine, value);
+    case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
+    case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_pl, value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }

@@ -200,7 +200,8 @@ int launch_done();
 extern std::atomic<int> g_tune_crc_var;
 // table-order sort: h1 bits sorted below the slot bits (0 = by batch size; 64 = the full key)
 extern std::atomic<int> g_tune_sort_bits;
-// table-order sort engine: 0 = bucketed when the batch fits it (else radix), 1 = radix (rocPRIM) always
+// table-order sort engine: 0 = two-pass bucketed when the batch fits it (else radix), 1 = radix (rocPRIM)
+// always, 2 = one-pass bucketed when the batch fits it
 extern std::atomic<int> g_tune_sort_engine;
 // span hashing: 2 / 1 = wave-chunked kernel with the short-key path, two / one spans per lane
 // (default 2), 0 = lane per span

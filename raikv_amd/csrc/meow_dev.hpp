@@ -251,6 +251,65 @@ __device__ __forceinline__ Blk meow_ct(const Blk* D, const MeowConst& K, const T
   return aesdec(S0b, K.M, T);
 }
 
+// meow_ct split at the last serial stretch, for software pipelining across
+// chunks (k_fixed_pl): HEAD = absorb, Mix and the first Compress rounds,
+// whose chains run side by side (4, then 4, then 2 independent rounds for a
+// 64-byte key); TAIL = S2b = AESDEC(X, M), S0b = AESDEC(Y, S2b), AESDEC(S0b,
+// M): three rounds in series.  X = AESDEC(S2, S3) (T2) or TG2 ^ S3 (T3);
+// Y = AESDEC(S0, S1) (T0).  meow_tail(meow_head(D)) == meow_ct(D).
+template <int L, class Tab>
+__device__ __forceinline__ void meow_head(const Blk* D, const MeowConst& K, const Tab& T, Blk& X, Blk& Y) {
+  using P = Plan<L>;
+  Blk S0, S1, S2, S3;
+#pragma unroll
+  for (int b = 0; b < P::NB; b++) {
+    const Blk& k0 = D[4 * b + 0]; const Blk& k1 = D[4 * b + 1];
+    const Blk& k2 = D[4 * b + 2]; const Blk& k3 = D[4 * b + 3];
+    if (b == 0) {
+      S0 = aesdec(bxor(K.F[0], k0), k0, T); S1 = aesdec(bxor(K.F[1], k1), k1, T);
+      S2 = aesdec(bxor(K.F[2], k2), k2, T); S3 = aesdec(bxor(K.F[3], k3), k3, T);
+    } else {
+      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
+      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+    }
+  }
+  constexpr bool first = P::NB == 0;
+  constexpr int base = 4 * P::NB;
+  if constexpr (P::T != 0) {
+    const Blk& k = D[base + P::C / 16];
+    S3 = first ? aesdec(bxor(K.F[3], k), k, T) : aesdec(aesdec(S3, k, T), k, T);
+  }
+  if constexpr (P::C >= 48) {
+    const Blk& k = D[base + 2];
+    S2 = first ? aesdec(bxor(K.F[2], k), k, T) : aesdec(aesdec(S2, k, T), k, T);
+  }
+  if constexpr (P::C >= 32) {
+    const Blk& k = D[base + 1];
+    S1 = first ? aesdec(bxor(K.F[1], k), k, T) : aesdec(aesdec(S1, k, T), k, T);
+  }
+  if constexpr (P::C >= 16) {
+    const Blk& k = D[base + 0];
+    S0 = first ? aesdec(bxor(K.F[0], k), k, T) : aesdec(aesdec(S0, k, T), k, T);
+  }
+  if constexpr (P::T3) S3 = aesdec(S3, K.M, T); else S3 = K.G[3];
+  if constexpr (P::T2) S2 = aesdec(S2, K.M, T); else S2 = K.G[2];
+  if constexpr (P::T1) S1 = aesdec(S1, K.M, T); else S1 = K.G[1];
+  if constexpr (P::T0) S0 = aesdec(S0, K.M, T); else S0 = K.G[0];
+  if constexpr (P::T2) X = aesdec(S2, S3, T);
+  else if constexpr (P::T3) X = bxor(K.TG2, S3);
+  else X = bzero();
+  if constexpr (P::T0) Y = aesdec(S0, S1, T); else Y = bzero();
+}
+template <int L, class Tab>
+__device__ __forceinline__ Blk meow_tail(const Blk& X, const Blk& Y, const MeowConst& K, const Tab& T) {
+  using P = Plan<L>;
+  Blk S2b;
+  if constexpr (P::T2 || P::T3) S2b = aesdec(X, K.M, T); else S2b = K.CS2b;
+  Blk S0b;
+  if constexpr (P::T0) S0b = aesdec(Y, S2b, T); else S0b = bxor(K.TCS0a, S2b);
+  return aesdec(S0b, K.M, T);
+}
+
 // ---------------------------------------------------- runtime lengths
 // bytes [p, p+n), 0 <= n <= 16, zero padded; reads only the dwords that
 // intersect [p, p+n), so it never touches memory past the key's last byte's

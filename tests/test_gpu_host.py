@@ -133,3 +133,75 @@ def test_multi_device_rejects_bad_device_lists(kvh):
     assert kvh.lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, 16, 100, 0, 0, out.ctypes.data, 0, bad, 0) == -22
     neg = (C.c_int * 1)(-1)
     assert kvh.lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, 16, 100, 0, 0, out.ctypes.data, 0, neg, 1) == -22
+
+
+def test_partially_registered_buffers_take_the_bounce_path(kvh):
+    """a buffer page-locked only in part (its first pages
+    registered, the rest pageable) must not be DMA'd past the registered
+    extent; the pipeline checks the range's first and last byte and bounces
+    it otherwise.  Keys, offsets and output each registered at the front only,
+    one chunk and several chunks."""
+    n = 300_001
+    keys, offs = zipf_batch(n, 21, lead=1)
+    want = dev_hash_var(kvh, keys, offs, STATIC)
+    page = 4096
+    bufs = {}
+    for name, arr in (("keys", keys), ("offs", offs)):
+        raw = np.empty(arr.nbytes + 2 * page, dtype=np.uint8)
+        start = (-raw.ctypes.data) % page
+        view = raw[start:start + arr.nbytes].view(arr.dtype)
+        view[:] = arr
+        bufs[name] = (raw, view)
+    out_raw = np.empty(n * 16 + 2 * page, dtype=np.uint8)
+    ostart = (-out_raw.ctypes.data) % page
+    out = out_raw[ostart:ostart + n * 16].view(np.uint64).reshape(n, 2)
+    regs = [bufs["keys"][1], bufs["offs"][1], out]
+    for r in regs:  # the first 2 pages only
+        assert kvh.lib.kvh_host_register(r.ctypes.data, 2 * page) == 0
+    pm = kvh.lib.kvh_set_tuning(15, 1)
+    try:
+        for mib in (1, 64):  # several chunks, then one chunk
+            kvh.lib.kvh_set_tuning(15, mib)
+            out[:] = 0
+            rc = kvh.lib.kvh_meow128_var_host(bufs["keys"][1].ctypes.data, bufs["offs"][1].ctypes.data, n,
+                                              C.c_uint64(STATIC[0]), C.c_uint64(STATIC[1]), out.ctypes.data, 0)
+            assert rc == 0
+            np.testing.assert_array_equal(out, want)
+    finally:
+        kvh.lib.kvh_set_tuning(15, pm)
+        for r in regs:
+            assert kvh.lib.kvh_host_unregister(r.ctypes.data) == 0
+
+
+@pytest.mark.parametrize("n", [1, 8, 64, 1024, 16384])
+def test_one_chunk_batches_at_raikv_sizes(kvh, n):
+    """raikv's own batch sizes (8 keys per prefetch pipe, ev_net.h:442; 16K
+    frags per ctest batch, ctest.c:34) take the one-chunk path: pinned and
+    pageable, fixed and variable length, against the device-resident kernel
+    and the oracle."""
+    rng = np.random.default_rng(n)
+    kb = rng.integers(0, 256, n * 16, dtype=np.uint8)
+    want = kvh.meow128_fixed(torch.from_numpy(kb).cuda(), 16, STATIC).cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(kvh.meow128_fixed_host(kb, 16, STATIC), want)
+    hk = kvh.host_empty(kb.shape, np.uint8)
+    hk[:] = kb
+    ho = kvh.host_empty((n, 2), np.uint64)
+    kvh.meow128_fixed_host(hk, 16, STATIC, out=ho)
+    np.testing.assert_array_equal(ho, want)
+    keys, offs = zipf_batch(n, 100 + n, lead=2)
+    got = kvh.meow128_var_host(keys, offs, STATIC)
+    np.testing.assert_array_equal(got, dev_hash_var(kvh, keys, offs, STATIC))
+    m = min(n, 500)
+    sub = keys[int(offs[0]):int(offs[m])]
+    np.testing.assert_array_equal(got[:m], orc_var(ORC, sub, offs[:m + 1] - offs[0], STATIC))
+
+
+def test_multi_device_pool_reused(kvh):
+    """The _multi entries run on persistent workers: many calls in a row
+    (and device lists of growing length) all equal the one-device call."""
+    rng = np.random.default_rng(5)
+    kb = rng.integers(0, 256, 4096 * 16, dtype=np.uint8)
+    want = kvh.meow128_fixed_host(kb, 16, STATIC)
+    for it in range(40):
+        devs = [0] * (1 + it % 4)
+        np.testing.assert_array_equal(kvh.meow128_host_multi(kb, STATIC, devs, key_len=16), want)

@@ -34,14 +34,14 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
 
 
-ENGINES = [(0, 0), (0, 1), (33, 0)]
-ENGINE_IDS = ["bucketed", "radix_u32", "radix_u64"]
+ENGINES = [(0, 0), (0, 2), (0, 1), (33, 0)]
+ENGINE_IDS = ["bucketed2", "bucketed1", "radix_u32", "radix_u64"]
 
 
 class _engine:
-    """knob 20 = 0 bucketed (the default), 1 radix; knob 17 = 33 forces the
-    radix engine on u64 keys over slot + 33 h1 bits (0: u32 keys when the
-    prefix fits 31 bits)."""
+    """knob 20 = 0 two-pass bucketed (the default), 2 one-pass bucketed, 1
+    radix; knob 17 = 33 forces the radix engine on u64 keys over slot + 33 h1
+    bits (0: u32 keys when the prefix fits 31 bits)."""
 
     def __init__(self, kvh, sort_bits, engine):
         self.kvh, self.v = kvh, (sort_bits, engine)
@@ -150,7 +150,9 @@ def test_long_runs(kvh, eng):
 
 
 @pytest.mark.parametrize("n,map_size", [(1, 1 << 30), (2, 1 << 30), (6144, 1 << 30), (6145, 1 << 30),
+                                        (12289, 1 << 30), (24577, 1 << 30), (2048, 1 << 30), (2049, 1 << 30),
                                         (65536, 1 << 30), (65537, 1 << 30), (1_000_003, 1 << 30),
+                                        (1_000_003, (3 << 28) + 64 * 1000), (30_000_001, (96 << 30) + 64 * 7),
                                         (20_000_000, 1 << 30), (65537, (448 << 10) + 64 * 600), (1_000_003, (448 << 10) + 64 * 600),
                                         (65537, 1 << 40), (1_000_003, 1 << 40)])
 def test_engines_agree(kvh, n, map_size):
@@ -169,11 +171,12 @@ def test_engines_agree(kvh, n, map_size):
     g = kvh.HtGeom.from_map(map_size, 64, 1.0, 4, 4)
     srt = kvh.HtSorter(g, n)
     res = {}
-    for e in (0, 1):
+    for e in (0, 2, 1):
         with _engine(kvh, 0, e):
             oh, oi = srt.sort(h, items=items, dedup=True)
             res[e] = (oh.clone(), oi.clone(), int(srt.dups.item()))
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1]) and res[0][2] == res[1][2]
+    for e in (2, 1):
+        assert torch.equal(res[0][0], res[e][0]) and torch.equal(res[0][1], res[e][1]) and res[0][2] == res[e][2], e
     if n <= 65537:
         og = orc_geom(ORC, map_size, 64, 1.0, 4, 4)
         wh, wi, wd = np_ht_sort(og, host(h), items=host(items), dedup=True)
@@ -200,6 +203,43 @@ def test_long_run_bound(kvh):
     assert np.array_equal(host(oi), np.arange(n - 1, -1, -1, dtype=np.uint64))
     assert int(srt.dups.item()) == 0
     assert dt < 30, dt
+
+
+def test_hot_key_bound(kvh):
+    """~20M copies of one (h1, h2) (the KVH_DEDUP hot key) in a
+    25M batch on the default engine.  The hot key's bucket overflows the LDS
+    sort; the two-pass scatter delivers its records in input order, so
+    k_bk_long finds it ordered and emits it in one pass (it took seconds
+    through the bitonic network).  Output: the hot key's rows contiguous,
+    all but the last marked duplicate, items the input indices in order;
+    the rest against the radix engine."""
+    import time
+    n, hot = 25_000_000, 20_000_000
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(9)
+    h = torch.randint(-2**63, 2**63 - 1, (n, 2), dtype=torch.int64, device="cuda", generator=gen)
+    sel = torch.randperm(n, device="cuda", generator=gen)[:hot]
+    h[sel, 0] = 0x0123_4567_89ab_cdef
+    h[sel, 1] = 0x7777
+    g = kvh.HtGeom.from_map(64 << 30, 64, 1.0, 4, 4)
+    srt = kvh.HtSorter(g, n)
+    srt.sort(h, dedup=True)  # warm
+    torch.cuda.synchronize()
+    t0 = time.time()
+    oh, oi = srt.sort(h, dedup=True)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    dups = int(srt.dups.item())
+    with _engine(kvh, 0, 1):
+        rh, ri = srt.sort(h, dedup=True)
+        rd = int(srt.dups.item())
+    assert torch.equal(oh, rh) and torch.equal(oi, ri) and dups == rd >= hot - 1
+    is_hot = (h[oi, 1] == 0x7777) & (h[oi, 0] == 0x0123_4567_89ab_cdef)
+    idx = torch.nonzero(is_hot).flatten()
+    assert idx.numel() == hot and int(idx[-1] - idx[0]) == hot - 1  # contiguous
+    hi = oi[idx]
+    assert bool((hi[1:] > hi[:-1]).all())  # input order
+    assert dt < 0.5, dt
 
 
 def test_full_size_properties(kvh):

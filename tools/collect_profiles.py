@@ -35,6 +35,21 @@ tpath = os.path.join(root, "profiles", "pmc_traffic.json")
 spath = os.path.join(dst, "summary.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
 summary = json.load(open(spath)) if os.path.exists(spath) else {}
+def timed_avg(d, names, steps):
+    """Mean duration of the LAST `steps` dispatches of the hot kernel(s) in
+    the traced bench run: bench.py's timed region (the settle phase and the
+    warm-up come before it, and nothing after it launches the kernel)."""
+    f = os.path.join(d, "trace", "run_kernel_trace.csv")
+    if not os.path.exists(f) or not steps:
+        return None, 0
+    rows = [r for r in csv.DictReader(open(f)) if any(h in r["Kernel_Name"] for h in names)]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    last = rows[-steps:]
+    if not last:
+        return None, 0
+    return sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last) / len(last), len(last)
+
+
 for c in sorted(os.listdir(src)):
     d = os.path.join(src, c)
     if not os.path.isdir(d) or c == "calib":
@@ -83,7 +98,10 @@ for c in sorted(os.listdir(src)):
             clk = None
             if hot and "GRBM_GUI_ACTIVE" in v:
                 clk = v["GRBM_GUI_ACTIVE"] / 8 / (float(hot[0]["AverageNs"]) * 1e-9) / 1e9
+            steps = json.loads(bj[-1]).get("steps") if bj else None
+            tavg, tn = timed_avg(d, hot_names, steps)
             summary[c] = {"kernel": hot[0]["Name"][:90] if hot else k, "avg_ns": float(hot[0]["AverageNs"]) if hot else None,
+                          "avg_ns_timed": tavg, "timed_dispatches": tn,
                           "calls": int(hot[0]["Calls"]) if hot else None, "hbm_bytes_per_launch": hbm,
                           "clock_GHz_est": clk,
                           "lds_util": (v["SQ_LDS_IDX_ACTIVE"] / 256 / (v["GRBM_GUI_ACTIVE"] / 8)) if "SQ_LDS_IDX_ACTIVE" in v else None}

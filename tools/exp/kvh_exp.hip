@@ -891,7 +891,14 @@ k_var6x(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uin
 }
 
 // ------------------------------------------------------------ k_var9x
-template <int NT, int NW, int KF, bool PF = false, bool PR = false>
+// ABL (counter-only builds, outputs are not hashes): 1 = hash stage written
+// in sorted order (no slot scatter), 3 = per-length constants read for the
+// wave's first lane's length (no lane-divergent constant reads), 4 = window
+// ranks by 6 ballots "match any" + one atomic per distinct class (no
+// same-address atomics; outputs ARE hashes).  ST: 0 = LDS hash stage, 1 =
+// hashes stored straight to their slots (normal stores), 2 = the same
+// non-temporal.
+template <int NT, int NW, int KF, bool PF = false, bool PR = false, int ABL = 0, int ST = 0, int SB = 4>
 __global__ void __launch_bounds__(NW * 64)
 k_var9x(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -956,21 +963,39 @@ k_var9x(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uin
     }
     // counting sort of the window by 16-byte length class
 #pragma unroll
-    for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
+    for (int q = 0; q < SB; q++) hist[lane * SB + q] = 0;
     wave_sync();
 #pragma unroll
     for (int m = 0; m < M; m++) {
       const uint32_t j = lane + 64 * m;
+      if constexpr (ABL == 4) {  // ranks by ballots; counters at class * 4 (sub-counter 0)
+        const bool v = j < k;
+        const uint32_t cls = (L[m] >> 4) < 63u ? (L[m] >> 4) : 63u;
+        b[m] = cls * 4u;
+        uint64_t eq = __ballot(v);
+#pragma unroll
+        for (int bit = 0; bit < 6; bit++) {
+          const uint64_t B = __ballot((cls >> bit) & 1u);
+          eq &= ((cls >> bit) & 1u) ? B : ~B;
+        }
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(eq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)eq, 0u));
+        uint32_t bs = 0;
+        if (v && below == 0) bs = atomicAdd(&hist[b[m]], (uint32_t)__popcll(eq));
+        const uint32_t lead = v ? (uint32_t)__builtin_ctzll(eq) : lane;
+        bs = __shfl(bs, lead, 64);
+        r[m] = bs + below;
+        continue;
+      }
       // 64 length classes x 4 sub-counters by lane & 3: a quarter of the
       // same-address atomics (a class's keys in one instruction serialise)
-      b[m] = ((L[m] >> 4) < 63u ? (L[m] >> 4) : 63u) * 4u + (lane & 3u);
+      b[m] = ((L[m] >> 4) < 63u ? (L[m] >> 4) : 63u) * (uint32_t)SB + (lane & (uint32_t)(SB - 1));
       r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
     }
     wave_sync();
     {
-      uint32_t v[4], sum = 0;
+      uint32_t v[SB], sum = 0;
 #pragma unroll
-      for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
+      for (int q = 0; q < SB; q++) { v[q] = hist[lane * SB + q]; sum += v[q]; }
       uint32_t inc = sum;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -979,7 +1004,7 @@ k_var9x(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uin
       }
       uint32_t run = inc - sum;
 #pragma unroll
-      for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
+      for (int q = 0; q < SB; q++) { hist[lane * SB + q] = run; run += v[q]; }
     }
     wave_sync();
 #pragma unroll
@@ -1023,23 +1048,174 @@ k_var9x(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uin
       if (valid) {
         const uint8_t* p = base + rc.x;
         const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
-        const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
+        const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, ABL == 3 ? rfl(kl) : kl, s1, s2, T);
         Blk h;
         if (al) h = meow_a<true, 48, PF>(p, kl, safe, K, T);
         else if (cm == 48) h = meow_a<false, 48, PF>(p, kl, safe, K, T);
         else if (cm == 32) h = meow_a<false, 32, PF>(p, kl, safe, K, T);
         else if (cm == 16) h = meow_a<false, 16, PF>(p, kl, safe, K, T);
         else h = meow_a<false, 0, PF>(p, kl, safe, K, T);
-        stage[rc.y & 255u] = fix ? fixup(h) : h;
+        if constexpr (ST == 1) store_h<false>(out, i0 + (rc.y & 255u), h, fix);
+        else if constexpr (ST == 2) store_h<true>(out, i0 + (rc.y & 255u), h, fix);
+        else stage[ABL == 1 ? pos : (rc.y & 255u)] = fix ? fixup(h) : h;
       }
+    }
+    if constexpr (ST == 0) {
+      wave_sync();
+#pragma unroll
+      for (int c = 0; c < M; c++) {
+        const uint32_t j = 64 * c + lane;
+        if (j < k) store_h<true>(out, i0 + j, stage[j], false);
+      }
+    }
+    wave_sync();  // stage and records reused by the next window
+  }
+}
+
+
+// ---------------------------------------------------------------------
+// k_var10: k_var9 with larger per-wave windows (WIN = 512 or 1024 keys).
+// A divergence model over the C2 lengths (one chunk of 64 sorted keys runs
+// as long as the meow_a variant its longest / widest key needs) gives 1.59x
+// the ideal lane-rounds at 256-key windows, 1.29x at 512, 1.16x at 1024.
+// LDS per wave is the sorted records only (8 B per key; the class counters
+// live in the same area while sorting): hashes are stored straight to their
+// slots (NTS: non-temporal) instead of through a 16 B/key LDS stage.  Record
+// = (window byte offset, length << LB | slot), LB = log2(WIN); a window
+// spanning 4 GiB or holding a key of 2^(32-LB) bytes or more takes
+// wide_window.  Offsets: one u64 per key per lane (the end offset of key j
+// is the start of key j+1: a lane shuffle).
+template <int NT, int NW, int KF, int WIN, bool NTS>
+__global__ void __launch_bounds__(NW * 64)
+k_var10(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+        uint64_t* __restrict__ out, uint32_t flags) {
+  constexpr int M = WIN / 64, AREA = WIN * 8;
+  constexpr int LB = WIN == 256 ? 8 : WIN == 512 ? 9 : 10;
+  static_assert((1 << LB) == WIN, "window size");
+  static_assert(AREA >= 1024, "class counters fit the record area");
+  constexpr int kTabB = LdsTab<NT>::kWords * 4, kFullB = kLT * (int)sizeof(VConst9), kKfB = KF * 64;
+  constexpr int kBytes = kTabB + kFullB + kKfB + NW * AREA;
+  static_assert(kBytes <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint32_t smem[kBytes / 4];
+  uint32_t* lds = smem;
+  VConst9* kfull = (VConst9*)((uint8_t*)smem + kTabB);
+  Blk* kf = (Blk*)((uint8_t*)smem + kTabB + kFullB);
+  uint8_t* wavemem = (uint8_t*)smem + kTabB + kFullB + kKfB;
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + KF); l += blockDim.x) {
+    if (l >= (uint32_t)kLT) {
+      const Blk Mx = mixer(s1, s2, l);
+#pragma unroll
+      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), Mx), T);
+      continue;
+    }
+    const MeowConst kc = make_const(s1, s2, l, T);
+    VConst9 v;
+#pragma unroll
+    for (int q = 0; q < 4; q++) { v.F[q] = kc.F[q]; v.G[q] = kc.G[q]; }
+    v.TG2 = kc.TG2; v.TCS0a = kc.TCS0a;
+    kfull[l] = v;
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint2* rec = (uint2*)(wavemem + wv * AREA);
+  uint32_t* hist = (uint32_t*)rec;
+  const uint64_t nwin = (n + WIN - 1) / WIN;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
+  const uint64_t kend = offs[n];
+  for (uint64_t w = gw; w < nwin; w += tw) {
+    const uint64_t i0 = w * WIN;
+    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    const uint64_t ws = offs[i0];
+    const uint64_t wend = kend - ws;
+    uint32_t o[M], L[M], b[M], r[M];
+    bool wide = false;
+    {
+      uint64_t a[M];
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        a[m] = offs[i0 + (j < k ? j : k)];
+      }
+      const uint64_t last = offs[i0 + k];
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        uint64_t e = __shfl_down(a[m], 1, 64);
+        const uint64_t nx = m + 1 < M ? __shfl(a[m + 1 < M ? m + 1 : m], 0, 64) : last;
+        if (lane == 63) e = nx;
+        if (j >= k) e = a[m];
+        o[m] = (uint32_t)(a[m] - ws);
+        L[m] = (uint32_t)(e - a[m]);
+        wide |= e - ws >= (1ull << 32) || e - a[m] >= (1ull << (32 - LB));
+      }
+    }
+    if (__ballot(wide) != 0) {
+      wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds);
+      continue;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
+    wave_sync();
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      b[m] = ((L[m] >> 4) < 63u ? (L[m] >> 4) : 63u) * 4u + (lane & 3u);
+      r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
+    }
+    wave_sync();
+    {
+      uint32_t v[4], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
+      uint32_t inc = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+      uint32_t run = inc - sum;
+#pragma unroll
+      for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
     }
     wave_sync();
 #pragma unroll
-    for (int c = 0; c < M; c++) {
-      const uint32_t j = 64 * c + lane;
-      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
+    for (int m = 0; m < M; m++) r[m] += hist[b[m]];  // final sorted positions
+    wave_sync();  // the counters are overwritten by records below
+#pragma unroll
+    for (int m = 0; m < M; m++) {
+      const uint32_t j = lane + 64 * m;
+      if (j < k) rec[r[m]] = make_uint2(o[m], (L[m] << LB) | j);
     }
-    wave_sync();  // stage and records reused by the next window
+    wave_sync();
+    const uint8_t* base = keys + ws;
+#pragma unroll 1
+    for (int c = 0; c < M; c++) {
+      const uint32_t pos = 64 * c + lane;
+      if (64u * c >= k) break;  // wave-uniform
+      const bool valid = pos < k;
+      const uint2 rc = rec[valid ? pos : 0];
+      const uint32_t kl = valid ? rc.y >> LB : 0u;
+      const bool al = __ballot(kl >= 64u) != 0;
+      const int cm = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
+                   : __ballot((kl & 48u) >= 16u) ? 16 : 0;
+      if (valid) {
+        const uint8_t* p = base + rc.x;
+        const bool safe = (uint64_t)rc.x + kl + 16 <= wend;
+        const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
+        Blk h;
+        if (al) h = meow_a<true, 48, false>(p, kl, safe, K, T);
+        else if (cm == 48) h = meow_a<false, 48, false>(p, kl, safe, K, T);
+        else if (cm == 32) h = meow_a<false, 32, false>(p, kl, safe, K, T);
+        else if (cm == 16) h = meow_a<false, 16, false>(p, kl, safe, K, T);
+        else h = meow_a<false, 0, false>(p, kl, safe, K, T);
+        store_h<NTS>(out, i0 + (rc.y & (WIN - 1)), h, fix);
+      }
+    }
+    wave_sync();  // records reused by the next window
   }
 }
 
@@ -1654,6 +1830,114 @@ k_hybrid(const uint8_t* __restrict__ keys, uint64_t n, uint64_t nB, uint64_t s1,
   }
 }
 
+
+// ---------------------------------------------------------------------
+// k_hybrid_lanes (round 3): config C3 (32-byte keys, 4 seeds per key,
+// kv_hash_meow128_4_same_length_4_seed with one key in all slots) with NBW
+// of the 16 waves running the bitsliced VALU round (bs_meow.hpp) on keys
+// [0, nB) and the others k_fixed_lanes' T-table code (LA = 4 lanes per key)
+// on the hash slots [4 nB, 4 n).  The bitsliced constant masks are
+// wave-uniform, so a bitsliced wave hashes each batch of 512 keys under
+// the four seeds in turn (the keys re-read from L2), storing slot 4 i + a
+// with normal stores (the four passes fill each line in L2).
+template <int NT, int U, int NBW, int PRIO>
+__global__ void __launch_bounds__(kBlock)
+k_hybrid_lanes(const uint8_t* __restrict__ keys, uint64_t n, uint64_t nB, uint64_t* __restrict__ out, uint32_t flags,
+               uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2, uint64_t a3,
+               uint64_t b3) {
+  constexpr int L = 32, NC = 2, SH = 2, NTW = kBlock / 64 - NBW;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ uint32_t bmask[4][bs::KeySrc::kN][32];  // per seed: register t's constant mask
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t sa[4] = {a0, a1, a2, a3}, sb[4] = {b0, b1, b2, b3};
+  if (wv == (uint32_t)NTW) {
+    const uint32_t t = (uint32_t)lane & 31u;
+    const uint32_t zero[4] = {0, 0, 0, 0};
+    auto mk = [&](const Blk& z, int kind) {
+      const uint32_t zz[4] = {z.w[0], z.w[1], z.w[2], z.w[3]};
+      return bs::mask_of(zz, t, kind);
+    };
+#pragma unroll 1
+    for (int a = 0; a < 4; a++) {
+      const MeowConst K = uniform(make_const(sa[a], sb[a], (uint64_t)L, T));
+      uint32_t v[bs::KeySrc::kN];
+      v[bs::KeySrc::kZero] = bs::mask_of(zero, t, bs::kKap);
+      v[bs::KeySrc::kA0] = mk(K.F[0], bs::kKapX);
+      v[bs::KeySrc::kA1] = mk(K.F[1], bs::kKapX);
+      v[bs::KeySrc::kA2] = mk(K.F[2], bs::kKapX);
+      v[bs::KeySrc::kM] = mk(K.M, bs::kKap);
+      v[bs::KeySrc::kG1] = mk(K.G[1], bs::kKap);
+      v[bs::KeySrc::kG3] = mk(K.G[3], bs::kKap);
+      v[bs::KeySrc::kCS2b] = mk(K.CS2b, bs::kKap);
+      v[bs::KeySrc::kMstd] = mk(K.M, bs::kStd);
+      if (lane < 32)
+#pragma unroll
+        for (int q = 0; q < bs::KeySrc::kN; q++) bmask[a][q][t] = v[q];
+    }
+  }
+  __syncthreads();
+  if (wv < (uint32_t)NTW) {
+    if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+    const uint32_t sl = threadIdx.x & 3;
+    uint64_t s1 = sa[0], s2 = sb[0];
+#pragma unroll
+    for (int q = 1; q < 4; q++)
+      if (sl == (uint32_t)q) { s1 = sa[q]; s2 = sb[q]; }
+    const MeowConst K = make_const(s1, s2, (uint64_t)L, T);
+    const uint64_t gw = (uint64_t)blockIdx.x * NTW + wv, tw = (uint64_t)gridDim.x * NTW;
+    const uint64_t ns = n << SH, lastk = n - 1;
+    for (uint64_t b = (nB << SH) + gw * 64 * U; b < ns; b += tw * 64 * U) {
+      Blk D[U][NC];
+      uint64_t slot[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t kk = (b + 64 * u + lane) >> SH;
+        kk = kk < lastk ? kk : lastk;
+        slot[u] = (kk << SH) | sl;
+        load_fixed<L, true, true>(keys + kk * L, D[u]);
+      }
+      Blk h[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
+#pragma unroll
+      for (int u = 0; u < U; u++) store_h<true>(out, slot[u], h[u], fix);
+    }
+  } else {
+    const uint64_t gw = (uint64_t)blockIdx.x * NBW + (wv - NTW), tw = (uint64_t)gridDim.x * NBW;
+    for (uint64_t b = gw * 512; b < nB; b += tw * 512) {
+#pragma unroll 1
+      for (int a = 0; a < 4; a++) {
+        bs::KeySrc cur;
+#pragma unroll
+        for (int q = 0; q < bs::KeySrc::kN; q++) cur.lv[q] = bmask[a][q][lane & 31];
+        uint32_t w[NC][8][4];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const uint8_t* p = keys + (b + 64 * j + lane) * L;
+#pragma unroll
+          for (int c = 0; c < NC; c++) {
+            const v4u v = *(const v4u*)(p + 16 * c);
+            w[c][j][0] = v.x; w[c][j][1] = v.y; w[c][j][2] = v.z; w[c][j][3] = v.w;
+          }
+        }
+        uint32_t h[8][4];
+        bs::meow_bs<L>(w, cur, h);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          Blk x;
+          x.w[0] = h[j][0]; x.w[1] = h[j][1]; x.w[2] = h[j][2]; x.w[3] = h[j][3];
+          store_h<false>(out, ((b + 64 * j + lane) << SH) | (uint64_t)a, x, fix);
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ host side
 using Knob = std::atomic<int>;
 Knob g_tune_pf{0};        // k_fixed: 1 = register prefetch of the next chunk
@@ -1763,6 +2047,20 @@ int exp_var_int(int var, const uint8_t* kp, const uint64_t* offsets, uint64_t n,
                 uint64_t* out, uint32_t flags, hipStream_t st, int cus) {
   const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
   switch (var) {
+    // conflict attribution (counter-only except 31) and store modes of k_var9 (round 3)
+    case 28: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 1>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 29: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 3>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 30: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 4>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 31: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 0, 1>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 32: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 0, 2>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 38: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 0, 0, 8>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 39: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 3, 0, 8>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    // k_var10: larger windows, records-only LDS, hashes stored straight to their slots
+    case 33: hipLaunchKernelGGL((k_var10<2, 16, 256, 512, false>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 34: hipLaunchKernelGGL((k_var10<2, 16, 256, 512, true>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 35: hipLaunchKernelGGL((k_var10<2, 8, 256, 1024, false>), dim3(grid), dim3(512), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 36: hipLaunchKernelGGL((k_var10<2, 12, 192, 512, false>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
+    case 37: hipLaunchKernelGGL((k_var10<2, 16, 256, 256, false>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     case 26:  // k_var9 with long keys two lanes per key (meow_pair), 16 waves: spills, 3.75 ms
       hipLaunchKernelGGL((k_var9x<2, 16, 256, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n,
                          seed1, seed2, out, flags);
@@ -1849,7 +2147,7 @@ bool exp_var(int var, const uint8_t* kp, const uint64_t* offsets, uint64_t n, ui
   return true;
 }
 
-bool exp_var_knob(int v) { return v >= 2 && v <= 27; }
+bool exp_var_knob(int v) { return v >= 2 && v <= 39; }
 
 int exp_set_tuning(int k, int value) {
   auto set = [](Knob& g, int v) { return g.exchange(v, std::memory_order_relaxed); };
@@ -1878,6 +2176,32 @@ struct Register {
 }  // namespace
 
 extern "C" {
+
+// C3 hybrid (research): `permille` of the keys (rounded down to 512) through
+// the bitsliced waves, nbw of 16 waves bitsliced (2, 4 or 8), T-table waves at
+// s_setprio(prio) (0 or 2).  32-byte keys at a 16-byte aligned base, 4 seeds
+// (seeds[8]), out[n][4][2].  permille = 0 runs the same kernel with no
+// bitsliced keys (the waves idle): compare with the product's k_fixed_lanes.
+int kvh_exp_multiseed_hybrid(const void* keys, size_t n, const uint64_t* seeds, uint64_t* out, int permille,
+                             int nbw, int prio, uint32_t flags, void* stream) {
+  if (!keys || !out || !seeds || n == 0 || ((uintptr_t)keys & 15)) return set_err(KVH_EINVAL);
+  int cus = 0, rc = device_cus(&cus);
+  if (rc) return rc;
+  const uint64_t nB = (uint64_t)((double)n * permille / 1000.0) / 512 * 512;
+  const uint64_t* s = seeds;
+  const int key = nbw * 10 + prio;
+  switch (key) {
+#define KVH_HL(NBWv, Pv)                                                                                         \
+  case NBWv * 10 + Pv:                                                                                           \
+    hipLaunchKernelGGL((k_hybrid_lanes<4, 2, NBWv, Pv>), dim3(cus), dim3(kBlock), 0, (hipStream_t)stream,         \
+                       (const uint8_t*)keys, (uint64_t)n, nB, out, flags, s[0], s[1], s[2], s[3], s[4], s[5], s[6], \
+                       s[7]);                                                                                    \
+    return launch_done();
+    KVH_HL(2, 0) KVH_HL(2, 2) KVH_HL(4, 0) KVH_HL(4, 2) KVH_HL(8, 2)
+#undef KVH_HL
+    default: return set_err(KVH_EINVAL);
+  }
+}
 // diagnostics: copy the per-wave phase stamps of the last STAMP launch
 int kvh_debug_stamps(uint64_t* host, size_t count) {
   if (count > 4096 * 8) count = 4096 * 8;

@@ -6,8 +6,9 @@
 
 n        keys per length (default 100M, the C1 batch size)
 lens     comma list (default 16,24,32,48,64)
-variants comma list of NT*10+U kernel shapes to A/B (e.g. 24,22,44,42),
-         or "default" (the shipped choice only)
+variants comma list of NT*10+U kernel shapes to A/B (e.g. 24,22,44,42;
+         a trailing p = the software-pipelined k_fixed_pl, knob 22), or
+         "default" (the shipped choice only)
 
 Per length: 500 ms settle (the post-idle power transient),
 then per variant 5 warm-up + 20 timed launches with HIP events on the launch
@@ -40,6 +41,10 @@ lib = kvh.lib
 
 
 def setv(v):
+    """'default', or NT*10+U with an optional 'p' (knob 22: the software-pipelined kernel)"""
+    pl = v.endswith("p")
+    lib.kvh_set_tuning(22, 1 if pl else 0)
+    v = v[:-1] if pl else v
     if v == "default":
         lib.kvh_set_tuning(0, 0)
         lib.kvh_set_tuning(3, 0)
