@@ -381,6 +381,25 @@ def load_traffic(config_name: str):
     return None, None
 
 
+def resolve_config(name, rank: int, world: int, keys_override: int = 0):
+    """The workload of this rank: c1 at N = 1 and c4g (BASELINE configs[4]:
+    one global 1B x 32 B batch, strong scaling) at N > 1 unless named; a
+    global batch's rank r hashes index range shard_range(n, r, N).  Returns
+    (name, cfg with this rank's n, the global key count)."""
+    if name is None:
+        name = "c1" if world == 1 else "c4g"
+    cfg = dict(CONFIGS[name])
+    if keys_override:
+        cfg["n"] = keys_override
+    n_global = cfg["n"]
+    if cfg.get("global_batch"):
+        from raikv_amd.workload import shard_range
+        lo, hi = shard_range(n_global, rank, world)
+        cfg["n"] = hi - lo
+        cfg["shard"] = [lo, hi]
+    return name, cfg, n_global
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -409,19 +428,9 @@ def main():
     import raikv_amd as kvh
     from raikv_amd.workload import STATIC_SEED, C3_SEEDS, zipf_lengths, offsets_from_lengths
 
-    if args.config is None:
-        args.config = "c1" if world == 1 else "c4g"
+    args.config, cfg, n_global = resolve_config(args.config, rank, world, args.keys)
     if args.e2e is None:
         args.e2e = args.config in ("c1", "c2")
-    cfg = dict(CONFIGS[args.config])
-    if args.keys:
-        cfg["n"] = args.keys
-    n_global = cfg["n"]
-    if cfg.get("global_batch"):  # this rank's index range of the one global batch
-        from raikv_amd.workload import shard_range
-        lo, hi = shard_range(n_global, rank, world)
-        cfg["n"] = hi - lo
-        cfg["shard"] = [lo, hi]
     n, L, arity = cfg["n"], cfg["key_len"], cfg["arity"]
     seed = STATIC_SEED
     gen = torch.Generator(device="cuda")

@@ -91,9 +91,9 @@ int kvh_meow128_var_seeded(const void *keys, const uint64_t *offsets,
  * the cuckoo probe).  Pinned buffers from kvh_host_alloc (or a range
  * page-locked by kvh_host_register whose first and last byte are) are
  * DMA'd directly; pageable ones go through pinned bounce buffers (about
- * half the rate).  Batches of <= 4096 keys (knob 21) are copied into a
- * coherent pinned buffer that one kernel reads and writes across PCIe (no
- * DMA, ~15 us per call).  Below ~16-32K 16-byte keys per call one CPU core
+ * half the rate).  Batches of <= 16384 keys and 512 KiB (knob 21) are
+ * copied into a coherent pinned buffer that one kernel reads and writes
+ * across PCIe (no DMA, ~15 us per call).  Below ~16-32K 16-byte keys per call one CPU core
  * running the reference hash is faster.
  * ------------------------------------------------------------------- */
 int kvh_meow128_fixed_host(const void *keys, uint32_t key_len, size_t n,
@@ -475,8 +475,8 @@ int         kvh_device_synchronize(void);
  *  19 = tokenizer (1 wave-chunked, 0 workgroup-chunked),
  *  20 = ht_sort engine (0 two-pass bucketed when the batch fits it, else
  *       radix; 1 radix always; 2 one-pass bucketed when the batch fits it),
- *  21 = host batches of at most this many keys (and 256 KiB of key bytes)
- *       take the zero-copy tiny path (default 4096; 0 off),
+ *  21 = host batches of at most this many keys (and 512 KiB of key bytes)
+ *       take the zero-copy tiny path (default 16384; 0 off),
  *   3 also takes 3 for the 40-64-byte fixed-length kernels.
  * Returns the previous value or KVH_EINVAL.  (Research kernels and ablation
  * builds whose outputs are not hashes exist only in the experiments build,

@@ -545,45 +545,135 @@ k_bk_sort(const Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const 
   }
 }
 
-// buckets B3 could not sort in LDS: a bitonic network over their records in
-// place (as k_sort_long), then the outputs.  One workgroup per bucket.
+// all-ascending bitonic network over R[0, len) by the full order (every
+// comparator puts the smaller record at the lower index, so the pad to a
+// power of two is virtual); one workgroup
+__device__ __forceinline__ void bk_bitonic(Rec* __restrict__ R, uint64_t len, const HtGeom& g, uint32_t sb) {
+  const uint32_t tid = threadIdx.x;
+  uint64_t P = 1;
+  while (P < len) P <<= 1;
+  for (uint64_t k = 2; k <= P; k <<= 1) {
+    for (uint64_t jj = k >> 1; jj > 0; jj >>= 1) {
+      for (uint64_t t = tid; t < P / 2; t += kSB) {
+        const uint64_t off = t & (jj - 1);
+        uint64_t a, c;
+        if (jj == (k >> 1)) {
+          a = (t / jj) * k + off;
+          c = (t / jj) * k + k - 1 - off;
+        } else {
+          a = (t / jj) * 2 * jj + off;
+          c = a + jj;
+        }
+        if (c >= len) continue;
+        const Rec x = R[a], y = R[c];
+        if (bk_less(g, sb, y, x)) { R[a] = y; R[c] = x; }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Stable three-way partition of R[0, len) around the key of q (key64, h1,
+// h2) into T: T = [less | equal | greater], each part in its input order.
+// One workgroup, blocks of kSB records in order: per block, each class's
+// wave ballots and the wave counts give the positions; running totals carry
+// across blocks.  Returns the sizes of the less and equal parts.
+__device__ __forceinline__ void bk_partition3(const Rec* __restrict__ R, Rec* __restrict__ T, uint64_t len,
+                                              const Rec& q, const HtGeom& g, uint32_t sb, uint64_t* n_less,
+                                              uint64_t* n_eq, uint32_t (&wc)[3][kSB / 64], uint64_t (&tot)[3]) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t qk = sort_key64(g, sb, q.h1);
+  auto cls = [&](const Rec& x) -> uint32_t {  // 0 less, 1 equal, 2 greater than q's key
+    const uint64_t k = sort_key64(g, sb, x.h1);
+    if (k != qk) return k < qk ? 0u : 2u;
+    if (x.h1 == q.h1 && x.h2 == q.h2) return 1u;
+    return rec_less(x.h1, x.h2, q.h1, q.h2) ? 0u : 2u;
+  };
+  // pass 1: the part sizes
+  uint32_t c0 = 0, c1 = 0;
+  for (uint64_t t = tid; t < len; t += kSB) {
+    const uint32_t c = cls(R[t]);
+    c0 += c == 0; c1 += c == 1;
+  }
+  __shared__ uint32_t ws0[kSB / 64], ws1[kSB / 64];
+  for (int o = 32; o >= 1; o >>= 1) { c0 += __shfl_xor(c0, o, 64); c1 += __shfl_xor(c1, o, 64); }
+  if (lane == 0) { ws0[w] = c0; ws1[w] = c1; }
+  __syncthreads();
+  uint64_t L0 = 0, L1 = 0;
+  for (int q2 = 0; q2 < kSB / 64; q2++) { L0 += ws0[q2]; L1 += ws1[q2]; }
+  *n_less = L0;
+  *n_eq = L1;
+  if (tid == 0) { tot[0] = 0; tot[1] = L0; tot[2] = L0 + L1; }
+  __syncthreads();
+  // pass 2: stable scatter
+  for (uint64_t b0 = 0; b0 < len; b0 += kSB) {
+    const uint64_t t = b0 + tid;
+    const bool v = t < len;
+    Rec x;
+    uint32_t c = 3;
+    if (v) { x = R[t]; c = cls(x); }
+    uint32_t below = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+      const uint64_t m = __ballot(c == k);
+      if (c == k) below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (lane == 0) wc[k][w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (v) {
+      uint64_t pos = tot[c] + below;
+      for (uint32_t q2 = 0; q2 < w; q2++) pos += wc[c][q2];
+      T[pos] = x;
+    }
+    __syncthreads();
+    if (tid < 3) {
+      uint64_t s = 0;
+      for (int q2 = 0; q2 < kSB / 64; q2++) s += wc[tid][q2];
+      tot[tid] += s;
+    }
+    __syncthreads();
+  }
+}
+
+// Buckets B3 could not sort in LDS, one workgroup each.  A bucket already in
+// the full order (with the tile-stable two-pass scatter a bucket's records
+// arrive in input order, so a bucket holding one repeated key) skips the
+// network.  Otherwise, when `tmp` is given (the two-pass path: its first
+// record buffer is free by now), a stable three-way partition around the
+// bucket's middle record's key: the equal part is then already in order
+// (all one key, input order), and only the other two parts go through the
+// bitonic network -- a hot key repeated millions of times (the KVH_DEDUP
+// case) among a bucket's ordinary keys costs two passes plus the
+// network over the ordinary keys instead of O(R log^2 R) over all of them
+// on one workgroup.  Without `tmp`, the whole bucket through the network.
 __global__ void __launch_bounds__(kSB)
-k_bk_long(Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start, HtGeom g,
-          uint32_t sb, uint64_t* __restrict__ h_out, uint64_t* __restrict__ items_out, uint32_t dedup,
-          unsigned long long* __restrict__ dups, const uint32_t* __restrict__ novf, const uint32_t* __restrict__ ovf) {
+k_bk_long(Rec* __restrict__ recs, Rec* __restrict__ tmp, const uint32_t* __restrict__ cnt,
+          const uint32_t* __restrict__ start, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
+          uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
+          const uint32_t* __restrict__ novf, const uint32_t* __restrict__ ovf) {
   __shared__ uint32_t wsum[kSB / 64];
+  __shared__ uint32_t wc[3][kSB / 64];
+  __shared__ uint64_t tot[3];
   const uint32_t count = *novf, tid = threadIdx.x;
   uint32_t d = 0;
   for (uint32_t r = blockIdx.x; r < count; r += gridDim.x) {
     const uint32_t b = ovf[r];
     const uint64_t len = cnt[b];
     Rec* R = recs + start[b];
-    // a bucket already in the full order skips the network: with the
-    // tile-stable two-pass scatter a bucket's records arrive in input order,
-    // so a hot key repeated millions of times (the KVH_DEDUP case) costs one
-    // pass here instead of O(R log^2 R) on one workgroup
     uint32_t unordered = 0;
     for (uint64_t t = tid; t + 1 < len; t += kSB) unordered |= bk_less(g, sb, R[t + 1], R[t]) ? 1u : 0u;
-    uint64_t P = 1;
-    while (P < len) P <<= 1;
-    if (!block_sum(unordered, wsum)) P = 1;  // (the loop below then does nothing)
-    for (uint64_t k = 2; k <= P; k <<= 1) {
-      for (uint64_t jj = k >> 1; jj > 0; jj >>= 1) {
-        for (uint64_t t = tid; t < P / 2; t += kSB) {
-          const uint64_t off = t & (jj - 1);
-          uint64_t a, c;
-          if (jj == (k >> 1)) {
-            a = (t / jj) * k + off;
-            c = (t / jj) * k + k - 1 - off;
-          } else {
-            a = (t / jj) * 2 * jj + off;
-            c = a + jj;
-          }
-          if (c >= len) continue;
-          const Rec x = R[a], y = R[c];
-          if (bk_less(g, sb, y, x)) { R[a] = y; R[c] = x; }
-        }
+    if (block_sum(unordered, wsum)) {
+      if (tmp) {
+        Rec* Tm = tmp + start[b];
+        const Rec q = R[len / 2];
+        uint64_t nl = 0, ne = 0;
+        bk_partition3(R, Tm, len, q, g, sb, &nl, &ne, wc, tot);
+        for (uint64_t t = tid; t < len; t += kSB) R[t] = Tm[t];
         __syncthreads();
+        bk_bitonic(R, nl, g, sb);
+        bk_bitonic(R + nl + ne, len - nl - ne, g, sb);
+      } else {
+        bk_bitonic(R, len, g, sb);
       }
     }
     for (uint64_t t = tid; t < len; t += kSB) {
@@ -1069,7 +1159,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                          (const Rec*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                          items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_bk_long, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st, recB,
+      hipLaunchKernelGGL(k_bk_long, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st, recB, recA,
                          (const uint32_t*)cnt, (const uint32_t*)start, g, sb, h_out, items_out, dedup ? 1u : 0u,
                          (unsigned long long*)dup_count, (const uint32_t*)novf, (const uint32_t*)ovf);
       return launch_done();
@@ -1110,7 +1200,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                          dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
       if ((rc = launch_done())) return rc;
       hipLaunchKernelGGL(k_bk_long, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st, rec,
-                         (const uint32_t*)cnt, (const uint32_t*)start, g, sb, h_out, items_out, dedup ? 1u : 0u,
+                         (Rec*)nullptr, (const uint32_t*)cnt, (const uint32_t*)start, g, sb, h_out, items_out, dedup ? 1u : 0u,
                          (unsigned long long*)dup_count, (const uint32_t*)novf, (const uint32_t*)ovf);
       return launch_done();
     }

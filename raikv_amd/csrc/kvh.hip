@@ -44,565 +44,6 @@ using namespace kvh::rt;
 
 namespace {
 
-// ------------------------------------------------------------ kernels
-// Wave-chunked streaming: wave w owns chunks of 64*U consecutive keys
-// (chunk c = keys [64U(w + c*W), 64U(w + c*W + 1)), W = waves in the grid);
-// lane l takes keys base + 64u + l, so every load/store instruction moves
-// one contiguous 64*L-byte (64*16-byte) run.  The U loads of a chunk are all
-// issued before the first round (U independent AES chains per lane hide LDS
-// latency; U loads per lane in flight hide HBM latency), loads and stores are
-// non-temporal (each byte is touched once).  Measured on MI355X this access
-// shape streams 6.2 TB/s where a grid-stride loop with a one-step register
-// prefetch tops out near 5.1 TB/s (tools/mem_probe.hip).
-// Indices past the end are clamped to n-1: those lanes recompute key n-1 and
-// store the identical hash to out[n-1] (benign duplicate), which keeps the
-// chunk body one basic block.
-template <int L, int NT, bool A16, int U>
-__global__ void __launch_bounds__(kBlock)
-k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
-        uint64_t* __restrict__ out, uint32_t flags) {
-  constexpr int NC = Plan<L>::NC;
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint64_t lane = threadIdx.x & 63;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
-  const uint64_t last = n - 1;
-  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
-    Blk D[U][NC];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t j = b + 64 * u + lane;
-      load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
-    }
-    Blk h[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t j = b + 64 * u + lane;
-      store_h<true>(out, j < last ? j : last, h[u], fix);
-    }
-  }
-}
-
-// k_fixed software-pipelined across chunks: while chunk c+1's key loads are
-// in flight, chunk c's TAIL (three serial rounds, meow_tail) runs; then
-// chunk c+1's HEAD (the absorb/Mix/Compress rounds whose chains run side by
-// side, meow_head) -- so the serial end of one chunk overlaps the loads and
-// the parallel start of the next instead of exposing its LDS latency.
-// Same chunking, clamping and stores as k_fixed.
-template <int L, int NT, bool A16, int U>
-__global__ void __launch_bounds__(kBlock)
-k_fixed_pl(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
-           uint64_t* __restrict__ out, uint32_t flags) {
-  constexpr int NC = Plan<L>::NC;
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint64_t lane = threadIdx.x & 63;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
-  const uint64_t last = n - 1;
-  uint64_t pb = wave * 64 * U;
-  if (pb >= n) return;  // wave-uniform
-  Blk X[U], Y[U];
-  {
-    Blk D[U][NC];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t j = pb + 64 * u + lane;
-      load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) meow_head<L>(D[u], K, T, X[u], Y[u]);
-  }
-  for (uint64_t b = pb + step; b < n; b += step) {  // wave-uniform trip count
-    Blk D[U][NC];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t j = b + 64 * u + lane;
-      load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
-    }
-    Blk h[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) h[u] = meow_tail<L>(X[u], Y[u], K, T);
-#pragma unroll
-    for (int u = 0; u < U; u++) meow_head<L>(D[u], K, T, X[u], Y[u]);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t j = pb + 64 * u + lane;
-      store_h<true>(out, j < last ? j : last, h[u], fix);
-    }
-    pb = b;
-  }
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const uint64_t j = pb + 64 * u + lane;
-    store_h<true>(out, j < last ? j : last, meow_tail<L>(X[u], Y[u], K, T), fix);
-  }
-}
-
-// Multi-seed (config C3, kv_hash_meow128_4_same_length_4_seed with one key
-// in all slots, key_hash.c:1891-1937): LA = 2, 4 or 8 lanes per key, lane l
-// hashes under seed (l & (LA-1)).  The output slot of (key i, seed a) is
-// i*LA + a, so lane j of a chunk writes slot j: every store is one contiguous
-// 1 KiB run (one lane per key with LA strided 16-byte stores inflated the
-// write traffic 1.3x).  The LA lanes of a key load the same 16-byte pieces
-// (same cache line, one request).  Constants are per lane (VGPRs), computed
-// once in the prologue for the lane's fixed seed.
-template <int L, int NT, bool A16, int U, int LA>
-__global__ void __launch_bounds__(kBlock)
-k_fixed_lanes(const uint8_t* __restrict__ keys, uint64_t n, uint64_t* __restrict__ out, uint32_t flags,
-              uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2, uint64_t a3,
-              uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5, uint64_t a6, uint64_t b6,
-              uint64_t a7, uint64_t b7) {
-  static_assert(LA == 2 || LA == 4 || LA == 8, "lanes per key");
-  constexpr int NC = Plan<L>::NC;
-  constexpr int SH = LA == 2 ? 1 : LA == 4 ? 2 : 3;
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  const uint32_t sl = threadIdx.x & (LA - 1);
-  const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
-  const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
-  uint64_t s1 = sa[0], s2 = sb[0];
-#pragma unroll
-  for (int q = 1; q < LA; q++)
-    if (sl == (uint32_t)q) { s1 = sa[q]; s2 = sb[q]; }
-  const MeowConst K = make_const(s1, s2, (uint64_t)L, T);
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint64_t lane = threadIdx.x & 63;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
-  const uint64_t ns = n << SH, lastk = n - 1;
-  for (uint64_t b = wave * 64 * U; b < ns; b += step) {
-    Blk D[U][NC];
-    uint64_t slot[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      uint64_t k = (b + 64 * u + lane) >> SH;
-      k = k < lastk ? k : lastk;
-      slot[u] = (k << SH) | sl;
-      load_fixed<L, A16, true>(keys + k * L, D[u]);
-    }
-    Blk h[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
-#pragma unroll
-    for (int u = 0; u < U; u++) store_h<true>(out, slot[u], h[u], fix);
-  }
-}
-
-
-template <int L, int NT, bool A16>
-__global__ void __launch_bounds__(kBlock)
-k_fixed_ms(const uint8_t* __restrict__ keys, uint64_t n, const uint64_t* __restrict__ seeds_unused,
-           uint64_t* __restrict__ out, uint32_t flags, uint32_t arity,
-           uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2,
-           uint64_t a3, uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5,
-           uint64_t a6, uint64_t b6, uint64_t a7, uint64_t b7) {
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  __shared__ MeowConst kc[KVH_MAX_ARITY];
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  if (threadIdx.x < KVH_MAX_ARITY && threadIdx.x < arity) {
-    const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
-    const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
-    kc[threadIdx.x] = make_const(sa[threadIdx.x], sb[threadIdx.x], (uint64_t)L, T);
-  }
-  __syncthreads();
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    Blk D[Plan<L>::NC];
-    load_fixed<L, A16>(keys + i * L, D);
-    for (uint32_t a = 0; a < arity; a++) {
-      const MeowConst K = uniform(kc[a]);
-      store_h(out, i * arity + a, meow_ct<L>(D, K, T), fix);
-    }
-  }
-}
-
-// per-lane constants for variable-length batches, from LDS records
-
-// Any length.  VAR: key i = keys[offs[i], offs[i+1]) with per-lane length;
-// !VAR: stride = fixed_len, every lane the same length, `arity` seeds.
-template <bool VAR, int NT>
-__global__ void __launch_bounds__(kBlock)
-k_generic(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t fixed_len,
-          uint64_t n, uint64_t* __restrict__ out, uint32_t flags, uint32_t arity,
-          uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2,
-          uint64_t a3, uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5,
-          uint64_t a6, uint64_t b6, uint64_t a7, uint64_t b7) {
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  __shared__ MeowConst kfull[VAR ? kLT : KVH_MAX_ARITY];
-  __shared__ Blk kf[VAR ? kNF * 4 : 1];
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  if constexpr (VAR) {
-    for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + kNF); l += blockDim.x) {
-      if (l < (uint32_t)kLT) {
-        kfull[l] = make_const(a0, b0, l, T);
-      } else {
-        const Blk M = mixer(a0, b0, l);
-#pragma unroll
-        for (int s = 0; s < 4; s++) kf[(l - kLT) * 4 + s] = aesT(bxor(ramp(s), M), T);
-      }
-    }
-  } else {
-    if (threadIdx.x < arity) {
-      const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
-      const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
-      kfull[threadIdx.x] = make_const(sa[threadIdx.x], sb[threadIdx.x], fixed_len, T);
-    }
-  }
-  __syncthreads();
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    if constexpr (VAR) {
-      const uint64_t o0 = offs[i], o1 = offs[i + 1];
-      const uint64_t L = o1 - o0;  // any size_t length, as kv_hash_meow128 (key_hash.c:1413)
-      const LdsK<LdsTab<NT>, uint64_t> K(kfull, kf, L, a0, b0, T);
-      store_h(out, i, meow_rt(keys + o0, L, K, T), fix);
-    } else {
-      const uint8_t* p = keys + i * (uint64_t)fixed_len;
-      for (uint32_t a = 0; a < arity; a++) {
-        const MeowConst Kc = uniform(kfull[a]);
-        const RegK K{Kc};
-        store_h(out, i * arity + a, meow_rt(p, fixed_len, K, T), fix);
-      }
-    }
-  }
-}
-
-
-
-
-// ---------------------------------------------------------------------
-// k_var6: per-WAVE windows, no workgroup barriers after the prologue.
-// Wave w takes windows of WIN consecutive keys (grid-stride over windows),
-// counting-sorts the window by length in its own LDS slice (LDS atomics
-// give each key its rank inside its length bucket; one wave-wide scan of
-// the 256 bucket counts), then hashes the window in WIN/64 chunks of 64
-// length-sorted keys: a chunk's lanes run (nearly) the same absorb trip
-// count and trail branches, where input order costs 2.7x in divergence for
-// zipf 8-256 B keys (simulation: 0.58 vs 0.29 lane-rounds/key at WIN 256).
-// A wave never waits for another wave, so the long-key chunk of one window
-// no longer stalls the whole workgroup (k_var5's 33 % barrier time).  Keys
-// are gathered from global memory (the window's ~12 KiB stay L2-hot across
-// its chunks); hashes are stored to their original slots.
-
-template <int NT, int WIN, int NW = kBlock / 64, int SH = 0>
-__global__ void __launch_bounds__(NW * 64)
-k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
-       uint64_t* __restrict__ out, uint32_t flags) {
-  using C = Var6Cfg<WIN, NW>;
-  constexpr int M = WIN / 64;
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  __shared__ VConst kfull[kLT];
-  __shared__ Blk kf[C::kWaves * C::kPerWave + LdsTab<NT>::kWords * 4 + kLT * sizeof(VConst) + kNF * 64 <= 163840
-                    ? kNF * 4 : 1];  // F folds for 64 <= L < 320 when the LDS has room
-  constexpr bool kHaveF = sizeof(kf) == kNF * 4 * sizeof(Blk);
-  __shared__ __attribute__((aligned(16))) uint8_t wavemem[C::kWaves * C::kPerWave];
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + (kHaveF ? kNF : 0)); l += blockDim.x) {
-    if (l >= (uint32_t)kLT) {
-      const Blk M = mixer(s1, s2, l);
-#pragma unroll
-      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), M), T);
-      continue;
-    }
-    const MeowConst k = make_const(s1, s2, l, T);
-    VConst v;
-#pragma unroll
-    for (int q = 0; q < 4; q++) { v.F[q] = k.F[q]; v.G[q] = k.G[q]; }
-    v.TG2 = k.TG2; v.CS2b = k.CS2b; v.TCS0a = k.TCS0a;
-    kfull[l] = v;
-  }
-  const Blk* ftab = kHaveF ? kf : nullptr;
-  __syncthreads();
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* hist = (uint32_t*)(wavemem + wv * C::kPerWave);
-  uint32_t* r_off = hist + 256;
-  uint32_t* r_len = r_off + WIN;
-  uint32_t* r_idx = r_len + WIN;
-  const uint64_t nwin = (n + WIN - 1) / WIN;
-  const uint64_t gw = (uint64_t)blockIdx.x * C::kWaves + wv, tw = (uint64_t)gridDim.x * C::kWaves;
-  for (uint64_t w = gw; w < nwin; w += tw) {
-    const uint64_t i0 = w * WIN;
-    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
-    const uint64_t ws = offs[i0];
-    uint64_t o[M];
-    uint32_t L[M], b[M], r[M];
-    bool wide = false;
-#pragma unroll
-    for (int m = 0; m < M; m++) {
-      const uint32_t j = lane + 64 * m;
-      const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
-      o[m] = a - ws;
-      L[m] = (uint32_t)(e - a);
-      wide |= e - ws >= (1ull << 32);
-    }
-    // A window spanning 4 GiB or more (some key of >= 16 MiB; a key of
-    // >= 4 GiB): the records below hold u32 window offsets and lengths, so
-    // this window is hashed in input order with u64 offsets and lengths
-    // instead (wave-uniform), through the same hash call site.
-    const bool wwin = __ballot(wide) != 0;
-    if (!wwin) {
-#pragma unroll
-      for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
-      wave_sync();
-#pragma unroll
-      for (int m = 0; m < M; m++) {
-        const uint32_t j = lane + 64 * m;
-        b[m] = (L[m] >> SH) < 255u ? (L[m] >> SH) : 255u;  // SH: see wave_sort_from
-        r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
-      }
-      wave_sync();
-      {  // exclusive scan of the 256 bucket counts, 4 per lane
-        uint32_t v[4], sum = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
-        uint32_t inc = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t y = __shfl_up(inc, d, 64);
-          if (lane >= (uint32_t)d) inc += y;
-        }
-        uint32_t run = inc - sum;
-#pragma unroll
-        for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
-      }
-      wave_sync();
-#pragma unroll
-      for (int m = 0; m < M; m++) {
-        const uint32_t j = lane + 64 * m;
-        if (j < k) {
-          const uint32_t pos = hist[b[m]] + r[m];
-          r_off[pos] = (uint32_t)o[m];
-          r_len[pos] = L[m];
-          r_idx[pos] = j;
-        }
-      }
-      wave_sync();
-    }
-    const uint8_t* base = keys + ws;
-    // hashes stay in registers until the window is done, then go through
-    // the wave's (now free) record area to leave as one contiguous run:
-    // scattered 16-byte stores in sorted order inflated HBM writes 1.76x
-    Blk hs[M];
-    uint32_t ix[M];
-#pragma unroll
-    for (int c = 0; c < M; c++) {
-      const uint32_t pos = 64 * c + lane;
-      ix[c] = WIN;
-      if (pos < k) {
-        const uint8_t* p;
-        uint64_t kl;
-        if (!wwin) {
-          p = base + r_off[pos];
-          kl = r_len[pos];
-          ix[c] = r_idx[pos];
-        } else {
-          const uint64_t a = offs[i0 + pos];
-          p = keys + a;
-          kl = offs[i0 + pos + 1] - a;
-          ix[c] = pos;
-        }
-        const LdsKV5<LdsTab<NT>, uint64_t> K(kfull, kl, s1, s2, T, ftab);
-        hs[c] = meow_rt(p, kl, K, T);
-        if (fix) hs[c] = fixup(hs[c]);
-      }
-    }
-    wave_sync();
-    static_assert(C::kPerWave >= WIN * 16, "output staging fits the wave's area");
-    Blk* stage = (Blk*)hist;
-#pragma unroll
-    for (int c = 0; c < M; c++)
-      if (ix[c] < (uint32_t)WIN) stage[ix[c]] = hs[c];
-    wave_sync();
-#pragma unroll
-    for (int c = 0; c < M; c++) {
-      const uint32_t j = 64 * c + lane;
-      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
-    }
-    wave_sync();  // records reused by the next window
-  }
-}
-
-// ---------------------------------------------------------------------
-// k_var9: k_var6's per-wave windows, sorted by 16-byte length class, with
-// the two costs its counters name removed:
-//  * L2 requests.  The L1 does not merge misses of different load
-//    instructions, so k_var6's byte-aligned pieces (dwordx4 + dword each)
-//    and dword-by-dword tails cost ~7 L2 requests per key, and the L1->L2
-//    queue (46 requests in flight per CU at ~430 cycles) sets its time.
-//    meow_a reads 16-byte aligned chunks: one request per 16 bytes;
-//  * serial latency.  meow_rt's per-lane branches run one after the other
-//    in a wave (each trail chunk's load, each Mix state, each Compress half);
-//    meow_a runs, per chunk of 64 sorted keys, one straight-line variant
-//    chosen by two wave-uniform facts (some key has a full block; the
-//    largest trail), so the state chains interleave and every short key's
-//    loads are issued before its first round.
-// The variants need ~165 VGPRs, so 12 waves per CU; hashes go straight to
-// the wave's LDS stage at their input slot, records are 8 bytes
-// (window offset, length << 8 | slot), and no per-window value lives in a
-// register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
-// more take wide_window (input order, u64 offsets and lengths).
-
-template <int NT, int NW, int KF, bool PF = false>
-__global__ void __launch_bounds__(NW * 64)
-k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
-       uint64_t* __restrict__ out, uint32_t flags) {
-  // per wave: the hash stage (4 KiB); while sorting it holds the bucket counts
-  // (first KiB) and the sorted records (last 2 KiB), which each lane then
-  // takes into registers (its four sorted positions) before hashes land
-  constexpr int WIN = 256, M = WIN / 64, AREA = WIN * 16;
-  // one LDS object, tables first: a lookup address is then the v_perm result
-  // itself (a table at a nonzero base costs one v_add per lookup)
-  constexpr int kTabB = LdsTab<NT>::kWords * 4, kFullB = kLT * (int)sizeof(VConst9), kKfB = KF * 64;
-  constexpr int kBytes = kTabB + kFullB + kKfB + NW * AREA;
-  static_assert(kBytes <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint32_t smem[kBytes / 4];
-  uint32_t* lds = smem;
-  VConst9* kfull = (VConst9*)((uint8_t*)smem + kTabB);
-  Blk* kf = (Blk*)((uint8_t*)smem + kTabB + kFullB);
-  uint8_t* wavemem = (uint8_t*)smem + kTabB + kFullB + kKfB;
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + KF); l += blockDim.x) {
-    if (l >= (uint32_t)kLT) {
-      const Blk Mx = mixer(s1, s2, l);
-#pragma unroll
-      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), Mx), T);
-      continue;
-    }
-    const MeowConst k = make_const(s1, s2, l, T);
-    VConst9 v;
-#pragma unroll
-    for (int q = 0; q < 4; q++) { v.F[q] = k.F[q]; v.G[q] = k.G[q]; }
-    v.TG2 = k.TG2; v.TCS0a = k.TCS0a;
-    kfull[l] = v;
-  }
-  __syncthreads();
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  Blk* stage = (Blk*)(wavemem + wv * AREA);
-  uint32_t* hist = (uint32_t*)stage;
-  uint2* rec = (uint2*)(wavemem + wv * AREA + WIN * 8);
-  const uint64_t nwin = (n + WIN - 1) / WIN;
-  const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
-  const uint64_t kend = offs[n];  // the buffer holds every byte up to the last key's end
-  for (uint64_t w = gw; w < nwin; w += tw) {
-    const uint64_t i0 = w * WIN;
-    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
-    const uint64_t ws = offs[i0];
-    const uint64_t wend = kend - ws;  // window-relative
-    uint32_t o[M], L[M], r[M], b[M];
-    bool wide = false;
-#pragma unroll
-    for (int m = 0; m < M; m++) {
-      const uint32_t j = lane + 64 * m;
-      const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
-      o[m] = (uint32_t)(a - ws);
-      L[m] = (uint32_t)(e - a);
-      wide |= e - ws >= (1ull << 32) || e - a >= (1ull << 24);
-    }
-    if (__ballot(wide) != 0) {  // wave-uniform
-      wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds);
-      continue;
-    }
-    // counting sort of the window by 16-byte length class
-#pragma unroll
-    for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
-    wave_sync();
-#pragma unroll
-    for (int m = 0; m < M; m++) {
-      const uint32_t j = lane + 64 * m;
-      // 64 length classes x 4 sub-counters by lane & 3: a quarter of the
-      // same-address atomics (a class's keys in one instruction serialise)
-      b[m] = ((L[m] >> 4) < 63u ? (L[m] >> 4) : 63u) * 4u + (lane & 3u);
-      r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
-    }
-    wave_sync();
-    {
-      uint32_t v[4], sum = 0;
-#pragma unroll
-      for (int q = 0; q < 4; q++) { v[q] = hist[lane * 4 + q]; sum += v[q]; }
-      uint32_t inc = sum;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (lane >= (uint32_t)d) inc += y;
-      }
-      uint32_t run = inc - sum;
-#pragma unroll
-      for (int q = 0; q < 4; q++) { hist[lane * 4 + q] = run; run += v[q]; }
-    }
-    wave_sync();
-#pragma unroll
-    for (int m = 0; m < M; m++) {
-      const uint32_t j = lane + 64 * m;
-      if (j < k) rec[hist[b[m]] + r[m]] = make_uint2(o[m], (L[m] << 8) | j);
-    }
-    wave_sync();
-    // this lane's sorted positions lane, 64 + lane, ... (rotated through
-    // scalars below: a register array indexed in a rolled loop is scratch)
-    uint2 rc0 = rec[lane], rc1 = rec[64 + lane], rc2 = rec[128 + lane], rc3 = rec[192 + lane];
-    wave_sync();  // the stage takes hashes from here on
-    const uint8_t* base = keys + ws;
-#pragma unroll 1
-    for (int c = 0; c < M; c++) {
-      const uint32_t pos = 64 * c + lane;
-      const bool valid = pos < k;
-      const uint2 rc = rc0;
-      rc0 = rc1; rc1 = rc2; rc2 = rc3;
-      const uint32_t kl = valid ? rc.y >> 8 : 0u;
-      const bool al = __ballot(kl >= 64u) != 0;
-      const int cm = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
-                   : __ballot((kl & 48u) >= 16u) ? 16 : 0;
-      if (valid) {
-        const uint8_t* p = base + rc.x;
-        const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
-        const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
-        Blk h;
-        if (al) h = meow_a<true, 48, PF>(p, kl, safe, K, T);
-        else if (cm == 48) h = meow_a<false, 48, PF>(p, kl, safe, K, T);
-        else if (cm == 32) h = meow_a<false, 32, PF>(p, kl, safe, K, T);
-        else if (cm == 16) h = meow_a<false, 16, PF>(p, kl, safe, K, T);
-        else h = meow_a<false, 0, PF>(p, kl, safe, K, T);
-        stage[rc.y & 255u] = fix ? fixup(h) : h;
-      }
-    }
-    wave_sync();
-#pragma unroll
-    for (int c = 0; c < M; c++) {
-      const uint32_t j = 64 * c + lane;
-      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
-    }
-    wave_sync();  // stage and records reused by the next window
-  }
-}
-
-
-
-
 // straight-line restatement, one thread per key, per-key seeds
 __global__ void __launch_bounds__(256)
 k_seeded(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
@@ -621,21 +62,41 @@ k_seeded(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, ui
 // across PCIe itself -- one launch and one synchronize, no DMA copies, no
 // LDS table fill (constant-memory tables, the literal restatement).  Key i
 // is keys[offs[i] - offs[0] ..) (variable length) or keys[i * key_len ..).
+// Each workgroup first copies its 256 keys' offsets and then their bytes
+// into LDS with coalesced 16-byte reads (two PCIe round trips for the whole
+// workgroup; one lane per key reading its own pieces across PCIe costs a
+// round trip per 16 bytes), then hashes from LDS; a workgroup whose keys
+// hold more than kTinyLds bytes reads them from host memory per lane.
+constexpr uint32_t kTinyLds = 32768;
 __global__ void __launch_bounds__(256)
 k_tiny(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint32_t key_len, uint64_t n, uint64_t s1,
        uint64_t s2, uint64_t* __restrict__ out, uint32_t flags) {
-  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+  __shared__ uint64_t so[257];
+  __shared__ __attribute__((aligned(16))) uint32_t buf[(kTinyLds + 32) / 4];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * 256;
+  const uint32_t cnt = (uint32_t)(n - i0 < 256 ? n - i0 : 256);
+  const uint64_t o0 = offs ? offs[0] : 0;
+  for (uint32_t t = tid; t <= cnt; t += 256) so[t] = offs ? offs[i0 + t] - o0 : (i0 + t) * key_len;
+  __syncthreads();
+  const uint64_t lo = so[0] & ~(uint64_t)15, hi = so[cnt], bytes = hi - lo;
   const ConstTab T;
-  uint64_t a, L;
-  if (offs) {
-    a = offs[i] - offs[0];
-    L = offs[i + 1] - offs[i];
-  } else {
-    a = i * key_len;
-    L = key_len;
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  if (bytes <= kTinyLds) {
+    // 16-byte reads of [lo, hi rounded up): inside the caller's batch buffer,
+    // which the host side pads to a 16-byte multiple
+    for (uint64_t x = tid * 16; x < bytes; x += 256 * 16) {
+      const uint4 v = *(const uint4*)(keys + lo + x);
+      *(uint4*)((uint8_t*)buf + x) = v;
+    }
+    __syncthreads();
+    if (tid < cnt) {
+      const uint64_t a = so[tid] - lo, L = so[tid + 1] - so[tid];
+      store_h(out, i0 + tid, meow_literal((const uint8_t*)buf + a, L, s1, s2, T, LdsBytes{}), fix);
+    }
+  } else if (tid < cnt) {
+    store_h(out, i0 + tid, meow_literal(keys + so[tid], so[tid + 1] - so[tid], s1, s2, T), fix);
   }
-  store_h(out, i, meow_literal(keys + a, L, s1, s2, T), (flags & KVH_FIXUP) != 0);
 }
 
 // streaming: state[16 words] in/out; absorb nblk full 64-byte blocks
@@ -711,297 +172,26 @@ namespace {
 // Tuning knobs (kvh_set_tuning): process-wide, read once per call with
 // relaxed atomic loads, so a knob set on one thread never races a launch on
 // another (a call in flight keeps the value it read).
+}  // namespace
+
+// Tuning knobs (kvh_set_tuning): process-wide, read once per call with
+// relaxed atomic loads, so a knob set on one thread never races a launch on
+// another (a call in flight keeps the value it read).  The kernel-selection
+// knobs are shared with kvh_fixed.hip / kvh_varlen.hip (kvh_internal.hpp).
 using Knob = std::atomic<int>;
+
+namespace kvh {
+namespace rt {
 Knob g_tune_nt{0};        // tables per LDS: 2 or 4 (0 = per-length default)
 Knob g_tune_wgmul{1};     // workgroups per CU multiplier
 Knob g_tune_generic{0};   // force the generic kernel
-Knob g_tune_kpl{0};       // keys per lane per chunk in k_fixed (1, 2, 4 or 8; 0 = per-length default)
+Knob g_tune_kpl{0};       // keys per lane per chunk in k_fixed (0 = per-length default)
 Knob g_tune_ms_lanes{1};  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
-Knob g_tune_pl{0};        // fixed-length kernel: 1 = software-pipelined across chunks (k_fixed_pl)
 Knob g_tune_var{23};      // var-length kernel: 23 = k_var9 (16 waves; 24 = 12 waves, 25 = 12 waves + block prefetch); 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic
-inline int knob(const Knob& k) { return k.load(std::memory_order_relaxed); }
+}  // namespace rt
+}  // namespace kvh
 
-uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
-  const uint64_t need = (n + kBlock - 1) / kBlock;
-  uint64_t g = (uint64_t)cus * (uint64_t)std::max(1, wg_per_cu * knob(g_tune_wgmul));
-  if (need < g) g = need;
-  return (uint32_t)std::max<uint64_t>(g, 1);
-}
-
-
-template <int L, int NT, int U>
-int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,
-             hipStream_t st, int cus) {
-  const bool a16 = ((uintptr_t)keys & 15) == 0;
-  const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
-  if (knob(g_tune_pl)) {
-    if (a16)
-      hipLaunchKernelGGL((k_fixed_pl<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
-    else
-      hipLaunchKernelGGL((k_fixed_pl<L, NT, false, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
-    return launch_done();
-  }
-  if (a16)
-    hipLaunchKernelGGL((k_fixed<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
-  else
-    hipLaunchKernelGGL((k_fixed<L, NT, false, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
-  return launch_done();
-}
-
-// Fixed-length keys of any length 1-63 (k_fixed<L> covers the multiples of
-// 8 at 8-byte aligned bases): the same wave-chunked streaming and U keys per
-// lane as k_fixed, with the length a kernel argument.  Every lane of the
-// launch has the same length, so every branch of the Meow plan below is
-// wave-uniform (scalar branches, each body U independent rounds: the ILP
-// k_generic's one key per lane lacks, which ran these lengths at half the
-// neighbouring multiples of 8).  NC = ceil(L / 16) 16-byte chunks per key,
-// each read as the dword-aligned 16 bytes at or below it plus one dword,
-// funnelled by the byte offset (v_alignbyte), then masked past the key.  A
-// chunk of keys within 32 bytes of the batch's last byte reads byte-exact
-// (load_bytes) instead: wave-uniform, the last chunk only.
-template <int NC, int U, class Tab>
-__device__ __forceinline__ void meow_small(Blk (&D)[U][NC], uint32_t L, const MeowConst& K, const Tab& T,
-                                           Blk (&h)[U]) {
-  // nb = 0: the trail only (key_hash.c:1200-1210); every state's first
-  // absorb is folded (F_s ^ k, one round)
-  const uint32_t C = L & 48u, t = L & 15u;
-  const bool T0 = C >= 16, T1 = C >= 32, T2 = C >= 48, T3 = t != 0;
-  Blk S0[U], S1[U], S2[U], S3[U];
-  if (T3) {  // the partial chunk is the last one
-#pragma unroll
-    for (int u = 0; u < U; u++) S3[u] = aesdec(aesdec(bxor(K.F[3], D[u][NC - 1]), D[u][NC - 1], T), K.M, T);
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; u++) S3[u] = K.G[3];
-  }
-  if constexpr (NC >= 3) {
-    if (T2) {
-#pragma unroll
-      for (int u = 0; u < U; u++) S2[u] = aesdec(aesdec(bxor(K.F[2], D[u][2]), D[u][2], T), K.M, T);
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; u++) S2[u] = K.G[2];
-    }
-  }
-  if constexpr (NC >= 2) {
-    if (T1) {
-#pragma unroll
-      for (int u = 0; u < U; u++) S1[u] = aesdec(aesdec(bxor(K.F[1], D[u][1]), D[u][1], T), K.M, T);
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; u++) S1[u] = K.G[1];
-    }
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; u++) S1[u] = K.G[1];
-  }
-  if (T0) {
-#pragma unroll
-    for (int u = 0; u < U; u++) S0[u] = aesdec(aesdec(bxor(K.F[0], D[u][0]), D[u][0], T), K.M, T);
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; u++) S0[u] = K.G[0];
-  }
-  // Compress_Meow2 / Compress_Meow and the final round, as meow_ct
-  Blk S2b[U];
-  if (NC >= 3 && T2) {
-    if constexpr (NC >= 3) {
-#pragma unroll
-      for (int u = 0; u < U; u++) S2b[u] = aesdec(aesdec(S2[u], S3[u], T), K.M, T);
-    }
-  } else if (T3) {
-#pragma unroll
-    for (int u = 0; u < U; u++) S2b[u] = aesdec(bxor(K.TG2, S3[u]), K.M, T);
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; u++) S2b[u] = K.CS2b;
-  }
-  if (T0) {
-#pragma unroll
-    for (int u = 0; u < U; u++) h[u] = aesdec(aesdec(aesdec(S0[u], S1[u], T), S2b[u], T), K.M, T);
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; u++) h[u] = aesdec(bxor(K.TCS0a, S2b[u]), K.M, T);
-  }
-}
-
-template <int NC, int NT, int U>
-__global__ void __launch_bounds__(kBlock)
-k_fixed_rt(const uint8_t* __restrict__ keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2,
-           uint64_t* __restrict__ out, uint32_t flags) {
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  fill_tables<NT>(lds);
-  __syncthreads();
-  const LdsTab<NT> T(lds);
-  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
-  const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint64_t lane = threadIdx.x & 63;
-  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
-  const uint64_t last = n - 1, total = n * (uint64_t)L;
-  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
-    const bool exact = (b + 64 * U) * (uint64_t)L + 32 > total;  // this chunk reaches the batch's end
-    Blk D[U][NC];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t j = b + 64 * u + lane;
-      const uint8_t* p = keys + (j < last ? j : last) * (uint64_t)L;
-#pragma unroll
-      for (int c = 0; c < NC; c++) {
-        const int left = (int)L - 16 * c;
-        const uint32_t nv = left >= 16 ? 16u : (uint32_t)left;
-        if (exact) {
-          D[u][c] = load_bytes(p + 16 * c, nv);
-        } else {
-          D[u][c] = load16_full(p + 16 * c);
-          if (c == NC - 1 && nv < 16) {
-#pragma unroll
-            for (int w = 0; w < 4; w++) {
-              const int keep = (int)nv - 4 * w;
-              D[u][c].w[w] &= keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
-            }
-          }
-        }
-      }
-    }
-    Blk h[U];
-    meow_small<NC, U>(D, L, K, T, h);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint64_t j = b + 64 * u + lane;
-      store_h<true>(out, j < last ? j : last, h[u], fix);
-    }
-  }
-}
-
-template <int NC, int NT, int U>
-int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2, uint64_t* out,
-                    uint32_t flags, hipStream_t st, int cus) {
-  const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
-  hipLaunchKernelGGL((k_fixed_rt<NC, NT, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, L, s1, s2, out, flags);
-  return launch_done();
-}
-
-// Default (NT, U) per length from tools/tune.py and tools/len_sweep.py
-// sweeps; knobs 0 and 3 select the others.
-template <int L>
-int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
-                    uint32_t flags, hipStream_t st, int cus) {
-  if (int rc = 0; g_exp.fixed && g_exp.fixed(L, keys, n, s1, s2, out, flags, st, cus, knob(g_tune_nt), knob(g_tune_kpl), &rc))
-    return rc;
-  if constexpr (L == 16 || L == 32) {
-    // per-length defaults from tools/tune.py: Td0..Td3 in LDS
-    // (no rotations), 4 keys per lane at 16 B, 2 at 32 B
-    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
-    const int nt = tnt ? tnt : 4;
-    const int kpl = tkpl ? tkpl : (L == 16 ? 4 : 2);
-    switch (nt * 100 + kpl) {
-      case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 408: return launch_k<L, 4, 8>(keys, n, s1, s2, out, flags, st, cus);
-      case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 208: return launch_k<L, 2, 8>(keys, n, s1, s2, out, flags, st, cus);
-      default: return set_err(KVH_EINVAL);
-    }
-  } else {
-    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
-    switch ((tnt ? tnt : 2) * 100 + (tkpl ? tkpl : 4)) {
-      case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 403: if constexpr (L >= 40) return launch_k<L, 4, 3>(keys, n, s1, s2, out, flags, st, cus); break;
-      case 203: if constexpr (L >= 40) return launch_k<L, 2, 3>(keys, n, s1, s2, out, flags, st, cus); break;
-      default: break;
-    }
-    return set_err(KVH_EINVAL);
-  }
-}
-
-template <int L, int NT, int U>
-int launch_lanes_v(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
-                   uint32_t flags, hipStream_t st, int cus) {
-  const uint32_t grid = grid_for(n * arity, cus, NT == 4 ? 1 : 2);
-#define KVH_LANES_V(LAv)                                                                                \
-  hipLaunchKernelGGL((k_fixed_lanes<L, NT, true, U, LAv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \
-                     s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13],   \
-                     s[14], s[15])
-  if (arity == 2) KVH_LANES_V(2); else if (arity == 4) KVH_LANES_V(4); else KVH_LANES_V(8);
-#undef KVH_LANES_V
-  return launch_done();
-}
-
-template <int L>
-int launch_lanes_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
-                   uint32_t flags, hipStream_t st, int cus) {
-  const bool a16 = ((uintptr_t)keys & 15) == 0;
-  if constexpr (L == 32) {
-    // C3's length: Td0..Td3 in LDS (no rotates, one 16-wave workgroup per CU)
-    // and 2 keys per lane by default -- 118 vs 112 G hash/s for Td0/Td1 with
-    // two workgroups per CU (tools/tune.py, profiles/r02/c3_layout_ab.txt);
-    // knobs 0 / 3 select the others
-    const int nt = knob(g_tune_nt), kpl = knob(g_tune_kpl);
-    if (a16) {
-      switch ((nt ? nt : 4) * 10 + (kpl ? kpl : 2)) {
-        case 22: break;
-        case 21: return launch_lanes_v<L, 2, 1>(keys, n, s, arity, out, flags, st, cus);
-        case 24: return launch_lanes_v<L, 2, 4>(keys, n, s, arity, out, flags, st, cus);
-        case 41: return launch_lanes_v<L, 4, 1>(keys, n, s, arity, out, flags, st, cus);
-        case 42: return launch_lanes_v<L, 4, 2>(keys, n, s, arity, out, flags, st, cus);
-        case 44: return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);
-        default: return set_err(KVH_EINVAL);
-      }
-    }
-  }
-  const uint32_t grid = grid_for(n * arity, cus, 2);
-#define KVH_LANES(A16v, LAv)                                                                            \
-  hipLaunchKernelGGL((k_fixed_lanes<L, 2, A16v, 2, LAv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \
-                     s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13],   \
-                     s[14], s[15])
-  if (a16) {
-    if (arity == 2) KVH_LANES(true, 2); else if (arity == 4) KVH_LANES(true, 4); else KVH_LANES(true, 8);
-  } else {
-    if (arity == 2) KVH_LANES(false, 2); else if (arity == 4) KVH_LANES(false, 4); else KVH_LANES(false, 8);
-  }
-#undef KVH_LANES
-  return launch_done();
-}
-
-template <int L>
-int launch_ms_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
-                uint32_t flags, hipStream_t st, int cus) {
-  const bool a16 = ((uintptr_t)keys & 15) == 0;
-  const uint32_t grid = grid_for(n, cus, 1);
-  if (a16)
-    hipLaunchKernelGGL((k_fixed_ms<L, 4, true>), dim3(grid), dim3(kBlock), 0, st, keys, n, nullptr, out,
-                       flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10],
-                       s[11], s[12], s[13], s[14], s[15]);
-  else
-    hipLaunchKernelGGL((k_fixed_ms<L, 4, false>), dim3(grid), dim3(kBlock), 0, st, keys, n, nullptr, out,
-                       flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10],
-                       s[11], s[12], s[13], s[14], s[15]);
-  return launch_done();
-}
-
-int launch_generic(bool var, const uint8_t* keys, const uint64_t* offs, uint32_t fixed_len, uint64_t n,
-                   const uint64_t* s, uint32_t arity, uint64_t* out, uint32_t flags, hipStream_t st,
-                   int cus) {
-  const uint32_t grid = grid_for(n, cus, 1);
-  if (var)
-    hipLaunchKernelGGL((k_generic<true, 4>), dim3(grid), dim3(kBlock), 0, st, keys, offs, fixed_len, n,
-                       out, flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
-                       s[10], s[11], s[12], s[13], s[14], s[15]);
-  else
-    hipLaunchKernelGGL((k_generic<false, 4>), dim3(grid), dim3(kBlock), 0, st, keys, offs, fixed_len, n,
-                       out, flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9],
-                       s[10], s[11], s[12], s[13], s[14], s[15]);
-  return launch_done();
-}
+namespace {
 
 // Pinned/device staging for the synchronous host drop-ins.
 struct Staging {
@@ -1094,8 +284,8 @@ constexpr int kMaxDev = 64;
 constexpr int kPipesPerDev = 4;
 Knob g_tune_pipe_mib{16};   // key bytes per pipeline chunk, MiB (knob 15)
 Knob g_tune_pipe_slots{4};  // chunks in flight (knob 16)
-Knob g_tune_tiny{4096};     // host batches of at most this many keys take the zero-copy tiny path (knob 21; 0 = off)
-constexpr size_t kTinyBytes = 256 << 10;  // ... and at most this many key bytes
+Knob g_tune_tiny{16384};    // host batches of at most this many keys take the zero-copy tiny path (knob 21; 0 = off)
+constexpr size_t kTinyBytes = 512 << 10;  // ... and at most this many key bytes
 struct HostPipe {
   std::mutex mu;
   hipStream_t s_in = nullptr, s_k = nullptr, s_out = nullptr;
@@ -1201,13 +391,14 @@ int host_pipeline(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, s
       if (P->tiny) (void)hipHostFree(P->tiny);
       P->tiny = nullptr;
       P->tinycap = 0;
-      const size_t cap = std::max<size_t>(need, kTinyBytes + 16 * 4096 + 8 * 4097 + 64);
+      const size_t cap = std::max<size_t>(need, (1 << 20) + 64);
       if ((e = hipHostMalloc((void**)&P->tiny, cap, hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess)
         return hip_err(e);
       P->tinycap = cap;
     }
     if (!P->s_k && (e = hipStreamCreateWithFlags(&P->s_k, hipStreamNonBlocking)) != hipSuccess) return hip_err(e);
     if (kb) memcpy(P->tiny, keys + (var ? offs[0] : 0), kb);
+    memset(P->tiny + kb, 0, al16(kb) - kb);  // k_tiny reads whole 16-byte groups
     if (var) memcpy(P->tiny + o_off, offs, 8 * (n + 1));
     hipLaunchKernelGGL(k_tiny, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, P->s_k, (const uint8_t*)P->tiny,
                        var ? (const uint64_t*)(P->tiny + o_off) : (const uint64_t*)nullptr, key_len, (uint64_t)n, s1,
@@ -1432,38 +623,7 @@ int kvh_meow128_fixed(const void* keys, uint32_t key_len, size_t n, uint64_t see
   if (!keys || !out) return set_err(KVH_EINVAL);
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
-  const uint8_t* k = (const uint8_t*)keys;
-  hipStream_t st = (hipStream_t)stream;
-  const bool a8 = ((uintptr_t)k & 7) == 0;
-  if (!knob(g_tune_generic) && a8) {
-    switch (key_len) {
-      case 8: return launch_fixed_nt<8>(k, n, seed1, seed2, out, flags, st, cus);
-      case 16: return launch_fixed_nt<16>(k, n, seed1, seed2, out, flags, st, cus);
-      case 24: return launch_fixed_nt<24>(k, n, seed1, seed2, out, flags, st, cus);
-      case 32: return launch_fixed_nt<32>(k, n, seed1, seed2, out, flags, st, cus);
-      case 40: return launch_fixed_nt<40>(k, n, seed1, seed2, out, flags, st, cus);
-      case 48: return launch_fixed_nt<48>(k, n, seed1, seed2, out, flags, st, cus);
-      case 56: return launch_fixed_nt<56>(k, n, seed1, seed2, out, flags, st, cus);
-      case 64: return launch_fixed_nt<64>(k, n, seed1, seed2, out, flags, st, cus);
-      default: break;
-    }
-  }
-  if (!knob(g_tune_generic) && key_len >= 1 && key_len < 64) {  // any other length below one block
-    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
-    const int nc = (int)(key_len + 15) / 16, nt = tnt ? tnt : 4, kpl = tkpl ? tkpl : (nc == 1 ? 4 : 2);
-    switch (nc * 1000 + nt * 10 + kpl) {
-#define KVH_RT(NCv, NTv, Uv) \
-  case NCv * 1000 + NTv * 10 + Uv: return launch_fixed_rt<NCv, NTv, Uv>(k, n, key_len, seed1, seed2, out, flags, st, cus);
-      KVH_RT(1, 4, 4) KVH_RT(1, 4, 2) KVH_RT(1, 4, 8) KVH_RT(1, 2, 4) KVH_RT(1, 2, 8)
-      KVH_RT(2, 4, 2) KVH_RT(2, 4, 4) KVH_RT(2, 2, 2) KVH_RT(2, 2, 4)
-      KVH_RT(3, 4, 2) KVH_RT(3, 4, 4) KVH_RT(3, 2, 2) KVH_RT(3, 2, 4)
-      KVH_RT(4, 4, 2) KVH_RT(4, 4, 4) KVH_RT(4, 2, 2) KVH_RT(4, 2, 4)
-#undef KVH_RT
-      default: break;  // a knob pair without an instance: the generic kernel
-    }
-  }
-  uint64_t s[16] = {seed1, seed2};
-  return launch_generic(false, k, nullptr, key_len, n, s, 1, out, flags, st, cus);
+  return fixed_dispatch((const uint8_t*)keys, key_len, n, seed1, seed2, out, flags, (hipStream_t)stream, cus);
 }
 
 int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_t seed1, uint64_t seed2,
@@ -1472,40 +632,7 @@ int kvh_meow128_var(const void* keys, const uint64_t* offsets, size_t n, uint64_
   if (!keys || !offsets || !out) return set_err(KVH_EINVAL);
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
-  hipStream_t st = (hipStream_t)stream;
-  const uint8_t* kp = (const uint8_t*)keys;
-  const int var = knob(g_tune_var);
-  const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
-  switch (var) {
-    case 0: {
-      uint64_t s[16] = {seed1, seed2};
-      return launch_generic(true, kp, offsets, 0, n, s, 1, out, flags, st, cus);
-    }
-    case 13:
-      hipLaunchKernelGGL((k_var6<2, 256, kBlock / 64, 4>), dim3(grid), dim3(kBlock), 0, st, kp, offsets,
-                         (uint64_t)n, seed1, seed2, out, flags);
-      return launch_done();
-    case 7:
-      hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
-                         out, flags);
-      return launch_done();
-    case 23:
-      hipLaunchKernelGGL((k_var9<2, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
-                         out, flags);
-      return launch_done();
-    case 24:
-      hipLaunchKernelGGL((k_var9<2, 12, 192>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
-                         out, flags);
-      return launch_done();
-    case 25:
-      hipLaunchKernelGGL((k_var9<2, 12, 192, true>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1,
-                         seed2, out, flags);
-      return launch_done();
-    default:
-      break;
-  }
-  if (int rc = 0; g_exp.var && g_exp.var(var, kp, offsets, n, seed1, seed2, out, flags, st, cus, &rc)) return rc;
-  return set_err(KVH_EINVAL);
+  return var_dispatch((const uint8_t*)keys, offsets, n, seed1, seed2, out, flags, (hipStream_t)stream, cus);
 }
 
 int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const uint64_t* seeds,
@@ -1517,31 +644,7 @@ int kvh_meow128_multiseed(const void* keys, uint32_t key_len, size_t n, const ui
   if (rc) return rc;
   uint64_t s[16] = {0};
   for (uint32_t a = 0; a < arity; a++) { s[2 * a] = seeds[2 * a]; s[2 * a + 1] = seeds[2 * a + 1]; }
-  const uint8_t* k = (const uint8_t*)keys;
-  hipStream_t st = (hipStream_t)stream;
-  const bool a8 = ((uintptr_t)k & 7) == 0;
-  if (!knob(g_tune_generic) && a8 && knob(g_tune_ms_lanes) && (arity == 2 || arity == 4 || arity == 8)) {
-    switch (key_len) {
-      case 8: return launch_lanes_L<8>(k, n, s, arity, out, flags, st, cus);
-      case 16: return launch_lanes_L<16>(k, n, s, arity, out, flags, st, cus);
-      case 24: return launch_lanes_L<24>(k, n, s, arity, out, flags, st, cus);
-      case 32: return launch_lanes_L<32>(k, n, s, arity, out, flags, st, cus);
-      case 40: return launch_lanes_L<40>(k, n, s, arity, out, flags, st, cus);
-      case 48: return launch_lanes_L<48>(k, n, s, arity, out, flags, st, cus);
-      case 56: return launch_lanes_L<56>(k, n, s, arity, out, flags, st, cus);
-      case 64: return launch_lanes_L<64>(k, n, s, arity, out, flags, st, cus);
-      default: break;
-    }
-  }
-  if (!knob(g_tune_generic) && a8) {
-    switch (key_len) {
-      case 16: return launch_ms_L<16>(k, n, s, arity, out, flags, st, cus);
-      case 32: return launch_ms_L<32>(k, n, s, arity, out, flags, st, cus);
-      case 64: return launch_ms_L<64>(k, n, s, arity, out, flags, st, cus);
-      default: break;
-    }
-  }
-  return launch_generic(false, k, nullptr, key_len, n, s, arity, out, flags, st, cus);
+  return multiseed_dispatch((const uint8_t*)keys, key_len, n, s, arity, out, flags, (hipStream_t)stream, cus);
 }
 
 int kvh_meow128_batch(const void* keys, const uint64_t* offsets, uint32_t fixed_len, size_t n,
@@ -1855,7 +958,6 @@ int kvh_set_tuning(int k, int value) {
     case 19: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_tok, value);
     case 20: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_engine, value);
     case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
-    case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_pl, value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }

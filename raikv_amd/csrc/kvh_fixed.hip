@@ -1,0 +1,477 @@
+// kvh_fixed.hip -- the fixed-length Meow128 kernels of the engine (configs
+// C1, C3, C4 and the metric's 16-64 B range) and their launchers; the C-ABI
+// entry points (kvh.hip) call fixed_dispatch / multiseed_dispatch after
+// checking their arguments.  See DESIGN.md §3.1-3.3 and meow_dev.hpp.
+//   k_fixed<L,NT,A16,U>   fixed length L in {8,16,..,64}, one seed, constants
+//                         folded into SGPRs (C1, C4)
+//   k_fixed_lanes         LA lanes per key, one seed each (C3)
+//   k_fixed_ms            one lane per key, `arity` seeds (C3 fallback)
+//   k_fixed_rt            any fixed length below one block (runtime L)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <atomic>
+#include <algorithm>
+#include "meow_dev.hpp"
+#include "kvh_internal.hpp"
+#include "kvh_var.hpp"
+#include "../../include/kvh.h"
+
+using namespace kvh;
+using namespace kvh::rt;
+
+namespace {
+
+// ------------------------------------------------------------ kernels
+// Wave-chunked streaming: wave w owns chunks of 64*U consecutive keys
+// (chunk c = keys [64U(w + c*W), 64U(w + c*W + 1)), W = waves in the grid);
+// lane l takes keys base + 64u + l, so every load/store instruction moves
+// one contiguous 64*L-byte (64*16-byte) run.  The U loads of a chunk are all
+// issued before the first round (U independent AES chains per lane hide LDS
+// latency; U loads per lane in flight hide HBM latency), loads and stores are
+// non-temporal (each byte is touched once).  Measured on MI355X this access
+// shape streams 6.2 TB/s where a grid-stride loop with a one-step register
+// prefetch tops out near 5.1 TB/s (tools/mem_probe.hip).
+// Indices past the end are clamped to n-1: those lanes recompute key n-1 and
+// store the identical hash to out[n-1] (benign duplicate), which keeps the
+// chunk body one basic block.
+template <int L, int NT, bool A16, int U>
+__global__ void __launch_bounds__(kBlock)
+k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
+        uint64_t* __restrict__ out, uint32_t flags) {
+  constexpr int NC = Plan<L>::NC;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  const uint64_t last = n - 1;
+  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
+    Blk D[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
+    }
+    Blk h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      store_h<true>(out, j < last ? j : last, h[u], fix);
+    }
+  }
+}
+
+// Multi-seed (config C3, kv_hash_meow128_4_same_length_4_seed with one key
+// in all slots, key_hash.c:1891-1937): LA = 2, 4 or 8 lanes per key, lane l
+// hashes under seed (l & (LA-1)).  The output slot of (key i, seed a) is
+// i*LA + a, so lane j of a chunk writes slot j: every store is one contiguous
+// 1 KiB run (one lane per key with LA strided 16-byte stores inflated the
+// write traffic 1.3x).  The LA lanes of a key load the same 16-byte pieces
+// (same cache line, one request).  Constants are per lane (VGPRs), computed
+// once in the prologue for the lane's fixed seed.
+template <int L, int NT, bool A16, int U, int LA>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_lanes(const uint8_t* __restrict__ keys, uint64_t n, uint64_t* __restrict__ out, uint32_t flags,
+              uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2, uint64_t a3,
+              uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5, uint64_t a6, uint64_t b6,
+              uint64_t a7, uint64_t b7) {
+  static_assert(LA == 2 || LA == 4 || LA == 8, "lanes per key");
+  constexpr int NC = Plan<L>::NC;
+  constexpr int SH = LA == 2 ? 1 : LA == 4 ? 2 : 3;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const uint32_t sl = threadIdx.x & (LA - 1);
+  const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
+  const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
+  uint64_t s1 = sa[0], s2 = sb[0];
+#pragma unroll
+  for (int q = 1; q < LA; q++)
+    if (sl == (uint32_t)q) { s1 = sa[q]; s2 = sb[q]; }
+  const MeowConst K = make_const(s1, s2, (uint64_t)L, T);
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  const uint64_t ns = n << SH, lastk = n - 1;
+  for (uint64_t b = wave * 64 * U; b < ns; b += step) {
+    Blk D[U][NC];
+    uint64_t slot[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      uint64_t k = (b + 64 * u + lane) >> SH;
+      k = k < lastk ? k : lastk;
+      slot[u] = (k << SH) | sl;
+      load_fixed<L, A16, true>(keys + k * L, D[u]);
+    }
+    Blk h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
+#pragma unroll
+    for (int u = 0; u < U; u++) store_h<true>(out, slot[u], h[u], fix);
+  }
+}
+
+
+template <int L, int NT, bool A16>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_ms(const uint8_t* __restrict__ keys, uint64_t n, const uint64_t* __restrict__ seeds_unused,
+           uint64_t* __restrict__ out, uint32_t flags, uint32_t arity,
+           uint64_t a0, uint64_t b0, uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2,
+           uint64_t a3, uint64_t b3, uint64_t a4, uint64_t b4, uint64_t a5, uint64_t b5,
+           uint64_t a6, uint64_t b6, uint64_t a7, uint64_t b7) {
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ MeowConst kc[KVH_MAX_ARITY];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  if (threadIdx.x < KVH_MAX_ARITY && threadIdx.x < arity) {
+    const uint64_t sa[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
+    const uint64_t sb[8] = {b0, b1, b2, b3, b4, b5, b6, b7};
+    kc[threadIdx.x] = make_const(sa[threadIdx.x], sb[threadIdx.x], (uint64_t)L, T);
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    Blk D[Plan<L>::NC];
+    load_fixed<L, A16>(keys + i * L, D);
+    for (uint32_t a = 0; a < arity; a++) {
+      const MeowConst K = uniform(kc[a]);
+      store_h(out, i * arity + a, meow_ct<L>(D, K, T), fix);
+    }
+  }
+}
+
+template <int L, int NT, int U>
+int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,
+             hipStream_t st, int cus) {
+  const bool a16 = ((uintptr_t)keys & 15) == 0;
+  const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
+  if (a16)
+    hipLaunchKernelGGL((k_fixed<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+  else
+    hipLaunchKernelGGL((k_fixed<L, NT, false, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
+  return launch_done();
+}
+
+// Fixed-length keys of any length 1-63 (k_fixed<L> covers the multiples of
+// 8 at 8-byte aligned bases): the same wave-chunked streaming and U keys per
+// lane as k_fixed, with the length a kernel argument.  Every lane of the
+// launch has the same length, so every branch of the Meow plan below is
+// wave-uniform (scalar branches, each body U independent rounds: the ILP
+// k_generic's one key per lane lacks, which ran these lengths at half the
+// neighbouring multiples of 8).  NC = ceil(L / 16) 16-byte chunks per key,
+// each read as the dword-aligned 16 bytes at or below it plus one dword,
+// funnelled by the byte offset (v_alignbyte), then masked past the key.  A
+// chunk of keys within 32 bytes of the batch's last byte reads byte-exact
+// (load_bytes) instead: wave-uniform, the last chunk only.
+template <int NC, int U, class Tab>
+__device__ __forceinline__ void meow_small(Blk (&D)[U][NC], uint32_t L, const MeowConst& K, const Tab& T,
+                                           Blk (&h)[U]) {
+  // nb = 0: the trail only (key_hash.c:1200-1210); every state's first
+  // absorb is folded (F_s ^ k, one round)
+  const uint32_t C = L & 48u, t = L & 15u;
+  const bool T0 = C >= 16, T1 = C >= 32, T2 = C >= 48, T3 = t != 0;
+  Blk S0[U], S1[U], S2[U], S3[U];
+  if (T3) {  // the partial chunk is the last one
+#pragma unroll
+    for (int u = 0; u < U; u++) S3[u] = aesdec(aesdec(bxor(K.F[3], D[u][NC - 1]), D[u][NC - 1], T), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S3[u] = K.G[3];
+  }
+  if constexpr (NC >= 3) {
+    if (T2) {
+#pragma unroll
+      for (int u = 0; u < U; u++) S2[u] = aesdec(aesdec(bxor(K.F[2], D[u][2]), D[u][2], T), K.M, T);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) S2[u] = K.G[2];
+    }
+  }
+  if constexpr (NC >= 2) {
+    if (T1) {
+#pragma unroll
+      for (int u = 0; u < U; u++) S1[u] = aesdec(aesdec(bxor(K.F[1], D[u][1]), D[u][1], T), K.M, T);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) S1[u] = K.G[1];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S1[u] = K.G[1];
+  }
+  if (T0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) S0[u] = aesdec(aesdec(bxor(K.F[0], D[u][0]), D[u][0], T), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S0[u] = K.G[0];
+  }
+  // Compress_Meow2 / Compress_Meow and the final round, as meow_ct
+  Blk S2b[U];
+  if (NC >= 3 && T2) {
+    if constexpr (NC >= 3) {
+#pragma unroll
+      for (int u = 0; u < U; u++) S2b[u] = aesdec(aesdec(S2[u], S3[u], T), K.M, T);
+    }
+  } else if (T3) {
+#pragma unroll
+    for (int u = 0; u < U; u++) S2b[u] = aesdec(bxor(K.TG2, S3[u]), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) S2b[u] = K.CS2b;
+  }
+  if (T0) {
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = aesdec(aesdec(aesdec(S0[u], S1[u], T), S2b[u], T), K.M, T);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = aesdec(bxor(K.TCS0a, S2b[u]), K.M, T);
+  }
+}
+
+template <int NC, int NT, int U>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_rt(const uint8_t* __restrict__ keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2,
+           uint64_t* __restrict__ out, uint32_t flags) {
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
+  const uint64_t last = n - 1, total = n * (uint64_t)L;
+  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
+    const bool exact = (b + 64 * U) * (uint64_t)L + 32 > total;  // this chunk reaches the batch's end
+    Blk D[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      const uint8_t* p = keys + (j < last ? j : last) * (uint64_t)L;
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        const int left = (int)L - 16 * c;
+        const uint32_t nv = left >= 16 ? 16u : (uint32_t)left;
+        if (exact) {
+          D[u][c] = load_bytes(p + 16 * c, nv);
+        } else {
+          D[u][c] = load16_full(p + 16 * c);
+          if (c == NC - 1 && nv < 16) {
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+              const int keep = (int)nv - 4 * w;
+              D[u][c].w[w] &= keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+            }
+          }
+        }
+      }
+    }
+    Blk h[U];
+    meow_small<NC, U>(D, L, K, T, h);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      store_h<true>(out, j < last ? j : last, h[u], fix);
+    }
+  }
+}
+
+template <int NC, int NT, int U>
+int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2, uint64_t* out,
+                    uint32_t flags, hipStream_t st, int cus) {
+  const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
+  hipLaunchKernelGGL((k_fixed_rt<NC, NT, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, L, s1, s2, out, flags);
+  return launch_done();
+}
+
+// Default (NT, U) per length from tools/tune.py and tools/len_sweep.py
+// sweeps; knobs 0 and 3 select the others.
+template <int L>
+int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
+                    uint32_t flags, hipStream_t st, int cus) {
+  if (int rc = 0; g_exp.fixed && g_exp.fixed(L, keys, n, s1, s2, out, flags, st, cus, knob(g_tune_nt), knob(g_tune_kpl), &rc))
+    return rc;
+  if constexpr (L == 16 || L == 32) {
+    // per-length defaults from tools/tune.py: Td0..Td3 in LDS
+    // (no rotations), 4 keys per lane at 16 B, 2 at 32 B
+    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
+    const int nt = tnt ? tnt : 4;
+    const int kpl = tkpl ? tkpl : (L == 16 ? 4 : 2);
+    switch (nt * 100 + kpl) {
+      case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
+      case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
+      case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
+      case 408: return launch_k<L, 4, 8>(keys, n, s1, s2, out, flags, st, cus);
+      case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
+      case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
+      case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
+      case 208: return launch_k<L, 2, 8>(keys, n, s1, s2, out, flags, st, cus);
+      default: return set_err(KVH_EINVAL);
+    }
+  } else {
+    // per-length defaults (NT, keys per lane) from tools/len_sweep.py over
+    // 100M keys (profiles/r03/len_sweep_*.jsonl): 24 B NT4/U4, 40-48 B
+    // NT4/U1, 56-64 B NT4/U2; 8 B (unmeasured) NT2/U4
+    constexpr int dnt = L == 8 ? 2 : 4, dkpl = L == 8 || L == 24 ? 4 : (L == 40 || L == 48) ? 1 : 2;
+    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
+    switch ((tnt ? tnt : dnt) * 100 + (tkpl ? tkpl : dkpl)) {
+      case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
+      case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
+      case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
+      case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
+      case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
+      case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
+      case 403: if constexpr (L >= 40) return launch_k<L, 4, 3>(keys, n, s1, s2, out, flags, st, cus); break;
+      case 203: if constexpr (L >= 40) return launch_k<L, 2, 3>(keys, n, s1, s2, out, flags, st, cus); break;
+      default: break;
+    }
+    return set_err(KVH_EINVAL);
+  }
+}
+
+template <int L, int NT, int U>
+int launch_lanes_v(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
+                   uint32_t flags, hipStream_t st, int cus) {
+  const uint32_t grid = grid_for(n * arity, cus, NT == 4 ? 1 : 2);
+#define KVH_LANES_V(LAv)                                                                                \
+  hipLaunchKernelGGL((k_fixed_lanes<L, NT, true, U, LAv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \
+                     s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13],   \
+                     s[14], s[15])
+  if (arity == 2) KVH_LANES_V(2); else if (arity == 4) KVH_LANES_V(4); else KVH_LANES_V(8);
+#undef KVH_LANES_V
+  return launch_done();
+}
+
+template <int L>
+int launch_lanes_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
+                   uint32_t flags, hipStream_t st, int cus) {
+  const bool a16 = ((uintptr_t)keys & 15) == 0;
+  if constexpr (L == 32) {
+    // C3's length: Td0..Td3 in LDS (no rotates, one 16-wave workgroup per CU)
+    // and 2 keys per lane by default -- 118 vs 112 G hash/s for Td0/Td1 with
+    // two workgroups per CU (tools/tune.py, profiles/r02/c3_layout_ab.txt);
+    // knobs 0 / 3 select the others
+    const int nt = knob(g_tune_nt), kpl = knob(g_tune_kpl);
+    if (a16) {
+      switch ((nt ? nt : 4) * 10 + (kpl ? kpl : 2)) {
+        case 22: break;
+        case 21: return launch_lanes_v<L, 2, 1>(keys, n, s, arity, out, flags, st, cus);
+        case 24: return launch_lanes_v<L, 2, 4>(keys, n, s, arity, out, flags, st, cus);
+        case 41: return launch_lanes_v<L, 4, 1>(keys, n, s, arity, out, flags, st, cus);
+        case 42: return launch_lanes_v<L, 4, 2>(keys, n, s, arity, out, flags, st, cus);
+        case 44: return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);
+        default: return set_err(KVH_EINVAL);
+      }
+    }
+  }
+  const uint32_t grid = grid_for(n * arity, cus, 2);
+#define KVH_LANES(A16v, LAv)                                                                            \
+  hipLaunchKernelGGL((k_fixed_lanes<L, 2, A16v, 2, LAv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \
+                     s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13],   \
+                     s[14], s[15])
+  if (a16) {
+    if (arity == 2) KVH_LANES(true, 2); else if (arity == 4) KVH_LANES(true, 4); else KVH_LANES(true, 8);
+  } else {
+    if (arity == 2) KVH_LANES(false, 2); else if (arity == 4) KVH_LANES(false, 4); else KVH_LANES(false, 8);
+  }
+#undef KVH_LANES
+  return launch_done();
+}
+
+template <int L>
+int launch_ms_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
+                uint32_t flags, hipStream_t st, int cus) {
+  const bool a16 = ((uintptr_t)keys & 15) == 0;
+  const uint32_t grid = grid_for(n, cus, 1);
+  if (a16)
+    hipLaunchKernelGGL((k_fixed_ms<L, 4, true>), dim3(grid), dim3(kBlock), 0, st, keys, n, nullptr, out,
+                       flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10],
+                       s[11], s[12], s[13], s[14], s[15]);
+  else
+    hipLaunchKernelGGL((k_fixed_ms<L, 4, false>), dim3(grid), dim3(kBlock), 0, st, keys, n, nullptr, out,
+                       flags, arity, s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10],
+                       s[11], s[12], s[13], s[14], s[15]);
+  return launch_done();
+}
+
+}  // namespace
+
+namespace kvh {
+namespace rt {
+
+int fixed_dispatch(const uint8_t* k, uint32_t key_len, uint64_t n, uint64_t seed1, uint64_t seed2, uint64_t* out,
+                   uint32_t flags, hipStream_t st, int cus) {
+  const bool a8 = ((uintptr_t)k & 7) == 0;
+  if (!knob(g_tune_generic) && a8) {
+    switch (key_len) {
+      case 8: return launch_fixed_nt<8>(k, n, seed1, seed2, out, flags, st, cus);
+      case 16: return launch_fixed_nt<16>(k, n, seed1, seed2, out, flags, st, cus);
+      case 24: return launch_fixed_nt<24>(k, n, seed1, seed2, out, flags, st, cus);
+      case 32: return launch_fixed_nt<32>(k, n, seed1, seed2, out, flags, st, cus);
+      case 40: return launch_fixed_nt<40>(k, n, seed1, seed2, out, flags, st, cus);
+      case 48: return launch_fixed_nt<48>(k, n, seed1, seed2, out, flags, st, cus);
+      case 56: return launch_fixed_nt<56>(k, n, seed1, seed2, out, flags, st, cus);
+      case 64: return launch_fixed_nt<64>(k, n, seed1, seed2, out, flags, st, cus);
+      default: break;
+    }
+  }
+  if (!knob(g_tune_generic) && key_len >= 1 && key_len < 64) {  // any other length below one block
+    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
+    const int nc = (int)(key_len + 15) / 16, nt = tnt ? tnt : 4, kpl = tkpl ? tkpl : (nc == 1 ? 4 : 2);
+    switch (nc * 1000 + nt * 10 + kpl) {
+#define KVH_RT(NCv, NTv, Uv) \
+  case NCv * 1000 + NTv * 10 + Uv: return launch_fixed_rt<NCv, NTv, Uv>(k, n, key_len, seed1, seed2, out, flags, st, cus);
+      KVH_RT(1, 4, 4) KVH_RT(1, 4, 2) KVH_RT(1, 4, 8) KVH_RT(1, 2, 4) KVH_RT(1, 2, 8)
+      KVH_RT(2, 4, 2) KVH_RT(2, 4, 4) KVH_RT(2, 2, 2) KVH_RT(2, 2, 4)
+      KVH_RT(3, 4, 2) KVH_RT(3, 4, 4) KVH_RT(3, 2, 2) KVH_RT(3, 2, 4)
+      KVH_RT(4, 4, 2) KVH_RT(4, 4, 4) KVH_RT(4, 2, 2) KVH_RT(4, 2, 4)
+#undef KVH_RT
+      default: break;  // a knob pair without an instance: the generic kernel
+    }
+  }
+  uint64_t s[16] = {seed1, seed2};
+  return generic_launch(false, k, nullptr, key_len, n, s, 1, out, flags, st, cus);
+}
+
+int multiseed_dispatch(const uint8_t* k, uint32_t key_len, uint64_t n, const uint64_t* s, uint32_t arity,
+                       uint64_t* out, uint32_t flags, hipStream_t st, int cus) {
+  const bool a8 = ((uintptr_t)k & 7) == 0;
+  if (!knob(g_tune_generic) && a8 && knob(g_tune_ms_lanes) && (arity == 2 || arity == 4 || arity == 8)) {
+    switch (key_len) {
+      case 8: return launch_lanes_L<8>(k, n, s, arity, out, flags, st, cus);
+      case 16: return launch_lanes_L<16>(k, n, s, arity, out, flags, st, cus);
+      case 24: return launch_lanes_L<24>(k, n, s, arity, out, flags, st, cus);
+      case 32: return launch_lanes_L<32>(k, n, s, arity, out, flags, st, cus);
+      case 40: return launch_lanes_L<40>(k, n, s, arity, out, flags, st, cus);
+      case 48: return launch_lanes_L<48>(k, n, s, arity, out, flags, st, cus);
+      case 56: return launch_lanes_L<56>(k, n, s, arity, out, flags, st, cus);
+      case 64: return launch_lanes_L<64>(k, n, s, arity, out, flags, st, cus);
+      default: break;
+    }
+  }
+  if (!knob(g_tune_generic) && a8) {
+    switch (key_len) {
+      case 16: return launch_ms_L<16>(k, n, s, arity, out, flags, st, cus);
+      case 32: return launch_ms_L<32>(k, n, s, arity, out, flags, st, cus);
+      case 64: return launch_ms_L<64>(k, n, s, arity, out, flags, st, cus);
+      default: break;
+    }
+  }
+  return generic_launch(false, k, nullptr, key_len, n, s, arity, out, flags, st, cus);
+}
+
+}  // namespace rt
+}  // namespace kvh

@@ -209,6 +209,32 @@ extern std::atomic<int> g_tune_spans;
 // tokenizer: 1 = wave-chunked (default), 0 = workgroup-chunked
 extern std::atomic<int> g_tune_tok;
 
+// The kernel-selection knobs (defined in kvh.hip, read by kvh_fixed.hip and
+// kvh_varlen.hip; kvh_set_tuning sets them): NT, workgroups per CU, force
+// the generic kernel, keys per lane, multi-seed lanes per key,
+// variable-length kernel.
+extern std::atomic<int> g_tune_nt, g_tune_wgmul, g_tune_generic, g_tune_kpl, g_tune_ms_lanes, g_tune_var;
+inline int knob(const std::atomic<int>& k) { return k.load(std::memory_order_relaxed); }
+// workgroups of kBlock threads for n items: wg_per_cu per CU (times knob 1), at most one per kBlock items
+inline uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
+  const uint64_t need = (n + kBlock - 1) / kBlock;
+  const int m = wg_per_cu * knob(g_tune_wgmul);
+  uint64_t g = (uint64_t)cus * (uint64_t)(m > 1 ? m : 1);
+  if (need < g) g = need;
+  return (uint32_t)(g > 1 ? g : 1);
+}
+// the kernels of kvh_fixed.hip / kvh_varlen.hip behind the C-ABI entry points
+// (arguments already checked; n > 0): everything kvh_meow128_fixed,
+// kvh_meow128_multiseed (s = 8 seed pairs, arity 2..8) and kvh_meow128_var launch
+int fixed_dispatch(const uint8_t* k, uint32_t key_len, uint64_t n, uint64_t seed1, uint64_t seed2, uint64_t* out,
+                   uint32_t flags, hipStream_t st, int cus);
+int multiseed_dispatch(const uint8_t* k, uint32_t key_len, uint64_t n, const uint64_t* s, uint32_t arity,
+                       uint64_t* out, uint32_t flags, hipStream_t st, int cus);
+int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_t seed1, uint64_t seed2,
+                 uint64_t* out, uint32_t flags, hipStream_t st, int cus);
+int generic_launch(bool var, const uint8_t* keys, const uint64_t* offs, uint32_t fixed_len, uint64_t n,
+                   const uint64_t* s, uint32_t arity, uint64_t* out, uint32_t flags, hipStream_t st, int cus);
+
 // Research-build hook table.  libkvh.so leaves it empty.  The experiments
 // library (`make experiments` -> tools/libkvh_exp.so: these objects plus
 // tools/exp/*.o) fills it from a static initialiser, so the research kernels

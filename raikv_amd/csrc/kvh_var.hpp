@@ -75,6 +75,16 @@ __device__ __forceinline__ void wave_sync() {
 struct VConst9 {  // VConst minus CS2b (meow_a never needs it), padded to 13 blocks:
   Blk F[4], G[4], TG2, TCS0a, pad;  // a 52-dword stride puts the 16 lengths of a class on distinct banks
 };
+// Block index of first-absorb fold F[i] of length L (kLT <= L) in the k_var9
+// fold table: 4 blocks per length, the block order XOR-swizzled by bits 2-3
+// of L - kLT, so that 16 consecutive lengths (a 16-byte class of long keys)
+// read any one F[i] from 16 distinct 16-byte bank slots (ds_read_b128: 16
+// lanes per LDS cycle over a 256-byte bank row); unswizzled, lengths 4
+// apart share a slot (4-way conflicts in a chunk of long keys).
+__device__ __forceinline__ uint32_t kf_index(uint32_t L, int i) {
+  const uint32_t r = L - (uint32_t)kLT;
+  return (r << 2) + ((uint32_t)i ^ ((r >> 2) & 3u));
+}
 template <class Tab, int NF>
 struct LdsKV9 {
   const VConst9* full;
@@ -89,11 +99,13 @@ struct LdsKV9 {
   __device__ __forceinline__ Blk M() const { return m; }
   __device__ __forceinline__ Blk F(int i) const {
     if (L < (uint32_t)kLT) return full[L].F[i];
-    if (L < (uint32_t)(kLT + NF)) return ftab[(L - kLT) * 4 + i];
+    if (L < (uint32_t)(kLT + NF)) return ftab[kf_index(L, i)];
     return aesT(bxor(ramp(i), m), T);
   }
-  // F of a key shorter than kLT, read branch-free (unused lanes read any record)
-  __device__ __forceinline__ Blk F0(int i) const { return full[L & (kLT - 1)].F[i]; }
+  // F of a key shorter than kLT, read branch-free; the lanes that do not use
+  // it (keys of kLT bytes or more) all read record 0: one broadcast address
+  // instead of scattered records that conflict with the short keys' reads
+  __device__ __forceinline__ Blk F0(int i) const { return full[L < (uint32_t)kLT ? L : 0u].F[i]; }
   __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
   __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
   __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }

@@ -251,65 +251,6 @@ __device__ __forceinline__ Blk meow_ct(const Blk* D, const MeowConst& K, const T
   return aesdec(S0b, K.M, T);
 }
 
-// meow_ct split at the last serial stretch, for software pipelining across
-// chunks (k_fixed_pl): HEAD = absorb, Mix and the first Compress rounds,
-// whose chains run side by side (4, then 4, then 2 independent rounds for a
-// 64-byte key); TAIL = S2b = AESDEC(X, M), S0b = AESDEC(Y, S2b), AESDEC(S0b,
-// M): three rounds in series.  X = AESDEC(S2, S3) (T2) or TG2 ^ S3 (T3);
-// Y = AESDEC(S0, S1) (T0).  meow_tail(meow_head(D)) == meow_ct(D).
-template <int L, class Tab>
-__device__ __forceinline__ void meow_head(const Blk* D, const MeowConst& K, const Tab& T, Blk& X, Blk& Y) {
-  using P = Plan<L>;
-  Blk S0, S1, S2, S3;
-#pragma unroll
-  for (int b = 0; b < P::NB; b++) {
-    const Blk& k0 = D[4 * b + 0]; const Blk& k1 = D[4 * b + 1];
-    const Blk& k2 = D[4 * b + 2]; const Blk& k3 = D[4 * b + 3];
-    if (b == 0) {
-      S0 = aesdec(bxor(K.F[0], k0), k0, T); S1 = aesdec(bxor(K.F[1], k1), k1, T);
-      S2 = aesdec(bxor(K.F[2], k2), k2, T); S3 = aesdec(bxor(K.F[3], k3), k3, T);
-    } else {
-      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
-      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
-    }
-  }
-  constexpr bool first = P::NB == 0;
-  constexpr int base = 4 * P::NB;
-  if constexpr (P::T != 0) {
-    const Blk& k = D[base + P::C / 16];
-    S3 = first ? aesdec(bxor(K.F[3], k), k, T) : aesdec(aesdec(S3, k, T), k, T);
-  }
-  if constexpr (P::C >= 48) {
-    const Blk& k = D[base + 2];
-    S2 = first ? aesdec(bxor(K.F[2], k), k, T) : aesdec(aesdec(S2, k, T), k, T);
-  }
-  if constexpr (P::C >= 32) {
-    const Blk& k = D[base + 1];
-    S1 = first ? aesdec(bxor(K.F[1], k), k, T) : aesdec(aesdec(S1, k, T), k, T);
-  }
-  if constexpr (P::C >= 16) {
-    const Blk& k = D[base + 0];
-    S0 = first ? aesdec(bxor(K.F[0], k), k, T) : aesdec(aesdec(S0, k, T), k, T);
-  }
-  if constexpr (P::T3) S3 = aesdec(S3, K.M, T); else S3 = K.G[3];
-  if constexpr (P::T2) S2 = aesdec(S2, K.M, T); else S2 = K.G[2];
-  if constexpr (P::T1) S1 = aesdec(S1, K.M, T); else S1 = K.G[1];
-  if constexpr (P::T0) S0 = aesdec(S0, K.M, T); else S0 = K.G[0];
-  if constexpr (P::T2) X = aesdec(S2, S3, T);
-  else if constexpr (P::T3) X = bxor(K.TG2, S3);
-  else X = bzero();
-  if constexpr (P::T0) Y = aesdec(S0, S1, T); else Y = bzero();
-}
-template <int L, class Tab>
-__device__ __forceinline__ Blk meow_tail(const Blk& X, const Blk& Y, const MeowConst& K, const Tab& T) {
-  using P = Plan<L>;
-  Blk S2b;
-  if constexpr (P::T2 || P::T3) S2b = aesdec(X, K.M, T); else S2b = K.CS2b;
-  Blk S0b;
-  if constexpr (P::T0) S0b = aesdec(Y, S2b, T); else S0b = bxor(K.TCS0a, S2b);
-  return aesdec(S0b, K.M, T);
-}
-
 // ---------------------------------------------------- runtime lengths
 // bytes [p, p+n), 0 <= n <= 16, zero padded; reads only the dwords that
 // intersect [p, p+n), so it never touches memory past the key's last byte's
@@ -658,25 +599,54 @@ __device__ __forceinline__ Blk absorb2(const Blk& s, const Blk& k, const Tab& T)
 
 struct MeowState { Blk S[4]; };
 
-template <class Tab>
-__device__ __forceinline__ void absorb_blocks(MeowState& st, const uint8_t* p, uint64_t nblk, const Tab& T) {
+// key-byte source of the literal path: global memory (bytes at or past the
+// key's last dword never read), or an LDS copy (LdsBytes)
+struct GlobalBytes {
+  __device__ __forceinline__ Blk part(const uint8_t* p, uint32_t n) const { return load_bytes(p, n); }
+};
+// bytes [p, p+n) of an LDS buffer, zero padded: the five dwords around them
+// (the buffer must hold 20 readable bytes from the dword at or below p),
+// funnel-shifted and masked
+struct LdsBytes {
+  __device__ __forceinline__ Blk part(const uint8_t* p, uint32_t n) const {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t* q = (const uint32_t*)(p - (a & 3));
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) d[j] = q[j];
+    Blk r;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t v = __builtin_amdgcn_alignbyte(d[c + 1], d[c], sh);
+      const int keep = (int)n - 4 * c;
+      r.w[c] = v & (keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u));
+    }
+    return r;
+  }
+};
+
+template <class Tab, class Ld = GlobalBytes>
+__device__ __forceinline__ void absorb_blocks(MeowState& st, const uint8_t* p, uint64_t nblk, const Tab& T,
+                                              const Ld& ld = Ld{}) {
   for (uint64_t b = 0; b < nblk; b++, p += 64) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) st.S[i] = absorb2(st.S[i], load_bytes(p + 16 * i, 16), T);
+    for (int i = 0; i < 4; i++) st.S[i] = absorb2(st.S[i], ld.part(p + 16 * i, 16), T);
   }
 }
 
 // Meow_Loop with `sz` selecting the trail (key_hash.c:1212-1226)
-template <class Tab>
-__device__ __forceinline__ void absorb_loop(MeowState& st, const uint8_t* p, uint64_t sz, const Tab& T) {
+template <class Tab, class Ld = GlobalBytes>
+__device__ __forceinline__ void absorb_loop(MeowState& st, const uint8_t* p, uint64_t sz, const Tab& T,
+                                            const Ld& ld = Ld{}) {
   const uint64_t nblk = sz >> 6;
-  absorb_blocks(st, p, nblk, T);
+  absorb_blocks(st, p, nblk, T, ld);
   p += 64 * nblk;
   const uint32_t t = (uint32_t)sz & 15, C = (uint32_t)sz & 48;
-  if (t) st.S[3] = absorb2(st.S[3], load_bytes(p + C, t), T);
-  if (C >= 48) st.S[2] = absorb2(st.S[2], load_bytes(p + 32, 16), T);
-  if (C >= 32) st.S[1] = absorb2(st.S[1], load_bytes(p + 16, 16), T);
-  if (C >= 16) st.S[0] = absorb2(st.S[0], load_bytes(p, 16), T);
+  if (t) st.S[3] = absorb2(st.S[3], ld.part(p + C, t), T);
+  if (C >= 48) st.S[2] = absorb2(st.S[2], ld.part(p + 32, 16), T);
+  if (C >= 32) st.S[1] = absorb2(st.S[1], ld.part(p + 16, 16), T);
+  if (C >= 16) st.S[0] = absorb2(st.S[0], ld.part(p, 16), T);
 }
 
 template <class Tab>
@@ -695,12 +665,13 @@ __device__ __forceinline__ void state_init(MeowState& st, const Blk& M) {
   for (int i = 0; i < 4; i++) st.S[i] = bxor(ramp(i), M);
 }
 
-template <class Tab>
-__device__ __forceinline__ Blk meow_literal(const uint8_t* p, uint64_t sz, uint64_t s1, uint64_t s2, const Tab& T) {
+template <class Tab, class Ld = GlobalBytes>
+__device__ __forceinline__ Blk meow_literal(const uint8_t* p, uint64_t sz, uint64_t s1, uint64_t s2, const Tab& T,
+                                            const Ld& ld = Ld{}) {
   MeowState st;
   const Blk M = mixer(s1, s2, sz);
   state_init(st, M);
-  absorb_loop(st, p, sz, T);
+  absorb_loop(st, p, sz, T, ld);
   return finish(st, M, T);
 }
 

@@ -17,7 +17,7 @@
 //                src/key_hash.c, dlopen'ed as the timed CPU baseline only)
 // Outputs of every host-pipeline call size are compared word for word with
 // the device-resident kernel before timing.  One JSON line per size.
-//   usage: host_latency [key_len=16, 0 = zipf 8-256 B] [pinned|pageable] [sizes]
+//   usage: host_latency [key_len=16, 0 = zipf 8-256 B] [pinned|pageable] [sizes] [tiny-path limit, knob 21]
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 #include <math.h>
@@ -90,6 +90,8 @@ int main(int argc, char** argv) {
     }
   }
   const bool var = L == 0;
+  const int tiny = argc > 4 ? atoi(argv[4]) : -1;
+  if (tiny >= 0 && kvh_set_tuning(21, tiny) < 0) return fail("knob 21");
   const size_t nmax = *std::max_element(sizes.begin(), sizes.end());
   const uint64_t s1 = 0xa8e0bcc94d1855f5ull, s2 = 0xad3bec1e8de4a1a3ull;
   uint64_t x = 0x9E3779B97F4A7C15ull;
@@ -174,10 +176,10 @@ int main(int argc, char** argv) {
     printf("{\"n\": %zu, \"key_len\": %s, \"host_mem\": \"%s\", \"host_pipe_us\": %.2f, \"host_pipe_p10_us\": %.2f, "
            "\"host_pipe_p90_us\": %.2f, \"host_pipe_hash_per_s\": %.4g, \"device_call_us\": %.2f, "
            "\"copy_roundtrip_us\": %.2f, \"ref_cpu_1t_us\": %.2f, \"ref_cpu_1t_hash_per_s\": %.4g, "
-           "\"gpu_faster_than_1_cpu_thread\": %s, \"reps\": %d}\n",
+           "\"gpu_faster_than_1_cpu_thread\": %s, \"tiny_limit\": %d, \"reps\": %d}\n",
            n, var ? "\"zipf 8-256\"" : std::to_string(L).c_str(), pageable ? "pageable" : "pinned", h.med * 1e6,
            h.p10 * 1e6, h.p90 * 1e6, n / h.med, d.med * 1e6, c.med * 1e6, cpu1 * 1e6, cpu1 > 0 ? n / cpu1 : -1.0,
-           cpu1 > 0 && h.med < cpu1 ? "true" : "false", reps);
+           cpu1 > 0 && h.med < cpu1 ? "true" : "false", tiny, reps);
     fflush(stdout);
   }
   return 0;

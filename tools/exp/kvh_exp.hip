@@ -923,7 +923,7 @@ k_var9x(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uin
     if (l >= (uint32_t)kLT) {
       const Blk Mx = mixer(s1, s2, l);
 #pragma unroll
-      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), Mx), T);
+      for (int q = 0; q < 4; q++) kf[kf_index(l, q)] = aesT(bxor(ramp(q), Mx), T);
       continue;
     }
     const MeowConst k = make_const(s1, s2, l, T);
@@ -1108,7 +1108,7 @@ k_var10(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uin
     if (l >= (uint32_t)kLT) {
       const Blk Mx = mixer(s1, s2, l);
 #pragma unroll
-      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), Mx), T);
+      for (int q = 0; q < 4; q++) kf[kf_index(l, q)] = aesT(bxor(ramp(q), Mx), T);
       continue;
     }
     const MeowConst kc = make_const(s1, s2, l, T);
@@ -1447,7 +1447,7 @@ k_var8(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     if (l >= (uint32_t)kLT) {
       const Blk Mx = mixer(s1, s2, l);
 #pragma unroll
-      for (int q = 0; q < 4; q++) kf[(l - kLT) * 4 + q] = aesT(bxor(ramp(q), Mx), T);
+      for (int q = 0; q < 4; q++) kf[kf_index(l, q)] = aesT(bxor(ramp(q), Mx), T);
       continue;
     }
     const MeowConst kc = make_const(s1, s2, l, T);
@@ -1948,15 +1948,7 @@ Knob g_tune_ablate{0};    // ablation build of k_fixed (0 = product path)
 Knob g_tune_dma{0};       // LDS-DMA ring depth for L in {16, 32} (0 = register path)
 Knob g_tune_var_mode{0};  // ablation of k_var3: 1 no-hash, 2 no-gather, 3 no-sort
 
-Knob g_tune_wgmul_x{1};
-inline int knob(const Knob& k) { return k.load(std::memory_order_relaxed); }
-
-uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {
-  const uint64_t need = (n + kBlock - 1) / kBlock;
-  uint64_t g = (uint64_t)cus * (uint64_t)std::max(1, wg_per_cu);
-  if (need < g) g = need;
-  return (uint32_t)std::max<uint64_t>(g, 1);
-}
+// knob() and grid_for() are the product's (kvh_internal.hpp)
 
 template <int L, int NT, int U, int MODE = 0, bool PF = false>
 int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,

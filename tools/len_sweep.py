@@ -7,7 +7,8 @@
 n        keys per length (default 100M, the C1 batch size)
 lens     comma list (default 16,24,32,48,64)
 variants comma list of NT*10+U kernel shapes to A/B (e.g. 24,22,44,42;
-         a trailing p = the software-pipelined k_fixed_pl, knob 22), or
+         the round-3 sweeps also had a trailing p for a software-pipelined kernel,
+         removed after it measured within 1 %), or
          "default" (the shipped choice only)
 
 Per length: 500 ms settle (the post-idle power transient),
@@ -41,10 +42,7 @@ lib = kvh.lib
 
 
 def setv(v):
-    """'default', or NT*10+U with an optional 'p' (knob 22: the software-pipelined kernel)"""
-    pl = v.endswith("p")
-    lib.kvh_set_tuning(22, 1 if pl else 0)
-    v = v[:-1] if pl else v
+    """'default', or NT*10+U"""
     if v == "default":
         lib.kvh_set_tuning(0, 0)
         lib.kvh_set_tuning(3, 0)
