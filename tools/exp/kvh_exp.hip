@@ -13,11 +13,14 @@
 //   k_var, k_var3, k_var5, k_var7, k_var8  variable-length experiments
 //   k_var6x     k_var6 with next-chunk prefetches (knob 7 = 9, 10, 20, 22)
 //   k_var9x     k_var9 with long keys two lanes per key (knob 7 = 26, 27)
+//   k_var11, k_var11_q, k_var12  long keys deferred to class-uniform queues
+//               (knob 7 = 40-43, round 3): fewer LDS instructions, slower
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 #include <atomic>
 #include <algorithm>
+#include <mutex>
 #include "../../raikv_amd/csrc/meow_dev.hpp"
 #include "../../raikv_amd/csrc/bs_prelude.hpp"
 #include "../../raikv_amd/csrc/kvh_internal.hpp"
@@ -1964,6 +1967,681 @@ int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t
   return launch_done();
 }
 
+// ---------------------------------------------------------------------
+// k_var11 + k_var11_q: k_var9 with the divergence of its sorted chunks cut
+// by DEFERRAL.  A chunk of 64 class-sorted keys runs as long as its longest
+// key, and in a 256-key window the 4th chunk holds the ~61 keys of 64 B or
+// more (24 % of C2's keys, lengths 64..256): it costs the longest key's
+// rounds for all of them.  A divergence model over the C2 lengths
+//  gives 16.3 lane-rounds per key for k_var9 against 10.2
+// ideal; with the keys of 64..319 B, and each window's remainder chunk of at
+// most REM short keys, sent to per-class queues and hashed there in
+// class-uniform chunks (every lane of a chunk has the same block count and
+// trail shape), 11.9.
+//  * k_var11 (windows): a wave pushes its window's long keys to ITS OWN
+//    queue region (no global atomics: one region per wave of the grid),
+//    counting-sorts the rest by class as k_var9 does, pushes the partial last
+//    chunk (<= REM keys) too, and hashes only full chunks.  A region is a
+//    bump-allocated array of 64-record blocks; each class has one open block
+//    whose (block, fill) lives in lane `class` of one VGPR.  A record is
+//    16 B {offset lo, offset hi, length, index}.  A key whose push finds the
+//    region full is hashed in the window as before.  The window's hash run
+//    is stored whole (deferred slots carry stale stage words), so its stores
+//    stay full lines;
+//  * k_var11_q (queues): one wave per region, one block at a time, every
+//    lane of a block the same class, so the straight-line meow_a variant is
+//    exact for all of them; each hash overwrites its slot in `out`.
+// Reference semantics are unchanged (key_hash.c:1155-1226): both kernels
+// hash with meow_a and the same folded constants.
+constexpr int kQCls = 20;  // deferred classes 0..19 (keys of 0..319 bytes)
+
+struct VarQ {
+  uint4* rec;       // [regions][rb][64]: {offset lo, offset hi, length, index}
+  uint32_t* meta;   // [regions][rb]: class << 8 | count
+  uint32_t* nblk;   // [regions]: blocks used
+  uint32_t rb;      // blocks per region
+};
+
+// Window sort buckets: the short classes first, then the classes hashed in
+// the window whatever happens (keys of 320 B and more), then the deferrable
+// long classes 4..19 -- so the keys hashed in the window are one prefix of
+// the sorted order and the deferred ones one suffix.
+__device__ __forceinline__ uint32_t v11_bucket(uint32_t c) {
+  return c < 4u ? c : c >= (uint32_t)kQCls ? 4u + (c - kQCls < 27u ? c - kQCls : 27u) : 32u + (c - 4u);
+}
+
+template <int NT, int NW, int REM>
+__global__ void __launch_bounds__(NW * 64)
+k_var11(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+        uint64_t* __restrict__ out, uint32_t flags, VarQ q) {
+  constexpr int WIN = 256, M = WIN / 64, AREA = WIN * 16;
+  // no first-absorb fold table: keys of 64 B or more are hashed here only
+  // when their region is full (or they are 320 B and longer): folds in-lane
+  constexpr int kTabB = LdsTab<NT>::kWords * 4, kFullB = kLT * (int)sizeof(VConst9);
+  constexpr int kBytes = kTabB + kFullB + NW * AREA;
+  static_assert(kBytes <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint32_t smem[kBytes / 4];
+  uint32_t* lds = smem;
+  VConst9* kfull = (VConst9*)((uint8_t*)smem + kTabB);
+  uint8_t* wavemem = (uint8_t*)smem + kTabB + kFullB;
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) {
+    const MeowConst k = make_const(s1, s2, l, T);
+    VConst9 v;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { v.F[i] = k.F[i]; v.G[i] = k.G[i]; }
+    v.TG2 = k.TG2; v.TCS0a = k.TCS0a;
+    kfull[l] = v;
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Blk* stage = (Blk*)(wavemem + wv * AREA);
+  uint32_t* hist = (uint32_t*)stage;
+  uint2* rec = (uint2*)(wavemem + wv * AREA + WIN * 8);
+  const uint64_t nwin = (n + WIN - 1) / WIN;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
+  const uint64_t kend = offs[n];
+  uint4* const qrec = q.rec + gw * q.rb * 64;
+  uint32_t* const qmeta = q.meta + gw * q.rb;
+  // lane c < kQCls: class c's open block << 16 | its fill (64: none open)
+  uint32_t qs = 0xffffu << 16 | 64u, nb = 0;
+  for (uint64_t w = gw; w < nwin; w += tw) {
+    const uint64_t i0 = w * WIN;
+    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    const uint64_t ws = offs[i0];
+    const uint64_t wend = kend - ws;
+    uint32_t kk, d0;  // keys of the window; the sorted positions [d0, kk) go to the queues
+    {
+      uint32_t o[M], L[M], r[M], b[M];
+      bool wide = false;
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
+        o[m] = (uint32_t)(a - ws);
+        L[m] = (uint32_t)(e - a);
+        wide |= e - ws >= (1ull << 32) || e - a >= (1ull << 24);
+      }
+      if (__ballot(wide) != 0) {
+        wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds);
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) hist[lane * 4 + i] = 0;
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        b[m] = v11_bucket(L[m] >> 4) * 4u + (lane & 3u);
+        r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
+      }
+      wave_sync();
+      {
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) { v[i] = hist[lane * 4 + i]; sum += v[i]; }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(inc, d, 64);
+          if (lane >= (uint32_t)d) inc += y;
+        }
+        uint32_t run = inc - sum;
+#pragma unroll
+        for (int i = 0; i < 4; i++) { hist[lane * 4 + i] = run; run += v[i]; }
+        kk = __builtin_amdgcn_readlane(inc, 63);
+      }
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        if (j < k) rec[hist[b[m]] + r[m]] = make_uint2(o[m], (L[m] << 8) | j);
+      }
+      wave_sync();
+    }
+    // the split: long classes, plus the partial last chunk of short keys
+    // when it is small and holds no key that must stay
+    const uint32_t x = __builtin_amdgcn_readfirstlane(hist[32 * 4]);    // start of the deferrable buckets
+    const uint32_t xs = __builtin_amdgcn_readfirstlane(hist[4 * 4]);    // end of the short classes
+    const uint32_t rem = x & 63u;
+    d0 = rem != 0 && rem <= (uint32_t)REM && xs == x ? x - rem : x;
+    if (nb + kQCls + M > q.rb) d0 = kk;  // region nearly full: this window keeps its keys
+    if (d0 < kk) {
+      // per class c (lane c): its run [cb, ce) of the deferred suffix
+      uint32_t cb = 0, cnt = 0;
+      if (lane < (uint32_t)kQCls) {
+        const uint32_t bk = v11_bucket(lane);
+        const uint32_t s0 = hist[bk * 4], e0 = hist[bk * 4 + 4];
+        cb = s0 > d0 ? s0 : d0;
+        cnt = e0 > cb ? e0 - cb : 0u;
+      }
+      // block placement, one class at a time (wave-uniform): fill the open
+      // block, then consecutive new blocks from the region's bump pointer
+      uint32_t pl = 0, pb = 0;  // lane c: open block << 16 | fill before, first new block
+      uint64_t cm = __ballot(cnt != 0);
+      while (cm) {
+        const uint32_t c = (uint32_t)__builtin_ctzll(cm);
+        cm &= cm - 1;
+        const uint32_t cc = __builtin_amdgcn_readlane(cnt, c);
+        const uint32_t st = __builtin_amdgcn_readlane(qs, c);
+        const uint32_t blk = st >> 16, fill = st & 0xffffu;
+        const uint32_t n1 = cc < 64u - fill ? cc : 64u - fill;
+        const uint32_t nnew = (cc - n1 + 63u) >> 6, nbase = nb;
+        nb += nnew;
+        const uint32_t lastfill = nnew ? cc - n1 - 64u * (nnew - 1u) : fill + n1;
+        const uint32_t lastblk = nnew ? nbase + nnew - 1u : blk;
+        if (lane == 0 && n1 != 0 && fill + n1 == 64u) qmeta[blk] = c << 8 | 64u;
+        if (lane < nnew && (lane + 1u < nnew || lastfill == 64u)) qmeta[nbase + lane] = c << 8 | 64u;
+        if (lane == c) { pl = st; pb = nbase; qs = lastblk << 16 | lastfill; }
+      }
+      // records of the deferred suffix to their blocks (the shuffles run in
+      // every lane: ds_bpermute reads nothing from a lane that is off)
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        if (d0 + 64u * m >= kk) break;  // wave-uniform
+        const uint32_t p = d0 + lane + 64 * m;
+        const bool v = p < kk;
+        const uint2 rr = rec[v ? p : d0];
+        const uint32_t kl = rr.y >> 8, c = kl >> 4;
+        const uint32_t rank = p - (uint32_t)__shfl((int)cb, (int)c, 64);
+        const uint32_t st = (uint32_t)__shfl((int)pl, (int)c, 64), fill = st & 0xffffu;
+        const uint32_t nbc = (uint32_t)__shfl((int)pb, (int)c, 64);
+        uint32_t blk, pos;
+        if (rank < 64u - fill) { blk = st >> 16; pos = fill + rank; }
+        else {
+          const uint32_t r2 = rank - (64u - fill);
+          blk = nbc + (r2 >> 6);
+          pos = r2 & 63u;
+        }
+        const uint64_t off = ws + rr.x;
+        if (v) qrec[blk * 64 + pos] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), kl, (uint32_t)(i0 + (rr.y & 255u)));
+      }
+    }
+    wave_sync();
+    uint2 rc0 = rec[lane], rc1 = rec[64 + lane], rc2 = rec[128 + lane], rc3 = rec[192 + lane];
+    wave_sync();  // the stage takes hashes from here on
+    const uint8_t* base = keys + ws;
+    const uint32_t nch = (d0 + 63) >> 6;
+#pragma unroll 1
+    for (uint32_t c = 0; c < nch; c++) {
+      const uint32_t pos = 64 * c + lane;
+      const bool valid = pos < d0;
+      const uint2 rc = rc0;
+      rc0 = rc1; rc1 = rc2; rc2 = rc3;
+      const uint32_t kl = valid ? rc.y >> 8 : 0u;
+      const bool al = __ballot(kl >= 64u) != 0;
+      const int cm = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
+                   : __ballot((kl & 48u) >= 16u) ? 16 : 0;
+      if (valid) {
+        const uint8_t* p = base + rc.x;
+        const bool safe = (uint64_t)rc.x + kl + 16 <= wend;
+        const LdsKV9<LdsTab<NT>, 0> K(kfull, nullptr, kl, s1, s2, T);
+        Blk h;
+        if (al) h = meow_a<true, 48, false>(p, kl, safe, K, T);
+        else if (cm == 48) h = meow_a<false, 48, false>(p, kl, safe, K, T);
+        else if (cm == 32) h = meow_a<false, 32, false>(p, kl, safe, K, T);
+        else if (cm == 16) h = meow_a<false, 16, false>(p, kl, safe, K, T);
+        else h = meow_a<false, 0, false>(p, kl, safe, K, T);
+        stage[rc.y & 255u] = fix ? fixup(h) : h;
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t j = 64 * c + lane;
+      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
+    }
+    wave_sync();
+  }
+  // close the open blocks; the region's block count
+  if (lane < (uint32_t)kQCls) {
+    const uint32_t blk = qs >> 16, fill = qs & 0xffffu;
+    if (fill < 64u) qmeta[blk] = lane << 8 | fill;
+  }
+  if (lane == 0) q.nblk[gw] = nb;
+}
+
+// Per-length constants for k_var11_q: full records for L < kLT, the
+// swizzled first-absorb folds for kLT <= L < kLT + KF, in-lane beyond.  F0
+// (the folded first trail round of a key without a full block) is only
+// selected when nb == 0, which a chunk of a long class never has.
+template <class Tab, int KF>
+struct LdsKQ {
+  const VConst9* full;
+  const Blk* ftab;
+  uint32_t L;
+  Blk m;
+  const Tab& T;
+  __device__ __forceinline__ LdsKQ(const VConst9* f, const Blk* ft, uint32_t len, uint64_t s1, uint64_t s2,
+                                   const Tab& t)
+      : full(f), ftab(ft), L(len), m(mixer(s1, s2, len)), T(t) {}
+  __device__ __forceinline__ uint32_t li() const { return L < (uint32_t)kLT ? L : (uint32_t)kLT - 1; }
+  __device__ __forceinline__ Blk M() const { return m; }
+  __device__ __forceinline__ Blk F(int i) const {
+    if (L < (uint32_t)kLT) return full[L].F[i];
+    if (L < (uint32_t)(kLT + KF)) return ftab[kf_index(L, i)];
+    return aesT(bxor(ramp(i), m), T);
+  }
+  __device__ __forceinline__ Blk F0(int) const { return bzero(); }
+  __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
+  __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
+  __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }
+};
+
+template <int NT, int NW, bool PF>
+__global__ void __launch_bounds__(NW * 64)
+k_var11_q(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ kendp, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out,
+          uint32_t flags, VarQ q, uint64_t regions) {
+  constexpr int KF = 16 * kQCls - kLT;
+  constexpr int kTabB = LdsTab<NT>::kWords * 4, kFullB = kLT * (int)sizeof(VConst9), kKfB = KF * 64;
+  constexpr int kBytes = kTabB + kFullB + kKfB;
+  static_assert(kBytes <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint32_t smem[kBytes / 4];
+  uint32_t* lds = smem;
+  VConst9* kfull = (VConst9*)((uint8_t*)smem + kTabB);
+  Blk* kf = (Blk*)((uint8_t*)smem + kTabB + kFullB);
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + KF); l += blockDim.x) {
+    if (l >= (uint32_t)kLT) {
+      const Blk Mx = mixer(s1, s2, l);
+#pragma unroll
+      for (int i = 0; i < 4; i++) kf[kf_index(l, i)] = aesT(bxor(ramp(i), Mx), T);
+      continue;
+    }
+    const MeowConst k = make_const(s1, s2, l, T);
+    VConst9 v;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { v.F[i] = k.F[i]; v.G[i] = k.G[i]; }
+    v.TG2 = k.TG2; v.TCS0a = k.TCS0a;
+    kfull[l] = v;
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
+  const uint64_t kend = *kendp;  // offsets[n]: the buffer holds every byte up to the last key's end
+  for (uint64_t rg = gw; rg < regions; rg += tw) {
+    const uint32_t nb = q.nblk[rg];
+    const uint4* rb = q.rec + rg * q.rb * 64;
+    uint4 nx = nb ? rb[lane] : make_uint4(0, 0, 0, 0);  // next block's record, one block ahead
+#pragma unroll 1
+    for (uint32_t b = 0; b < nb; b++) {
+      const uint32_t meta = __builtin_amdgcn_readfirstlane(q.meta[rg * q.rb + b]);
+      const uint4 rc = nx;
+      if (b + 1 < nb) nx = rb[(b + 1) * 64 + lane];
+      const uint32_t c = meta >> 8, cnt = meta & 255u;
+      if (lane < cnt) {
+        const uint64_t off = (uint64_t)rc.y << 32 | rc.x;
+        const uint32_t kl = rc.z;
+        const uint8_t* p = keys + off;
+        const bool safe = off + kl + 16 <= kend;
+        const LdsKQ<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
+        Blk h;
+        switch (c & 3u | (c >= 4u ? 4u : 0u)) {  // class-uniform: the exact variant of every lane
+          case 0: h = meow_a<false, 0, false>(p, kl, safe, K, T); break;
+          case 1: h = meow_a<false, 16, false>(p, kl, safe, K, T); break;
+          case 2: h = meow_a<false, 32, false>(p, kl, safe, K, T); break;
+          case 3: h = meow_a<false, 48, false>(p, kl, safe, K, T); break;
+          case 4: h = meow_a<true, 0, PF>(p, kl, safe, K, T); break;
+          case 5: h = meow_a<true, 16, PF>(p, kl, safe, K, T); break;
+          case 6: h = meow_a<true, 32, PF>(p, kl, safe, K, T); break;
+          default: h = meow_a<true, 48, PF>(p, kl, safe, K, T); break;
+        }
+        store_h(out, rc.w, h, fix);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------
+// k_var12: k_var11's deferral in ONE kernel, each wave its own consumer.
+// k_var11 + k_var11_q cut the LDS instructions by 22 % and still lost (4.5
+// vs 3.0 ms): the queue kernel found the long keys' lines cold and had no
+// short-key work to hide the waits behind (53 % of its wave time waiting).
+// Here a wave hashes a class block as soon as it is full -- right after the
+// window that filled it, while those keys' lines are recent -- so every wave
+// keeps k_var9's mix of short-key chunks and (now class-uniform) long-key
+// chunks.  A wave's queue is 64 blocks of 64 records in its own slice of a
+// scratch buffer (<= 20 open blocks + <= 24 filled per window, so it never
+// runs out); free blocks are a 64-bit mask.  The window's hash run is stored
+// first (deferred slots carry stale stage words), then, after a fence, the
+// filled blocks overwrite their slots; at the end the open blocks are hashed.
+template <int NT, class K2, int KF>
+__device__ __forceinline__ void v12_block(const uint8_t* __restrict__ keys, uint64_t kend, const uint4* blk,
+                                          uint32_t c, uint32_t cnt, uint64_t s1, uint64_t s2,
+                                          uint64_t* __restrict__ out, bool fix, const VConst9* kfull,
+                                          const Blk* kf, const LdsTab<NT>& T) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (lane < cnt) {
+    const uint4 rc = blk[lane];
+    const uint64_t off = (uint64_t)rc.y << 32 | rc.x;
+    const uint32_t kl = rc.z;
+    const uint8_t* p = keys + off;
+    const bool safe = off + kl + 16 <= kend;
+    const LdsKQ<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
+    Blk h;
+    switch (c & 3u | (c >= 4u ? 4u : 0u)) {  // class-uniform: the exact variant of every lane
+      case 0: h = meow_a<false, 0, false>(p, kl, safe, K, T); break;
+      case 1: h = meow_a<false, 16, false>(p, kl, safe, K, T); break;
+      case 2: h = meow_a<false, 32, false>(p, kl, safe, K, T); break;
+      case 3: h = meow_a<false, 48, false>(p, kl, safe, K, T); break;
+      case 4: h = meow_a<true, 0, false>(p, kl, safe, K, T); break;
+      case 5: h = meow_a<true, 16, false>(p, kl, safe, K, T); break;
+      case 6: h = meow_a<true, 32, false>(p, kl, safe, K, T); break;
+      default: h = meow_a<true, 48, false>(p, kl, safe, K, T); break;
+    }
+    store_h(out, rc.w, h, fix);
+  }
+}
+
+template <int NT, int NW, int REM>
+__global__ void __launch_bounds__(NW * 64)
+k_var12(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
+        uint64_t* __restrict__ out, uint32_t flags, uint4* __restrict__ qbuf) {
+  constexpr int WIN = 256, M = WIN / 64, AREA = WIN * 16, QB = 64;  // blocks per wave
+  constexpr int KF = 16 * kQCls - kLT;
+  constexpr int kTabB = LdsTab<NT>::kWords * 4, kFullB = kLT * (int)sizeof(VConst9), kKfB = KF * 64;
+  constexpr int kBytes = kTabB + kFullB + kKfB + NW * AREA;
+  static_assert(kBytes <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint32_t smem[kBytes / 4];
+  uint32_t* lds = smem;
+  VConst9* kfull = (VConst9*)((uint8_t*)smem + kTabB);
+  Blk* kf = (Blk*)((uint8_t*)smem + kTabB + kFullB);
+  uint8_t* wavemem = (uint8_t*)smem + kTabB + kFullB + kKfB;
+  fill_tables<NT>(lds);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + KF); l += blockDim.x) {
+    if (l >= (uint32_t)kLT) {
+      const Blk Mx = mixer(s1, s2, l);
+#pragma unroll
+      for (int i = 0; i < 4; i++) kf[kf_index(l, i)] = aesT(bxor(ramp(i), Mx), T);
+      continue;
+    }
+    const MeowConst k = make_const(s1, s2, l, T);
+    VConst9 v;
+#pragma unroll
+    for (int i = 0; i < 4; i++) { v.F[i] = k.F[i]; v.G[i] = k.G[i]; }
+    v.TG2 = k.TG2; v.TCS0a = k.TCS0a;
+    kfull[l] = v;
+  }
+  __syncthreads();
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Blk* stage = (Blk*)(wavemem + wv * AREA);
+  uint32_t* hist = (uint32_t*)stage;
+  uint2* rec = (uint2*)(wavemem + wv * AREA + WIN * 8);
+  const uint64_t nwin = (n + WIN - 1) / WIN;
+  const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
+  const uint64_t kend = offs[n];
+  uint4* const qrec = qbuf + gw * QB * 64;
+  uint32_t qs = 0xffffu << 16 | 64u;  // lane c < kQCls: class c's open block << 16 | fill (64: none)
+  uint64_t freem = ~0ull;              // free blocks (wave-uniform)
+  for (uint64_t w = gw; w < nwin; w += tw) {
+    const uint64_t i0 = w * WIN;
+    const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
+    const uint64_t ws = offs[i0];
+    const uint64_t wend = kend - ws;
+    uint32_t kk, d0;
+    {
+      uint32_t o[M], L[M], r[M], b[M];
+      bool wide = false;
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        const uint64_t a = offs[i0 + (j < k ? j : k)], e = offs[i0 + (j < k ? j + 1 : k)];
+        o[m] = (uint32_t)(a - ws);
+        L[m] = (uint32_t)(e - a);
+        wide |= e - ws >= (1ull << 32) || e - a >= (1ull << 24);
+      }
+      if (__ballot(wide) != 0) {
+        wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds);
+        continue;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) hist[lane * 4 + i] = 0;
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        b[m] = v11_bucket(L[m] >> 4) * 4u + (lane & 3u);
+        r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
+      }
+      wave_sync();
+      {
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) { v[i] = hist[lane * 4 + i]; sum += v[i]; }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(inc, d, 64);
+          if (lane >= (uint32_t)d) inc += y;
+        }
+        uint32_t run = inc - sum;
+#pragma unroll
+        for (int i = 0; i < 4; i++) { hist[lane * 4 + i] = run; run += v[i]; }
+        kk = __builtin_amdgcn_readlane(inc, 63);
+      }
+      wave_sync();
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        if (j < k) rec[hist[b[m]] + r[m]] = make_uint2(o[m], (L[m] << 8) | j);
+      }
+      wave_sync();
+    }
+    const uint32_t x = __builtin_amdgcn_readfirstlane(hist[32 * 4]);
+    const uint32_t xs = __builtin_amdgcn_readfirstlane(hist[4 * 4]);
+    const uint32_t rem = x & 63u;
+    d0 = rem != 0 && rem <= (uint32_t)REM && xs == x ? x - rem : x;
+    uint32_t fb = 0, nfb = 0;  // lane i < nfb: class << 8 | block of the i-th block filled in this window
+    if (d0 < kk) {
+      uint32_t cb = 0, cnt = 0;
+      if (lane < (uint32_t)kQCls) {
+        const uint32_t bk = v11_bucket(lane);
+        const uint32_t s0 = hist[bk * 4], e0 = hist[bk * 4 + 4];
+        cb = s0 > d0 ? s0 : d0;
+        cnt = e0 > cb ? e0 - cb : 0u;
+      }
+      uint32_t pl = 0, pb = 0;  // lane c: open block << 16 | fill before; its new blocks, 8 bits each
+      uint64_t cm = __ballot(cnt != 0);
+      while (cm) {
+        const uint32_t c = (uint32_t)__builtin_ctzll(cm);
+        cm &= cm - 1;
+        const uint32_t cc = __builtin_amdgcn_readlane(cnt, c);
+        const uint32_t st = __builtin_amdgcn_readlane(qs, c);
+        const uint32_t blk = st >> 16, fill = st & 0xffffu;
+        const uint32_t n1 = cc < 64u - fill ? cc : 64u - fill;
+        const uint32_t nnew = (cc - n1 + 63u) >> 6;
+        uint32_t nbs = 0, last = blk;
+        if (n1 != 0 && fill + n1 == 64u) {  // the open block is full
+          if (lane == nfb) fb = c << 8 | blk;
+          nfb++;
+        }
+        for (uint32_t t = 0; t < nnew; t++) {
+          const uint32_t nbk = (uint32_t)__builtin_ctzll(freem);
+          freem &= freem - 1;
+          nbs |= nbk << (8 * t);
+          last = nbk;
+          if (t + 1 < nnew) {  // a full new block
+            if (lane == nfb) fb = c << 8 | nbk;
+            nfb++;
+          }
+        }
+        uint32_t lastfill = nnew ? cc - n1 - 64u * (nnew - 1u) : fill + n1;
+        if (nnew && lastfill == 64u) {
+          if (lane == nfb) fb = c << 8 | last;
+          nfb++;
+        }
+        if (lastfill == 64u) { last = 0xffffu; }  // nothing open
+        if (lane == c) { pl = st; pb = nbs; qs = last << 16 | lastfill; }
+      }
+#pragma unroll
+      for (int m = 0; m < M; m++) {
+        if (d0 + 64u * m >= kk) break;  // wave-uniform
+        const uint32_t p = d0 + lane + 64 * m;
+        const bool v = p < kk;
+        const uint2 rr = rec[v ? p : d0];
+        const uint32_t kl = rr.y >> 8, c = kl >> 4;
+        const uint32_t rank = p - (uint32_t)__shfl((int)cb, (int)c, 64);
+        const uint32_t st = (uint32_t)__shfl((int)pl, (int)c, 64), fill = st & 0xffffu;
+        const uint32_t nbc = (uint32_t)__shfl((int)pb, (int)c, 64);
+        uint32_t blk, pos;
+        if (rank < 64u - fill) { blk = st >> 16; pos = fill + rank; }
+        else {
+          const uint32_t r2 = rank - (64u - fill);
+          blk = (nbc >> (8 * (r2 >> 6))) & 255u;
+          pos = r2 & 63u;
+        }
+        const uint64_t off = ws + rr.x;
+        if (v) qrec[blk * 64 + pos] = make_uint4((uint32_t)off, (uint32_t)(off >> 32), kl, (uint32_t)(i0 + (rr.y & 255u)));
+      }
+    }
+    wave_sync();
+    uint2 rc0 = rec[lane], rc1 = rec[64 + lane], rc2 = rec[128 + lane], rc3 = rec[192 + lane];
+    wave_sync();
+    const uint8_t* base = keys + ws;
+    const uint32_t nch = (d0 + 63) >> 6;
+#pragma unroll 1
+    for (uint32_t c = 0; c < nch; c++) {
+      const uint32_t pos = 64 * c + lane;
+      const bool valid = pos < d0;
+      const uint2 rc = rc0;
+      rc0 = rc1; rc1 = rc2; rc2 = rc3;
+      const uint32_t kl = valid ? rc.y >> 8 : 0u;
+      const bool al = __ballot(kl >= 64u) != 0;
+      const int cmx = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
+                    : __ballot((kl & 48u) >= 16u) ? 16 : 0;
+      if (valid) {
+        const uint8_t* p = base + rc.x;
+        const bool safe = (uint64_t)rc.x + kl + 16 <= wend;
+        const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
+        Blk h;
+        if (al) h = meow_a<true, 48, false>(p, kl, safe, K, T);
+        else if (cmx == 48) h = meow_a<false, 48, false>(p, kl, safe, K, T);
+        else if (cmx == 32) h = meow_a<false, 32, false>(p, kl, safe, K, T);
+        else if (cmx == 16) h = meow_a<false, 16, false>(p, kl, safe, K, T);
+        else h = meow_a<false, 0, false>(p, kl, safe, K, T);
+        stage[rc.y & 255u] = fix ? fixup(h) : h;
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+      const uint32_t j = 64 * c + lane;
+      if (j < k) store_h<true>(out, i0 + j, stage[j], false);
+    }
+    wave_sync();
+    if (nfb) {
+      // the run's stores (stale words in deferred slots) before the blocks'
+      // hashes for those slots; the blocks' records visible to every lane
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll 1
+      for (uint32_t i = 0; i < nfb; i++) {
+        const uint32_t e = __builtin_amdgcn_readlane(fb, i);
+        const uint32_t blk = e & 255u;
+        v12_block<NT, void, KF>(keys, kend, qrec + blk * 64, e >> 8, 64u, s1, s2, out, fix, kfull, kf, T);
+        freem |= 1ull << blk;
+      }
+    }
+  }
+  // the open blocks
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  uint64_t om = __ballot(lane < (uint32_t)kQCls && (qs & 0xffffu) < 64u);
+  while (om) {
+    const uint32_t c = (uint32_t)__builtin_ctzll(om);
+    om &= om - 1;
+    const uint32_t st = __builtin_amdgcn_readlane(qs, c);
+    v12_block<NT, void, KF>(keys, kend, qrec + (st >> 16) * 64, c, st & 0xffffu, s1, s2, out, fix, kfull, kf, T);
+  }
+}
+
+// Per-stream scratch for the deferral queues: a private stream-ordered pool
+// per device (allocations are cached by the pool, so a call does not pay for
+// a fresh hipMalloc, and concurrent calls on different streams get disjoint
+// buffers).
+std::mutex g_qpool_mu;
+hipMemPool_t g_qpool[64] = {};
+
+int qpool_get(hipMemPool_t* out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  if (dev < 0 || dev >= 64) return set_err(KVH_EINVAL);
+  std::lock_guard<std::mutex> g(g_qpool_mu);
+  if (!g_qpool[dev]) {
+    hipMemPoolProps p = {};
+    p.allocType = hipMemAllocationTypePinned;
+    p.location.type = hipMemLocationTypeDevice;
+    p.location.id = dev;
+    e = hipMemPoolCreate(&g_qpool[dev], &p);
+    if (e != hipSuccess) { g_qpool[dev] = nullptr; return hip_err(e); }
+    uint64_t keep = ~0ull;  // never release cached memory on synchronisation
+    (void)hipMemPoolSetAttribute(g_qpool[dev], hipMemPoolAttrReleaseThreshold, &keep);
+  }
+  *out = g_qpool[dev];
+  return 0;
+}
+
+// k_var12: one kernel; scratch = 64 blocks of 64 records per wave.
+template <int REM>
+int var12_launch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_t seed1, uint64_t seed2,
+                 uint64_t* out, uint32_t flags, hipStream_t st, int cus) {
+  if (n >= (1ull << 32) || n < 4096) return 1;
+  const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
+  const size_t bytes = (size_t)grid * 16 * 64 * 64 * sizeof(uint4);
+  hipMemPool_t pool;
+  if (qpool_get(&pool) != 0) return 1;
+  void* mem = nullptr;
+  if (hipMallocFromPoolAsync(&mem, bytes, pool, st) != hipSuccess) { (void)hipGetLastError(); return 1; }
+  hipLaunchKernelGGL((k_var12<2, 16, REM>), dim3(grid), dim3(1024), 0, st, kp, offsets, n, seed1, seed2, out, flags,
+                     (uint4*)mem);
+  int rc = launch_done();
+  const hipError_t e = hipFreeAsync(mem, st);
+  if (rc == 0 && e != hipSuccess) rc = hip_err(e);
+  return rc;
+}
+
+// Windows, then queues.  Returns 1 when the batch does not take this path
+// (the caller runs k_var9), 0 or an error otherwise.
+template <int REM>
+int var11_launch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_t seed1, uint64_t seed2,
+                 uint64_t* out, uint32_t flags, hipStream_t st, int cus) {
+  if (n >= (1ull << 32) || n < 4096) return 1;  // u32 record indices; small batches gain nothing
+  const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
+  const uint64_t regions = (uint64_t)grid * 16;
+  const uint64_t nwin = (n + 255) / 256;
+  const uint64_t keys_per_wave = (nwin + regions - 1) / regions * 256;
+  // blocks for 3/8 of a wave's keys (C2 defers ~1/4) plus one open block per class
+  const uint64_t rb = (keys_per_wave * 3 / 8 + 63) / 64 + 2 * kQCls + 4;
+  const size_t rec_b = (size_t)(regions * rb * 64 * sizeof(uint4));
+  const size_t meta_b = (size_t)(regions * rb * 4), bytes = rec_b + meta_b + regions * 4;
+  hipMemPool_t pool;
+  if (qpool_get(&pool) != 0) return 1;
+  void* mem = nullptr;
+  if (hipMallocFromPoolAsync(&mem, bytes, pool, st) != hipSuccess) { (void)hipGetLastError(); return 1; }
+  VarQ q{(uint4*)mem, (uint32_t*)((uint8_t*)mem + rec_b), (uint32_t*)((uint8_t*)mem + rec_b + meta_b),
+         (uint32_t)rb};
+  hipLaunchKernelGGL((k_var11<2, 16, REM>), dim3(grid), dim3(1024), 0, st, kp, offsets, n, seed1, seed2, out,
+                     flags, q);
+  int rc = launch_done();
+  if (rc == 0) {
+    hipLaunchKernelGGL((k_var11_q<4, 16, false>), dim3(grid), dim3(1024), 0, st, kp, offsets + n, seed1,
+                       seed2, out, flags, q, regions);
+    rc = launch_done();
+  }
+  const hipError_t e = hipFreeAsync(mem, st);
+  if (rc == 0 && e != hipSuccess) rc = hip_err(e);
+  return rc;
+}
+
+
 constexpr int kNotMine = 1;  // the knob value belongs to the product path
 
 // fixed length: the research kernels for L = 16 / 32 (the product knobs 0
@@ -2039,6 +2717,17 @@ int exp_var_int(int var, const uint8_t* kp, const uint64_t* offsets, uint64_t n,
                 uint64_t* out, uint32_t flags, hipStream_t st, int cus) {
   const uint32_t grid = grid_for(n / 4 + 1, cus, 1);
   switch (var) {
+    case 40: case 41: case 42: case 43: {  // deferral (round 3); batches they do not take: the generic kernel
+      int r = var == 40 ? var11_launch<32>(kp, offsets, n, seed1, seed2, out, flags, st, cus)
+            : var == 41 ? var11_launch<0>(kp, offsets, n, seed1, seed2, out, flags, st, cus)
+            : var == 42 ? var12_launch<32>(kp, offsets, n, seed1, seed2, out, flags, st, cus)
+                        : var12_launch<0>(kp, offsets, n, seed1, seed2, out, flags, st, cus);
+      if (r == 1) {
+        uint64_t sd[16] = {seed1, seed2};
+        r = generic_launch(true, kp, offsets, 0, n, sd, 1, out, flags, st, cus);
+      }
+      return r;
+    }
     // conflict attribution (counter-only except 31) and store modes of k_var9 (round 3)
     case 28: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 1>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
     case 29: hipLaunchKernelGGL((k_var9x<2, 16, 256, false, false, 3>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2, out, flags); return launch_done();
@@ -2139,7 +2828,7 @@ bool exp_var(int var, const uint8_t* kp, const uint64_t* offsets, uint64_t n, ui
   return true;
 }
 
-bool exp_var_knob(int v) { return v >= 2 && v <= 39; }
+bool exp_var_knob(int v) { return v >= 2 && v <= 43; }
 
 int exp_set_tuning(int k, int value) {
   auto set = [](Knob& g, int v) { return g.exchange(v, std::memory_order_relaxed); };
