@@ -438,18 +438,25 @@ __device__ __forceinline__ uint32_t bk_emit(uint64_t j, const Rec& r, bool has_n
   return dup ? 1u : 0u;
 }
 
-__global__ void __launch_bounds__(kBkT)
+// CAP / D: bucket capacity and counting-sort bits.  <12288, 13> needs
+// 128 KiB of LDS (one workgroup per CU); <8000, 12> fits two per CU (78.6
+// KiB), so one workgroup's loads overlap the other's LDS phases -- used when
+// the mean bucket leaves the largest far below 8000.
+template <uint32_t CAP, int D>
+__global__ void __launch_bounds__(kBkT, CAP <= 8192 ? 8 : 1)
 k_bk_sort(const Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
           uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
           uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
           uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
+  constexpr uint32_t kBkCap = CAP;
+  constexpr int kBkD = D;
   __shared__ uint32_t K[kBkCap];         // key64 bits [B, B + 32) of each record
   __shared__ uint16_t dig[kBkCap];       // its top kBkD bits
   __shared__ uint16_t ord[kBkCap];       // sorted position -> record
   __shared__ uint32_t hist[1u << kBkD];  // digit counts -> starts -> ends
   __shared__ uint32_t wsum[kBkT / 64], wmax[kBkT / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr uint32_t nd = 1u << kBkD, per = nd / kBkT;  // 8 digits per thread
+  constexpr uint32_t nd = 1u << kBkD, per = nd / kBkT;  // 4-8 digits per thread
   uint32_t d_total = 0;
   for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
     const uint32_t R = cnt[b], base = start[b];
@@ -1107,6 +1114,9 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
     auto mean_of = [&](uint32_t B) { return (double)n / (reach * std::ldexp(1.0, (int)B)); };
     uint32_t B = 0;
     while (B < (uint32_t)kBkMaxB && mean_of(B) > 6144.0) B++;
+    // buckets then hold ~mean +- sqrt(mean): the two-per-CU bucket sort (capacity
+    // 8000) when the mean leaves a wide margin (knob 22 = 1 forces the 12288 one)
+    const bool small_b = mean_of(B) <= 6400.0 && g_tune_sort_cap.load(std::memory_order_relaxed) == 0;
     if (mean_of(B) <= 9000.0 && engine != 2 && B >= 2) {
       // two passes of <= 7 bits, tile-stable LDS-staged scatters
       const uint32_t B2 = B / 2, B1 = B - B2, nb1 = 1u << B1, nb = 1u << B;
@@ -1155,7 +1165,12 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                          (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
                          (const uint32_t*)H2, (const uint32_t*)start, recB);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_bk_sort, dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
+      if (small_b)
+        hipLaunchKernelGGL((k_bk_sort<8000, 12>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
+                           (const Rec*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
+                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      else
+      hipLaunchKernelGGL((k_bk_sort<12288, 13>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
                          (const Rec*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                          items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
       if ((rc = launch_done())) return rc;
@@ -1195,7 +1210,12 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       hipLaunchKernelGGL(k_bk_scatter, dim3(ntiles), dim3(kBkT), 0, st, hashes, items, (uint64_t)n, g, sb, B,
                          (const uint32_t*)H, rec);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_bk_sort, dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st, (const Rec*)rec,
+      if (small_b)
+        hipLaunchKernelGGL((k_bk_sort<8000, 12>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
+                           (const Rec*)rec, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out,
+                           dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      else
+      hipLaunchKernelGGL((k_bk_sort<12288, 13>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st, (const Rec*)rec,
                          (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out,
                          dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
       if ((rc = launch_done())) return rc;
@@ -1267,7 +1287,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
 
 }  // namespace
 
-namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; } }
 
 extern "C" {
 

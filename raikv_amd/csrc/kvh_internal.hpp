@@ -203,6 +203,9 @@ extern std::atomic<int> g_tune_sort_bits;
 // table-order sort engine: 0 = two-pass bucketed when the batch fits it (else radix), 1 = radix (rocPRIM)
 // always, 2 = one-pass bucketed when the batch fits it
 extern std::atomic<int> g_tune_sort_engine;
+// bucket sort: 0 = two workgroups per CU (capacity 8000) when the buckets are small enough, 1 = always the
+// one-per-CU kernel (capacity 12288)
+extern std::atomic<int> g_tune_sort_cap;
 // span hashing: 2 / 1 = wave-chunked kernel with the short-key path, two / one spans per lane
 // (default 2), 0 = lane per span
 extern std::atomic<int> g_tune_spans;

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """A/B of the table-order sort (kvh_set_tuning(17, bits): h1 bits sorted
-below the slot bits; 64 = the full 64-bit key) on bench.py's f2 workload;
-outputs asserted equal."""
+below the slot bits; 64 = the full 64-bit key; or, with TUNE_KNOB=20, the
+engines: 0 two-pass bucketed, 2 one-pass bucketed, 1 radix) on bench.py's
+f2 workload; outputs asserted equal."""
 import json, os, sys
+KNOB = int(os.environ.get("TUNE_KNOB", "17"))
 import numpy as np
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -25,7 +27,7 @@ res = {}
 st = torch.cuda.current_stream()
 for r in range(3):
     for bits in [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "64,16,8").split(",")]:
-        kvh.lib.kvh_set_tuning(17, bits)
+        kvh.lib.kvh_set_tuning(KNOB, bits)
         srt.sort(h, items, dedup=True, out=ho, items_out=io)
         torch.cuda.synchronize()
         if ref is None: ref = (ho.clone(), io.clone(), int(srt.dups.item()))
@@ -35,7 +37,7 @@ for r in range(3):
             a.record(st); srt.sort(h, items, dedup=True, out=ho, items_out=io); b.record(st)
         torch.cuda.synchronize()
         res.setdefault(bits, []).extend(a.elapsed_time(b) for a, b in ev)
-kvh.lib.kvh_set_tuning(17, 16)
+kvh.lib.kvh_set_tuning(KNOB, 0 if KNOB == 20 else 16)
 for bits, t in res.items():
     ms = float(np.median(t))
-    print(json.dumps({"sort_bits_below_slot": bits, "median_ms": ms, "Gkeys_s": n / ms / 1e6, "dups": ref[2]}))
+    print(json.dumps({"knob": KNOB, "value": bits, "median_ms": ms, "Gkeys_s": n / ms / 1e6, "dups": ref[2]}))
