@@ -45,7 +45,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
 # (MI355X_MICROARCH.md §LDS, 128 B/clk), 256 CUs, 2.4 GHz peak engine clock
 LDS_PEAK_LOOKUPS = 32 * 256 * 2.4e9
 # T-table lookups per unit of work (16 per AES round; folded rounds)
-LOOKUPS_PER_UNIT = {"c1": 5 * 16, "c4": 7 * 16, "c4g": 7 * 16, "c64": 13 * 16, "c3": 4 * 7 * 16, "f1": 5 * 16,
+# (C3's unit is one hash: 7 rounds of 16 lookups per seed, four seeds per key)
+LOOKUPS_PER_UNIT = {"c1": 5 * 16, "c4": 7 * 16, "c4g": 7 * 16, "c64": 13 * 16, "c3": 7 * 16, "f1": 5 * 16,
                     "f4": 16}
 # the float4 copy rate MI355X_MICROARCH.md records for this part (the guide's
 # achievable streaming figure, beside the box's own copy probe)

@@ -32,7 +32,7 @@ if a.var >= 0:
 torch.cuda.set_device(0)
 g = torch.Generator(device="cuda")
 g.manual_seed(1)
-cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1),
+cfg = {"c1": (100_000_000, 16, 1), "c2": (100_000_000, 0, 1), "c3": (50_000_000, 32, 4), "c4": (125_000_000, 32, 1), "c64": (100_000_000, 64, 1), "c4g": (1_000_000_000, 32, 1),
        "f1": (100_000_000, 16, -1), "f1p": (100_000_000, 16, -2), "f4": (100_000_000, 16, -4),
        "f4v": (100_000_000, 0, -4), "f3": (1 << 30, 0, -3), "f2": (100_000_000, 16, -5)}
 n, L, ar = cfg[a.config]
