@@ -313,6 +313,19 @@ __device__ __forceinline__ bool bk_less(const HtGeom& g, uint32_t sb, const Rec&
   return a.pad < b.pad;
 }
 
+// Tile of workgroup `bid` in a grid of G: the tiles of each XCD consecutive.
+// Workgroups are dispatched to the 8 XCDs round-robin (bid % 8, speed only:
+// correctness never depends on it), and each XCD has its own L2.  With tile
+// = bid, neighbouring tiles ran on different XCDs, so the 128-byte lines
+// where one tile's run of a bucket ends and the next tile's begins were
+// written back partially from two L2s (k_tw_scatter2 wrote 6.4 GB for 3.2 GB
+// of records); here XCD x takes tiles [x q + min(x, r), ...), q = G / 8,
+// r = G % 8 -- a bijection on [0, G).
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t G) {
+  const uint32_t q = G >> 3, r = G & 7u, x = bid & 7u, k = bid >> 3;
+  return x * q + (x < r ? x : r) + k;
+}
+
 __global__ void __launch_bounds__(kBkT)
 k_bk_hist(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sb, uint32_t B, uint32_t* __restrict__ H,
           uint32_t* __restrict__ novf) {
@@ -410,7 +423,7 @@ __global__ void __launch_bounds__(kBkT)
 k_bk_scatter(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, HtGeom g, uint32_t sb,
              uint32_t B, const uint32_t* __restrict__ H, Rec* __restrict__ recs) {
   __shared__ uint32_t pos[1u << kBkMaxB];
-  const uint32_t nb = 1u << B, tile = blockIdx.x;
+  const uint32_t nb = 1u << B, tile = xcd_tile(blockIdx.x, gridDim.x);
   for (uint32_t b = threadIdx.x; b < nb; b += kBkT) pos[b] = H[(uint64_t)tile * nb + b];
   __syncthreads();
   const uint64_t i0 = (uint64_t)tile * kBkTile;
@@ -811,7 +824,7 @@ k_tw_scatter1(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items
               uint32_t B, uint32_t B2, const uint32_t* __restrict__ H, Rec* __restrict__ recA,
               uint16_t* __restrict__ bA) {
   __shared__ TwShared S;
-  const uint32_t tid = threadIdx.x, tile = blockIdx.x, nb1 = 1u << (B - B2);
+  const uint32_t tid = threadIdx.x, tile = xcd_tile(blockIdx.x, gridDim.x), nb1 = 1u << (B - B2);
   const uint64_t i0 = (uint64_t)tile * kTwTile;
   Rec r[kTwPer];
   uint32_t dg[kTwPer], bk[kTwPer], pos[kTwPer];
@@ -983,7 +996,7 @@ k_tw_scatter2(const Rec* __restrict__ recA, const uint16_t* __restrict__ bA, con
               const uint32_t* __restrict__ cnt1, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
               const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, Rec* __restrict__ rec) {
   __shared__ TwShared S;
-  const uint32_t tid = threadIdx.x, nb2 = 1u << B2, j = blockIdx.x;
+  const uint32_t tid = threadIdx.x, nb2 = 1u << B2, j = xcd_tile(blockIdx.x, gridDim.x);
   uint32_t d1, p0, p1;
   if (!tw_tile2(j, tbs, nb1, cnt1, start1, &d1, &p0, &p1)) return;  // workgroup-uniform
   Rec r[kTwPer];
@@ -1008,9 +1021,13 @@ k_tw_scatter2(const Rec* __restrict__ recA, const uint16_t* __restrict__ bA, con
       S.dig[pos[k]] = (uint8_t)dg[k];
     }
   __syncthreads();
-  for (uint32_t p = tid; p < p1 - p0; p += kTwT) {
+  // one 16-byte half record per lane: a store instruction covers 32 whole
+  // consecutive records (1 KiB) instead of the same half of 64 records
+  for (uint32_t p2 = tid; p2 < 2 * (p1 - p0); p2 += kTwT) {
+    const uint32_t p = p2 >> 1, half = p2 & 1u;
     const uint32_t d = S.dig[p];
-    rec[(uint64_t)S.gofs[d] + (p - S.lstart[d])] = S.stage[p];
+    const uint4 v = ((const uint4*)&S.stage[p])[half];
+    ((uint4*)(rec + (uint64_t)S.gofs[d] + (p - S.lstart[d])))[half] = v;
   }
 }
 

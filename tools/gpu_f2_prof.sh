@@ -13,10 +13,11 @@ o = sys.argv[1]
 st = list(csv.DictReader(open(o + "/trace/run_kernel_stats.csv")))
 pm = json.load(open(o + "/pmc_summary.json"))
 for r in st:
-    if "k_bk" in r["Name"] or "k_sort" in r["Name"]:
+    if "k_bk" in r["Name"] or "k_sort" in r["Name"] or "k_tw" in r["Name"]:
         k = [v for n, v in pm.items() if n[:60] == r["Name"][:60]]
         fw = ""
         if k and "FETCH_SIZE" in k[0]:
-            fw = "fetch %.2f GB write %.2f GB per call" % (k[0]["FETCH_SIZE"] * 2048 / k[0]["_dispatches"] / 1e9, k[0]["WRITE_SIZE"] * 1024 / k[0]["_dispatches"] / 1e9)
+            # pmc_summary holds per-dispatch means (KB): x1024, FETCH x2 (gfx950 streaming rule)
+            fw = "fetch %.2f GB write %.2f GB per dispatch" % (k[0]["FETCH_SIZE"] * 2048 / 1e9, k[0]["WRITE_SIZE"] * 1024 / 1e9)
         print("%-40s calls %4s avg %8.1f us  %s" % (r["Name"][:40], r["Calls"], float(r["AverageNs"]) / 1e3, fw))
 PY
