@@ -60,6 +60,12 @@ constexpr uint64_t kShortRun = 64;
 struct __attribute__((aligned(16))) Rec {
   uint64_t h1, h2, item, pad;
 };
+// (h1, h2, item) without the input index: the two-pass bucketed path, whose
+// tile-stable scatters deliver every bucket in input order, so a record's
+// position in its bucket is its tie-break (a quarter less to move per pass)
+struct R24 {
+  uint64_t h1, h2, item;
+};
 
 __device__ __forceinline__ bool rec_less(uint64_t a1, uint64_t a2, uint64_t b1, uint64_t b2) {
   const uint64_t a0 = a1 << 1, b0 = b1 << 1;
@@ -312,6 +318,19 @@ __device__ __forceinline__ bool bk_less(const HtGeom& g, uint32_t sb, const Rec&
   if (a.h1 != b.h1 || a.h2 != b.h2) return rec_less(a.h1, a.h2, b.h1, b.h2);
   return a.pad < b.pad;
 }
+// the same for records at bucket positions ia, ib: a Rec carries its input
+// index; an R24 bucket is in input order, so the position stands in for it
+__device__ __forceinline__ bool bk_less_at(const HtGeom& g, uint32_t sb, const Rec& a, const Rec& b, uint32_t,
+                                           uint32_t) {
+  return bk_less(g, sb, a, b);
+}
+__device__ __forceinline__ bool bk_less_at(const HtGeom& g, uint32_t sb, const R24& a, const R24& b, uint32_t ia,
+                                           uint32_t ib) {
+  const uint64_t ka = sort_key64(g, sb, a.h1), kb = sort_key64(g, sb, b.h1);
+  if (ka != kb) return ka < kb;
+  if (a.h1 != b.h1 || a.h2 != b.h2) return rec_less(a.h1, a.h2, b.h1, b.h2);
+  return ia < ib;
+}
 
 // Tile of workgroup `bid` in a grid of G: the tiles of each XCD consecutive.
 // Workgroups are dispatched to the 8 XCDs round-robin (bid % 8, speed only:
@@ -441,7 +460,8 @@ k_bk_scatter(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items,
 
 // outputs for sorted position p of a bucket whose record for p is r, next
 // the record at p + 1 (when has_next): dedup marks as ctest.c:96-104
-__device__ __forceinline__ uint32_t bk_emit(uint64_t j, const Rec& r, bool has_next, uint64_t n1, uint64_t n2,
+template <class RT>
+__device__ __forceinline__ uint32_t bk_emit(uint64_t j, const RT& r, bool has_next, uint64_t n1, uint64_t n2,
                                             uint32_t dedup, uint64_t* __restrict__ h_out,
                                             uint64_t* __restrict__ items_out) {
   const bool dup = dedup && has_next && r.h1 == n1 && r.h2 == n2;
@@ -455,9 +475,9 @@ __device__ __forceinline__ uint32_t bk_emit(uint64_t j, const Rec& r, bool has_n
 // 128 KiB of LDS (one workgroup per CU); <8000, 12> fits two per CU (78.6
 // KiB), so one workgroup's loads overlap the other's LDS phases -- used when
 // the mean bucket leaves the largest far below 8000.
-template <uint32_t CAP, int D>
+template <uint32_t CAP, int D, class RT = Rec>
 __global__ void __launch_bounds__(kBkT, CAP <= 8192 ? 8 : 1)
-k_bk_sort(const Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
+k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
           uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
           uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
           uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
@@ -478,7 +498,7 @@ k_bk_sort(const Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const 
       if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
       continue;
     }
-    const Rec* rb = recs + base;
+    const RT* rb = recs + base;
 #pragma unroll
     for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
     __syncthreads();
@@ -533,7 +553,7 @@ k_bk_sort(const Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const 
         while (c > s0) {
           const uint16_t y = ord[c - 1];
           const uint32_t ky = K[y];
-          const bool lt = kx != ky ? kx < ky : bk_less(g, sb, rb[x], rb[y]);
+          const bool lt = kx != ky ? kx < ky : bk_less_at(g, sb, rb[x], rb[y], x, y);
           if (!lt) break;
           ord[c] = y;
           c--;
@@ -544,14 +564,14 @@ k_bk_sort(const Rec* __restrict__ recs, const uint32_t* __restrict__ cnt, const 
     __syncthreads();
     for (uint32_t p0 = 0; p0 < R; p0 += kBkT) {
       const uint32_t p = p0 + tid;
-      Rec r;
+      RT r;
       if (p < R) r = rb[ord[p]];
       // the successor's pair: the next lane's record, or a load at a wave's edge
       uint64_t n1 = (uint64_t)__shfl_down((unsigned long long)r.h1, 1, 64),
                n2 = (uint64_t)__shfl_down((unsigned long long)r.h2, 1, 64);
       const bool has_next = p + 1 < R;
       if (lane == 63 && has_next) {
-        const Rec& q = rb[ord[p + 1]];
+        const RT& q = rb[ord[p + 1]];
         n1 = q.h1;
         n2 = q.h2;
       }
@@ -711,6 +731,26 @@ k_bk_long(Rec* __restrict__ recs, Rec* __restrict__ tmp, const uint32_t* __restr
   }
 }
 
+// Two-pass path, before k_bk_long: each overflowing bucket (R24 records in
+// input order) copied as 32-byte records whose `pad` is the bucket position
+// (the input order's stand-in) into the first-pass buffer, free by now; the
+// second-pass buffer then serves as k_bk_long's partition space.
+__global__ void __launch_bounds__(kSB)
+k_bk_cvt(const R24* __restrict__ src, Rec* __restrict__ dst, const uint32_t* __restrict__ cnt,
+         const uint32_t* __restrict__ start, const uint32_t* __restrict__ novf, const uint32_t* __restrict__ ovf) {
+  const uint32_t count = *novf;
+  for (uint32_t r = blockIdx.x; r < count; r += gridDim.x) {
+    const uint32_t b = ovf[r];
+    const uint64_t len = cnt[b], base = start[b];
+    for (uint64_t t = threadIdx.x; t < len; t += kSB) {
+      const R24 x = src[base + t];
+      Rec y;
+      y.h1 = x.h1; y.h2 = x.h2; y.item = x.item; y.pad = t;
+      dst[base + t] = y;
+    }
+  }
+}
+
 
 // ---------------------------------------------------------------------
 // Two-pass bucketed path (round 3): the B bucket bits of B2 (k_bk_scatter's
@@ -745,7 +785,7 @@ constexpr int kTwPer = (int)(kTwTile / kTwT);  // elements per thread
 constexpr int kTwD = 128;                      // digit values (<= 7 bits)
 
 struct TwShared {
-  Rec stage[kTwTile];                  // the tile in digit order
+  R24 stage[kTwTile];                  // the tile in digit order
   uint16_t cnt[kTwPer][kTwW][kTwD];    // per (round, wave, digit) counts -> offsets in the digit
   uint16_t bkt[kTwTile];               // the full bucket id of each staged record
   uint8_t dig[kTwTile];                // its digit
@@ -821,12 +861,12 @@ k_tw_hist1(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sb, ui
 
 __global__ void __launch_bounds__(kTwT)
 k_tw_scatter1(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items, uint64_t n, HtGeom g, uint32_t sb,
-              uint32_t B, uint32_t B2, const uint32_t* __restrict__ H, Rec* __restrict__ recA,
+              uint32_t B, uint32_t B2, const uint32_t* __restrict__ H, R24* __restrict__ recA,
               uint16_t* __restrict__ bA) {
   __shared__ TwShared S;
   const uint32_t tid = threadIdx.x, tile = xcd_tile(blockIdx.x, gridDim.x), nb1 = 1u << (B - B2);
   const uint64_t i0 = (uint64_t)tile * kTwTile;
-  Rec r[kTwPer];
+  R24 r[kTwPer];
   uint32_t dg[kTwPer], bk[kTwPer], pos[kTwPer];
   bool v[kTwPer];
 #pragma unroll
@@ -837,7 +877,6 @@ k_tw_scatter1(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items
       r[k].h1 = h[2 * i];
       r[k].h2 = h[2 * i + 1];
       r[k].item = items ? items[i] : i;
-      r[k].pad = i;
       bk[k] = bk_of(sort_key64(g, sb, r[k].h1), B);
     } else {
       bk[k] = 0;
@@ -855,11 +894,15 @@ k_tw_scatter1(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items
     }
   __syncthreads();
   const uint32_t total = (uint32_t)min<uint64_t>(kTwTile, n - i0);
-  for (uint32_t p = tid; p < total; p += kTwT) {
+  // one 8-byte word per lane: a store instruction covers ~21 whole
+  // consecutive records (512 B)
+  const uint64_t* sw = (const uint64_t*)S.stage;
+  for (uint32_t w = tid; w < 3 * total; w += kTwT) {
+    const uint32_t p = w / 3, part = w - 3 * p;
     const uint32_t d = S.dig[p];
     const uint64_t q = (uint64_t)S.gofs[d] + (p - S.lstart[d]);
-    recA[q] = S.stage[p];
-    bA[q] = S.bkt[p];
+    ((uint64_t*)(recA + q))[part] = sw[w];
+    if (part == 0) bA[q] = S.bkt[p];
   }
 }
 
@@ -992,14 +1035,14 @@ k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start
 }
 
 __global__ void __launch_bounds__(kTwT)
-k_tw_scatter2(const Rec* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
+k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
               const uint32_t* __restrict__ cnt1, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
-              const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, Rec* __restrict__ rec) {
+              const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, R24* __restrict__ rec) {
   __shared__ TwShared S;
   const uint32_t tid = threadIdx.x, nb2 = 1u << B2, j = xcd_tile(blockIdx.x, gridDim.x);
   uint32_t d1, p0, p1;
   if (!tw_tile2(j, tbs, nb1, cnt1, start1, &d1, &p0, &p1)) return;  // workgroup-uniform
-  Rec r[kTwPer];
+  R24 r[kTwPer];
   uint32_t dg[kTwPer], pos[kTwPer];
   bool v[kTwPer];
 #pragma unroll
@@ -1021,13 +1064,13 @@ k_tw_scatter2(const Rec* __restrict__ recA, const uint16_t* __restrict__ bA, con
       S.dig[pos[k]] = (uint8_t)dg[k];
     }
   __syncthreads();
-  // one 16-byte half record per lane: a store instruction covers 32 whole
-  // consecutive records (1 KiB) instead of the same half of 64 records
-  for (uint32_t p2 = tid; p2 < 2 * (p1 - p0); p2 += kTwT) {
-    const uint32_t p = p2 >> 1, half = p2 & 1u;
+  // one 8-byte word per lane: a store instruction covers ~21 whole
+  // consecutive records (512 B) instead of the same third of 64 records
+  const uint64_t* sw = (const uint64_t*)S.stage;
+  for (uint32_t w = tid; w < 3 * (p1 - p0); w += kTwT) {
+    const uint32_t p = w / 3, part = w - 3 * p;
     const uint32_t d = S.dig[p];
-    const uint4 v = ((const uint4*)&S.stage[p])[half];
-    ((uint4*)(rec + (uint64_t)S.gofs[d] + (p - S.lstart[d])))[half] = v;
+    ((uint64_t*)(rec + (uint64_t)S.gofs[d] + (p - S.lstart[d])))[part] = sw[w];
   }
 }
 
@@ -1139,8 +1182,8 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       const uint32_t B2 = B / 2, B1 = B - B2, nb1 = 1u << B1, nb = 1u << B;
       const uint32_t ntiles = (uint32_t)((n + kTwTile - 1) / kTwTile);
       const uint32_t nch = (ntiles + kBkChunk - 1) / kBkChunk;
-      Rec* recA = (Rec*)(s + L.tw_recA);
-      Rec* recB = (Rec*)(s + L.tw_rec);
+      R24* recA = (R24*)(s + L.tw_recA);
+      R24* recB = (R24*)(s + L.tw_rec);
       uint16_t* bA = (uint16_t*)(s + L.tw_bA);
       uint32_t* H1 = (uint32_t*)(s + L.tw_H1);
       uint32_t* S1 = (uint32_t*)(s + L.tw_S1);
@@ -1178,20 +1221,25 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       hipLaunchKernelGGL(k_tw_start2, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
                          nb1, B2, start);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_tw_scatter2, dim3(ntB), dim3(kTwT), 0, st, (const Rec*)recA, (const uint16_t*)bA,
+      hipLaunchKernelGGL(k_tw_scatter2, dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA, (const uint16_t*)bA,
                          (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
                          (const uint32_t*)H2, (const uint32_t*)start, recB);
       if ((rc = launch_done())) return rc;
       if (small_b)
-        hipLaunchKernelGGL((k_bk_sort<8000, 12>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
-                           (const Rec*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
+        hipLaunchKernelGGL((k_bk_sort<8000, 12, R24>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
+                           (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                            items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
       else
-      hipLaunchKernelGGL((k_bk_sort<12288, 13>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
-                         (const Rec*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
+      hipLaunchKernelGGL((k_bk_sort<12288, 13, R24>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
+                         (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                          items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_bk_long, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st, recB, recA,
+      hipLaunchKernelGGL(k_bk_cvt, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st, (const R24*)recB,
+                         (Rec*)(s + L.tw_recA), (const uint32_t*)cnt, (const uint32_t*)start, (const uint32_t*)novf,
+                         (const uint32_t*)ovf);
+      if ((rc = launch_done())) return rc;
+      hipLaunchKernelGGL(k_bk_long, dim3(std::min<uint32_t>(nb, (uint32_t)cus * 2)), dim3(kSB), 0, st,
+                         (Rec*)(s + L.tw_recA), (Rec*)(s + L.tw_rec),
                          (const uint32_t*)cnt, (const uint32_t*)start, g, sb, h_out, items_out, dedup ? 1u : 0u,
                          (unsigned long long*)dup_count, (const uint32_t*)novf, (const uint32_t*)ovf);
       return launch_done();
