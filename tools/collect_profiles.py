@@ -15,7 +15,7 @@ HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",), "f4": ("k_crc_fix
 # a kernel that runs once per call: its dispatch counts give the calls in the
 # PMC run and in the traced bench run).  f2's rocPRIM kernels are the
 # library's trampoline kernels (torch's own rocPRIM sorts use other names).
-MULTI = {"f2": (("k_bk_",), "k_bk_hist") if os.environ.get("F2_ENGINE", "bucketed") == "bucketed"
+MULTI = {"f2": (("k_bk_", "k_tw_"), "k_bk_scan") if os.environ.get("F2_ENGINE", "bucketed") == "bucketed"
          else (("k_sort", "trampoline_kernel"), "k_sort_keys"),
          "f3": (("k_tok", "k_spans"), "k_spans")}
 # configs whose hot kernel gathers 16-byte key pieces in length-sorted windows: keys per launch
