@@ -175,7 +175,14 @@ def test_engines_agree(kvh, n, map_size):
         with _engine(kvh, 0, e):
             oh, oi = srt.sort(h, items=items, dedup=True)
             res[e] = (oh.clone(), oi.clone(), int(srt.dups.item()))
-    for e in (2, 1):
+    # the one-workgroup-per-CU bucket sort (knob 22 = 1) on the default engine
+    prev = kvh.lib.kvh_set_tuning(22, 1)
+    try:
+        oh, oi = srt.sort(h, items=items, dedup=True)
+        res["cap"] = (oh.clone(), oi.clone(), int(srt.dups.item()))
+    finally:
+        kvh.lib.kvh_set_tuning(22, prev)
+    for e in (2, 1, "cap"):
         assert torch.equal(res[0][0], res[e][0]) and torch.equal(res[0][1], res[e][1]) and res[0][2] == res[e][2], e
     if n <= 65537:
         og = orc_geom(ORC, map_size, 64, 1.0, 4, 4)
