@@ -248,13 +248,15 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 //    chosen by two wave-uniform facts (some key has a full block; the
 //    largest trail), so the state chains interleave and every short key's
 //    loads are issued before its first round.
+// Keys used in several rounds (a block's chunks, the Mixer) are prepared
+// once for the two-table round (PKY, LdsTab::prep; 2.89 vs 2.93 ms).
 // The variants need ~165 VGPRs, so 12 waves per CU; hashes go straight to
 // the wave's LDS stage at their input slot, records are 8 bytes
 // (window offset, length << 8 | slot), and no per-window value lives in a
 // register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
 // more take wide_window (input order, u64 offsets and lengths).
 
-template <int NT, int NW, int KF, bool PF = false>
+template <int NT, int NW, int KF, bool PF = false, bool PKY = true>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -371,11 +373,11 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
         const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
         const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
         Blk h;
-        if (al) h = meow_a<true, 48, PF>(p, kl, safe, K, T);
-        else if (cm == 48) h = meow_a<false, 48, PF>(p, kl, safe, K, T);
-        else if (cm == 32) h = meow_a<false, 32, PF>(p, kl, safe, K, T);
-        else if (cm == 16) h = meow_a<false, 16, PF>(p, kl, safe, K, T);
-        else h = meow_a<false, 0, PF>(p, kl, safe, K, T);
+        if (al) h = meow_a<true, 48, PF, PKY>(p, kl, safe, K, T);
+        else if (cm == 48) h = meow_a<false, 48, PF, PKY>(p, kl, safe, K, T);
+        else if (cm == 32) h = meow_a<false, 32, PF, PKY>(p, kl, safe, K, T);
+        else if (cm == 16) h = meow_a<false, 16, PF, PKY>(p, kl, safe, K, T);
+        else h = meow_a<false, 0, PF, PKY>(p, kl, safe, K, T);
         stage[rc.y & 255u] = fix ? fixup(h) : h;
       }
     }

@@ -81,6 +81,23 @@ struct LdsTab {
       return xor3(t0, t1, k) ^ rotl32(t2 ^ t3, 16);
     }
   }
+  // A round key as colk() takes it: with two tables the Td2/Td3 half of a
+  // column is rotl16(Td0[c] ^ Td1[d]); XORing rotl16(k) into it before the
+  // rotation (one v_bitop3) saves the separate XOR of k, so a key used in
+  // several rounds (an absorbed chunk twice, the Mixer up to six times) is
+  // rotated once.  With four tables the key is used as it is.
+  __device__ __forceinline__ static uint32_t prep(uint32_t k) { return NT == 4 ? k : rotl32(k, 16); }
+  __device__ __forceinline__ uint32_t colk(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kp) const {
+    if constexpr (NT == 4) {
+      return col(a, b, c, d, kp);
+    } else {
+      const uint32_t t0 = ld(__builtin_amdgcn_perm(a, lw[0], sel<0>()));
+      const uint32_t t1 = ld(__builtin_amdgcn_perm(b, lw[1], sel<1>()));
+      const uint32_t t2 = ld(__builtin_amdgcn_perm(c, lw[0], sel<2>()));
+      const uint32_t t3 = ld(__builtin_amdgcn_perm(d, lw[1], sel<3>()));
+      return xor3(t0, t1, rotl32(xor3(t2, t3, kp), 16));
+    }
+  }
 };
 
 // fill the replicated tables; dword index i = addr >> 2 decodes to
@@ -111,6 +128,25 @@ __device__ __forceinline__ Blk aesdec(const Blk& s, const Blk& k, const Tab& T) 
 #pragma unroll
   for (int c = 0; c < 4; c++)
     o.w[c] = T.col(s.w[c], s.w[(c + 3) & 3], s.w[(c + 2) & 3], s.w[(c + 1) & 3], k.w[c]);
+  return o;
+}
+// a round key prepared for T.colk (see LdsTab::prep), and AESDEC with it
+struct PKey {
+  uint32_t w[4];
+};
+template <class Tab>
+__device__ __forceinline__ PKey pkey(const Blk& k, const Tab&) {
+  PKey p;
+#pragma unroll
+  for (int c = 0; c < 4; c++) p.w[c] = Tab::prep(k.w[c]);
+  return p;
+}
+template <class Tab>
+__device__ __forceinline__ Blk aesdec_p(const Blk& s, const PKey& k, const Tab& T) {
+  Blk o;
+#pragma unroll
+  for (int c = 0; c < 4; c++)
+    o.w[c] = T.colk(s.w[c], s.w[(c + 3) & 3], s.w[(c + 2) & 3], s.w[(c + 1) & 3], k.w[c]);
   return o;
 }
 // the keyless half: T(s) = AESDEC(s, 0)
@@ -461,7 +497,7 @@ __device__ __forceinline__ Blk mask_bytes(Blk b, uint32_t n) {
 // chunks of a short key, and each block's four new chunks of a long key, are
 // requested before the rounds that use them.  Same dataflow as
 // key_hash.c:1155-1226.
-template <bool AL, int CM, bool PF, class Tab, class KGet, class LenT = uint32_t>
+template <bool AL, int CM, bool PF, bool PKY = false, class Tab, class KGet, class LenT = uint32_t>
 __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const KGet& K, const Tab& T) {
   constexpr bool P0 = AL || CM >= 16, P1 = AL || CM >= 32, P2 = AL || CM >= 48;  // state touched by some lane
   const LenT nb = L >> 6;
@@ -469,6 +505,19 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
   const bool first = nb == 0;
   const AChunks A(p, L, safe);
   const Blk M = K.M();
+  // PKY: keys used in more than one round go through LdsTab::prep once
+  PKey MP{};
+  if constexpr (PKY) MP = pkey(M, T);
+  auto adM = [&](const Blk& x) { if constexpr (PKY) return aesdec_p(x, MP, T); else return aesdec(x, M, T); };
+  auto ad2 = [&](const Blk& x, const Blk& k) {
+    if constexpr (PKY) { const PKey kp = pkey(k, T); return aesdec_p(aesdec_p(x, kp, T), kp, T); }
+    else return aesdec(aesdec(x, k, T), k, T);
+  };
+  // AESDEC(first ? f ^ k : AESDEC(s, k), k)
+  auto adT = [&](bool first_, const Blk& f, const Blk& s_, const Blk& k) {
+    if constexpr (PKY) { const PKey kp = pkey(k, T); return aesdec_p(bsel(first_, f, aesdec_p(s_, kp, T)), kp, T); }
+    else return aesdec(bsel(first_, f, aesdec(s_, k, T)), k, T);
+  };
   Blk S0 = bxor(ramp(0), M), S1 = bxor(ramp(1), M), S2 = bxor(ramp(2), M), S3 = bxor(ramp(3), M);
   // groups 4nb .. 4nb+4 (the trail's) once the blocks are absorbed
   Blk c0 = A.chunk(0), c1, c2 = bzero(), c3 = bzero(), c4 = bzero();
@@ -485,8 +534,8 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
       S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);                           \
       S2 = aesdec(bxor(K.F(2), k2), k2, T); S3 = aesdec(bxor(K.F(3), k3), k3, T);                           \
     } else {                                                                                               \
-      S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);                         \
-      S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);                         \
+      S0 = ad2(S0, k0); S1 = ad2(S1, k1);                                                                   \
+      S2 = ad2(S2, k2); S3 = ad2(S3, k3);                                                                   \
     }                                                                                                      \
     c0 = c4; c1 = n1; c2 = n2; c3 = n3; c4 = n4;                                                           \
   }
@@ -515,8 +564,8 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
           const Blk c1 = A.chunk(i + 1), c2 = A.chunk(i + 2), c3 = A.chunk(i + 3), c4 = A.chunk(i + 4);
           const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
           c0 = c4;
-          S0 = aesdec(aesdec(S0, k0, T), k0, T); S1 = aesdec(aesdec(S1, k1, T), k1, T);
-          S2 = aesdec(aesdec(S2, k2, T), k2, T); S3 = aesdec(aesdec(S3, k3, T), k3, T);
+          S0 = ad2(S0, k0); S1 = ad2(S1, k1);
+          S2 = ad2(S2, k2); S3 = ad2(S3, k3);
         }
       }
     }
@@ -541,19 +590,19 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
   if constexpr (AL) {
     // a block-absorbed state takes two rounds, an init state the folded one
     {
-      const Blk Y = aesdec(bsel(first, bxor(K.F0(3), r3), aesdec(S3, r3, T)), r3, T);
+      const Blk Y = adT(first, bxor(K.F0(3), r3), S3, r3);
       S3 = bsel(t != 0, Y, S3);
     }
     if constexpr (CM >= 48) {
-      const Blk Y = aesdec(bsel(first, bxor(K.F0(2), q2), aesdec(S2, q2, T)), q2, T);
+      const Blk Y = adT(first, bxor(K.F0(2), q2), S2, q2);
       S2 = bsel(C >= 48, Y, S2);
     }
     if constexpr (CM >= 32) {
-      const Blk Y = aesdec(bsel(first, bxor(K.F0(1), q1), aesdec(S1, q1, T)), q1, T);
+      const Blk Y = adT(first, bxor(K.F0(1), q1), S1, q1);
       S1 = bsel(C >= 32, Y, S1);
     }
     if constexpr (CM >= 16) {
-      const Blk Y = aesdec(bsel(first, bxor(K.F0(0), q0), aesdec(S0, q0, T)), q0, T);
+      const Blk Y = adT(first, bxor(K.F0(0), q0), S0, q0);
       S0 = bsel(C >= 16, Y, S0);
     }
   } else {
@@ -565,17 +614,17 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
     if constexpr (CM >= 32) { const Blk Y = aesdec(bxor(K.F(1), q1), q1, T); S1 = bsel(C >= 32, Y, S1); }
     if constexpr (CM >= 16) { const Blk Y = aesdec(bxor(K.F(0), q0), q0, T); S0 = bsel(C >= 16, Y, S0); }
   }
-  S3 = aesdec(S3, M, T);
-  if constexpr (P2) S2 = aesdec(S2, M, T); else S2 = K.G(2);
-  if constexpr (P1) S1 = aesdec(S1, M, T); else S1 = K.G(1);
-  if constexpr (P0) S0 = aesdec(S0, M, T); else S0 = K.G(0);
+  S3 = adM(S3);
+  if constexpr (P2) S2 = adM(S2); else S2 = K.G(2);
+  if constexpr (P1) S1 = adM(S1); else S1 = K.G(1);
+  if constexpr (P0) S0 = adM(S0); else S0 = K.G(0);
   Blk S2b;
-  if constexpr (P2) S2b = aesdec(aesdec(S2, S3, T), M, T);
-  else S2b = aesdec(bxor(K.TG2(), S3), M, T);
+  if constexpr (P2) S2b = adM(aesdec(S2, S3, T));
+  else S2b = adM(bxor(K.TG2(), S3));
   Blk S0b;
   if constexpr (P0) S0b = bxor(aesT(aesdec(S0, S1, T), T), S2b);
   else S0b = bxor(K.TCS0a(), S2b);
-  return aesdec(S0b, M, T);
+  return adM(S0b);
 }
 
 // constants held in registers (uniform length)
