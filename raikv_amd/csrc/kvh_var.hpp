@@ -106,6 +106,8 @@ struct LdsKV9 {
   // it (keys of kLT bytes or more) all read record 0: one broadcast address
   // instead of scattered records that conflict with the short keys' reads
   __device__ __forceinline__ Blk F0(int i) const { return full[L < (uint32_t)kLT ? L : 0u].F[i]; }
+  // the same for meow_a's chunks without a full block (every key under kLT bytes)
+  __device__ __forceinline__ Blk Fs(int i) const { return full[L < (uint32_t)kLT ? L : 0u].F[i]; }
   __device__ __forceinline__ Blk G(int i) const { return full[li()].G[i]; }
   __device__ __forceinline__ Blk TG2() const { return full[li()].TG2; }
   __device__ __forceinline__ Blk TCS0a() const { return full[li()].TCS0a; }

@@ -497,6 +497,14 @@ __device__ __forceinline__ Blk mask_bytes(Blk b, uint32_t n) {
 // chunks of a short key, and each block's four new chunks of a long key, are
 // requested before the rounds that use them.  Same dataflow as
 // key_hash.c:1155-1226.
+// F[i] of a key known to be shorter than 64 bytes: K.Fs(i) where the
+// accessor has one (one LDS record read, no select against the long-key
+// fold table), else K.F(i)
+template <class KGet>
+__device__ __forceinline__ auto f_short(const KGet& K, int i, int) -> decltype(K.Fs(i)) { return K.Fs(i); }
+template <class KGet>
+__device__ __forceinline__ Blk f_short(const KGet& K, int i, long) { return K.F(i); }
+
 template <bool AL, int CM, bool PF, bool PKY = false, class Tab, class KGet, class LenT = uint32_t>
 __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const KGet& K, const Tab& T) {
   constexpr bool P0 = AL || CM >= 16, P1 = AL || CM >= 32, P2 = AL || CM >= 48;  // state touched by some lane
@@ -607,12 +615,12 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
     }
   } else {
     {
-      const Blk Y = aesdec(bxor(K.F(3), r3), r3, T);
+      const Blk Y = aesdec(bxor(f_short(K, 3, 0), r3), r3, T);
       S3 = bsel(t != 0, Y, S3);
     }
-    if constexpr (CM >= 48) { const Blk Y = aesdec(bxor(K.F(2), q2), q2, T); S2 = bsel(C >= 48, Y, S2); }
-    if constexpr (CM >= 32) { const Blk Y = aesdec(bxor(K.F(1), q1), q1, T); S1 = bsel(C >= 32, Y, S1); }
-    if constexpr (CM >= 16) { const Blk Y = aesdec(bxor(K.F(0), q0), q0, T); S0 = bsel(C >= 16, Y, S0); }
+    if constexpr (CM >= 48) { const Blk Y = aesdec(bxor(f_short(K, 2, 0), q2), q2, T); S2 = bsel(C >= 48, Y, S2); }
+    if constexpr (CM >= 32) { const Blk Y = aesdec(bxor(f_short(K, 1, 0), q1), q1, T); S1 = bsel(C >= 32, Y, S1); }
+    if constexpr (CM >= 16) { const Blk Y = aesdec(bxor(f_short(K, 0, 0), q0), q0, T); S0 = bsel(C >= 16, Y, S0); }
   }
   S3 = adM(S3);
   if constexpr (P2) S2 = adM(S2); else S2 = K.G(2);
