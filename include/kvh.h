@@ -478,7 +478,7 @@ int         kvh_device_synchronize(void);
  *  21 = host batches of at most this many keys (and 512 KiB of key bytes)
  *       take the zero-copy tiny path (default 16384; 0 off),
  *  22 = ht_sort bucket sort (0 two workgroups per CU when the buckets are
- *       small enough; 1 always one per CU; 2 records kept on chip, one per CU),
+ *       small enough; 1 always one per CU),
  *   3 also takes 3 for the 40-64-byte fixed-length kernels.
  * Returns the previous value or KVH_EINVAL.  (Research kernels and ablation
  * builds whose outputs are not hashes exist only in the experiments build,

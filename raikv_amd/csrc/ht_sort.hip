@@ -585,135 +585,6 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
   }
 }
 
-// The R24 bucket sort with the records kept on chip (knob 22 = 2): each
-// thread holds its <= 8 records in registers from the one coalesced read, and
-// the sorted output leaves through an LDS stage in rounds of kStCh positions,
-// so no record is fetched a second time (k_bk_sort's final gather misses L2:
-// ~9 MB of buckets in flight per XCD).  One workgroup per CU (145 KiB).
-constexpr uint32_t kStCap = 8000, kStCh = 2048;
-constexpr int kStD = 12;
-__global__ void __launch_bounds__(kBkT, 1)
-k_bk_sort_st(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
-             uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
-             uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
-             uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
-  constexpr uint32_t PER = (kStCap + kBkT - 1) / kBkT;
-  __shared__ uint32_t K[kStCap];
-  __shared__ uint16_t dig[kStCap];
-  __shared__ uint16_t ord[kStCap];
-  __shared__ uint16_t inv[kStCap];
-  __shared__ uint32_t hist[1u << kStD];
-  __shared__ R24 stage[kStCh + 1];
-  __shared__ uint32_t wsum[kBkT / 64], wmax[kBkT / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  constexpr uint32_t nd = 1u << kStD, per = nd / kBkT;
-  uint32_t d_total = 0;
-  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-    const uint32_t R = cnt[b], base = start[b];
-    if (R == 0) continue;
-    if (R > kStCap) {
-      if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
-      continue;
-    }
-    const R24* rb = recs + base;
-#pragma unroll
-    for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
-    __syncthreads();
-    R24 rr[PER];
-#pragma unroll
-    for (uint32_t j = 0; j < PER; j++) {
-      const uint32_t t = tid + j * kBkT;
-      if (t < R) {
-        rr[j] = rb[t];
-        const uint32_t k32 = (uint32_t)((sort_key64(g, sb, rr[j].h1) << B) >> 32);
-        K[t] = k32;
-        dig[t] = (uint16_t)(k32 >> (32 - kStD));
-        atomicAdd(&hist[k32 >> (32 - kStD)], 1u);
-      }
-    }
-    __syncthreads();
-    {
-      uint32_t v[per], s = 0, mx = 0;
-#pragma unroll
-      for (uint32_t j = 0; j < per; j++) { v[j] = hist[tid * per + j]; s += v[j]; mx = max(mx, v[j]); }
-      uint32_t inc = s;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(inc, d, 64);
-        if (lane >= (uint32_t)d) inc += y;
-      }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
-      if (lane == 63) wsum[w] = inc;
-      if (lane == 0) wmax[w] = mx;
-      __syncthreads();
-      uint32_t wo = 0, bm = 0;
-      for (uint32_t q = 0; q < kBkT / 64; q++) {
-        if (q < w) wo += wsum[q];
-        bm = max(bm, wmax[q]);
-      }
-      if (bm > kBkRun) {
-        if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
-        __syncthreads();
-        continue;
-      }
-      uint32_t run = wo + inc - s;
-#pragma unroll
-      for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
-    }
-    __syncthreads();
-    for (uint32_t t = tid; t < R; t += kBkT) ord[atomicAdd(&hist[dig[t]], 1u)] = (uint16_t)t;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < per; j++) {
-      const uint32_t d = tid * per + j;
-      const uint32_t e = hist[d], s0 = d ? hist[d - 1] : 0u;
-      for (uint32_t a = s0 + 1; a < e; a++) {
-        const uint16_t x = ord[a];
-        const uint32_t kx = K[x];
-        uint32_t c = a;
-        while (c > s0) {
-          const uint16_t y = ord[c - 1];
-          const uint32_t ky = K[y];
-          const bool lt = kx != ky ? kx < ky : bk_less_at(g, sb, rb[x], rb[y], x, y);
-          if (!lt) break;
-          ord[c] = y;
-          c--;
-        }
-        ord[c] = x;
-      }
-    }
-    __syncthreads();
-    for (uint32_t p = tid; p < R; p += kBkT) inv[ord[p]] = (uint16_t)p;
-    __syncthreads();
-    for (uint32_t c0 = 0; c0 < R; c0 += kStCh) {
-      const uint32_t c1 = min(c0 + kStCh + 1, R);  // + the successor of the round's last position
-#pragma unroll
-      for (uint32_t j = 0; j < PER; j++) {
-        const uint32_t t = tid + j * kBkT;
-        if (t < R) {
-          const uint32_t p = inv[t];
-          if (p >= c0 && p < c1) stage[p - c0] = rr[j];
-        }
-      }
-      __syncthreads();
-      const uint32_t ce = min(c0 + kStCh, R);
-      for (uint32_t p = c0 + tid; p < ce; p += kBkT) {
-        const R24 r = stage[p - c0];
-        const bool has_next = p + 1 < R;
-        uint64_t n1 = 0, n2 = 0;
-        if (has_next) { n1 = stage[p + 1 - c0].h1; n2 = stage[p + 1 - c0].h2; }
-        d_total += bk_emit((uint64_t)base + p, r, has_next, n1, n2, dedup, h_out, items_out);
-      }
-      __syncthreads();
-    }
-  }
-  if (dedup && dups) {
-    const uint32_t t = block_sum<kBkT>(d_total, wsum);
-    if (tid == 0 && t) atomicAdd(dups, (unsigned long long)t);
-  }
-}
-
 // all-ascending bitonic network over R[0, len) by the full order (every
 // comparator puts the smaller record at the lower index, so the pad to a
 // power of two is virtual); one workgroup
@@ -1305,7 +1176,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
     while (B < (uint32_t)kBkMaxB && mean_of(B) > 6144.0) B++;
     // buckets then hold ~mean +- sqrt(mean): the two-per-CU bucket sort (capacity
     // 8000) when the mean leaves a wide margin (knob 22 = 1 forces the 12288 one)
-    const bool small_b = mean_of(B) <= 6400.0 && g_tune_sort_cap.load(std::memory_order_relaxed) != 1;
+    const bool small_b = mean_of(B) <= 6400.0 && g_tune_sort_cap.load(std::memory_order_relaxed) == 0;
     if (mean_of(B) <= 9000.0 && engine != 2 && B >= 2) {
       // two passes of <= 7 bits, tile-stable LDS-staged scatters
       const uint32_t B2 = B / 2, B1 = B - B2, nb1 = 1u << B1, nb = 1u << B;
@@ -1354,11 +1225,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                          (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
                          (const uint32_t*)H2, (const uint32_t*)start, recB);
       if ((rc = launch_done())) return rc;
-      if (small_b && g_tune_sort_cap.load(std::memory_order_relaxed) == 2)
-        hipLaunchKernelGGL(k_bk_sort_st, dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
-                           (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
-                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
-      else if (small_b)
+      if (small_b)
         hipLaunchKernelGGL((k_bk_sort<8000, 12, R24>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                            items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
