@@ -1,0 +1,58 @@
+// scatter2_probe: the write address streams of f2's two record passes,
+// replayed alone.  n 24-byte records, tiles of
+// 2048, 128 runs of 16 records per tile, one 8-byte word per lane stored:
+//   mode 1 (pass-1 shape): run d of tile t -> region d (n/128 records each)
+//          at record t*16
+//   mode 2 (pass-2 shape): tiles grouped 381 per first-level region; run d2
+//          of the k-th tile of region d1 -> sub-region (d1, d2) (n/16384
+//          records each) at record k*16
+// Prints ms per launch; run under rocprofv3 --pmc WRITE_SIZE for the bytes.
+// usage: scatter2_probe <mode> [n_millions=100] [reps=10]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+
+constexpr uint32_t kTile = 2048, kRuns = 128, kRun = kTile / kRuns;
+
+__global__ void __launch_bounds__(512) probe(uint64_t* __restrict__ out, uint64_t n, int mode) {
+  const uint64_t ntiles = n / kTile, t = blockIdx.x;
+  if (t >= ntiles) return;
+  const uint64_t region1 = n / kRuns;                 // pass-1 region size (records)
+  const uint64_t tiles_per_d1 = ntiles / kRuns;        // ~381 at 100M
+  const uint64_t sub = region1 / kRuns;                // pass-2 sub-region size
+  for (uint32_t w = threadIdx.x; w < 3 * kTile; w += 512) {
+    const uint32_t p = w / 3, part = w - 3 * p, run = p / kRun, in = p % kRun;
+    uint64_t rec;
+    if (mode == 1) {
+      rec = run * region1 + t * kRun + in;
+    } else {
+      const uint64_t d1 = t / tiles_per_d1 < kRuns ? t / tiles_per_d1 : kRuns - 1, k = t - d1 * tiles_per_d1;
+      rec = d1 * region1 + run * sub + (k * kRun + in) % sub;
+    }
+    out[rec * 3 + part] = w;
+  }
+}
+
+int main(int argc, char** argv) {
+  const int mode = argc > 1 ? atoi(argv[1]) : 1;
+  const uint64_t n = (argc > 2 ? atoll(argv[2]) : 100) * 1000000ull;
+  const int reps = argc > 3 ? atoi(argv[3]) : 10;
+  uint64_t* out;
+  if (hipMalloc(&out, n * 24) != hipSuccess) return 1;
+  hipEvent_t a, b;
+  hipEventCreate(&a); hipEventCreate(&b);
+  const uint32_t grid = (uint32_t)(n / kTile);
+  hipLaunchKernelGGL(probe, dim3(grid), dim3(512), 0, 0, out, n, mode);
+  hipDeviceSynchronize();
+  hipEventRecord(a);
+  for (int r = 0; r < reps; r++) hipLaunchKernelGGL(probe, dim3(grid), dim3(512), 0, 0, out, n, mode);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  printf("{\"mode\": %d, \"n\": %llu, \"ms\": %.4f, \"GBps_written\": %.1f}\n", mode, (unsigned long long)n, ms / reps,
+         n * 24.0 / (ms / reps * 1e6));
+  hipFree(out);
+  return 0;
+}
