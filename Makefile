@@ -13,7 +13,7 @@ HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/
             raikv_amd/csrc/bs_meow.hpp raikv_amd/csrc/kvh_var.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
 CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/host_latency tests/cpp/paths_gpu \
-             tools/copy_peak tools/fetch_calib
+             tools/copy_peak tools/fetch_calib tools/scatter2_probe
 
 KV_LIB   := raikv_amd/libkvh_kv.so
 
@@ -92,3 +92,7 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle cpptests clean experiments
+
+# f2 pass-2 write-pattern probe
+tools/scatter2_probe: tools/scatter2_probe.hip
+	$(HIPCC) $(HIPFLAGS) -Wno-unused-result -o $@ $<
