@@ -3,6 +3,7 @@
 // 2048, 128 runs of 16 records per tile, one 8-byte word per lane stored:
 //   mode 1 (pass-1 shape): run d of tile t -> region d (n/128 records each)
 //          at record t*16
+//   mode 3: mode 2 with the tile first read from the previous launch's output
 //   mode 2 (pass-2 shape): tiles grouped 381 per first-level region; run d2
 //          of the k-th tile of region d1 -> sub-region (d1, d2) (n/16384
 //          records each) at record k*16
@@ -34,12 +35,50 @@ __global__ void __launch_bounds__(512) probe(uint64_t* __restrict__ out, uint64_
   }
 }
 
+// mode 3: the pass-2 stream preceded, in the same kernel, by a coalesced read
+// of the tile's 2048 records from `in` (written by the previous launch, as
+// f2's pass 2 reads pass 1's output); each read word is folded into the store
+__global__ void __launch_bounds__(512) probe_rd(const uint64_t* __restrict__ in, uint64_t* __restrict__ out, uint64_t n) {
+  __shared__ uint64_t st[3 * kTile];
+  const uint64_t ntiles = n / kTile, t = blockIdx.x;
+  if (t >= ntiles) return;
+  for (uint32_t w = threadIdx.x; w < 3 * kTile; w += 512) st[w] = in[t * 3 * kTile + w];
+  __syncthreads();
+  const uint64_t region1 = n / kRuns, tiles_per_d1 = ntiles / kRuns, sub = region1 / kRuns;
+  for (uint32_t w = threadIdx.x; w < 3 * kTile; w += 512) {
+    const uint32_t p = w / 3, part = w - 3 * p, run = p / kRun, in_ = p % kRun;
+    const uint64_t d1 = t / tiles_per_d1 < kRuns ? t / tiles_per_d1 : kRuns - 1, k = t - d1 * tiles_per_d1;
+    const uint64_t rec = d1 * region1 + run * sub + (k * kRun + in_) % sub;
+    out[rec * 3 + part] = st[(w + 3 * 37) % (3 * kTile)];
+  }
+}
+
 int main(int argc, char** argv) {
   const int mode = argc > 1 ? atoi(argv[1]) : 1;
   const uint64_t n = (argc > 2 ? atoll(argv[2]) : 100) * 1000000ull;
   const int reps = argc > 3 ? atoi(argv[3]) : 10;
   uint64_t* out;
   if (hipMalloc(&out, n * 24) != hipSuccess) return 1;
+  if (mode == 3) {  // in = the previous launch's mode-1 output; out written in the pass-2 shape
+    uint64_t* in;
+    if (hipMalloc(&in, n * 24) != hipSuccess) return 1;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+    const uint32_t grid = (uint32_t)(n / kTile);
+    float tot = 0;
+    for (int r = 0; r < reps; r++) {
+      hipLaunchKernelGGL(probe, dim3(grid), dim3(512), 0, 0, in, n, 1);
+      (void)hipEventRecord(a);
+      hipLaunchKernelGGL(probe_rd, dim3(grid), dim3(512), 0, 0, in, out, n);
+      (void)hipEventRecord(b);
+      (void)hipEventSynchronize(b);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, a, b);
+      tot += ms;
+    }
+    printf("{\"mode\": 3, \"n\": %llu, \"ms\": %.4f}\n", (unsigned long long)n, tot / reps);
+    return 0;
+  }
   hipEvent_t a, b;
   hipEventCreate(&a); hipEventCreate(&b);
   const uint32_t grid = (uint32_t)(n / kTile);
