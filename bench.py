@@ -382,6 +382,64 @@ def load_traffic(config_name: str):
     return None, None
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(rank: int, world: int, port: int, base=None) -> dict:
+    """The environment torch.distributed.run would give rank `rank` of a
+    one-node job (one process per GPU; rendezvous on 127.0.0.1)."""
+    env = dict(os.environ if base is None else base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", ROLE_RANK=str(rank), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def launch_ranks(world: int, argv, exe=None, port=None, poll_s: float = 0.2) -> int:
+    """`bench.py --gpus N` with no WORLD_SIZE: start N fresh rank processes
+    of this script (the parent has imported neither torch nor HIP), print
+    rank 0's JSON line, and return non-zero if any rank fails (the others are
+    then terminated: exact PIDs this function started)."""
+    import subprocess
+    import threading
+    port = port or free_port()
+    cmd = [sys.executable, os.path.abspath(__file__)] if exe is None else list(exe)
+    procs, lines = [], []
+    for r in range(world):
+        procs.append(subprocess.Popen(cmd + list(argv), env=rank_env(r, world, port),
+                                      stdout=subprocess.PIPE if r == 0 else 2, text=True))
+    reader = threading.Thread(target=lambda: lines.extend(procs[0].stdout), daemon=True)
+    reader.start()
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        failed = next((r for r, p in enumerate(procs) if p.poll() not in (None, 0)), None)
+        time.sleep(poll_s)
+    if failed is None:
+        failed = next((r for r, p in enumerate(procs) if p.returncode != 0), None)
+    if failed is not None:
+        log(f"bench.py: rank {failed} exited with {procs[failed].returncode}; stopping the other ranks")
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    reader.join(timeout=30)
+    js = [l for l in lines if l.lstrip().startswith("{")]
+    if failed is None and js:
+        print(js[-1].rstrip("\n"), flush=True)
+        return 0
+    for l in lines:
+        log(l.rstrip("\n"))
+    return 1
+
+
 def resolve_config(name, rank: int, world: int, keys_override: int = 0):
     """The workload of this rank: c1 at N = 1 and c4g (BASELINE configs[4]:
     one global 1B x 32 B batch, strong scaling) at N > 1 unless named; a
@@ -403,7 +461,8 @@ def resolve_config(name, rank: int, world: int, keys_override: int = 0):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks; without WORLD_SIZE in the environment bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
@@ -418,7 +477,21 @@ def main():
                     help="untimed launches before the warmup, until the engine clock has left its post-idle "
                          "power transient (DESIGN.md §4.5); 0 disables")
     ap.add_argument("--no-copy-peak", action="store_true", help="skip the achievable-peak copy probe")
+    ap.add_argument("--parity-keys", type=int, default=20_000,
+                    help="keys of the timed launch's output checked against the reference after the timed region")
     args = ap.parse_args()
+
+    # N ranks: under torch.distributed.run WORLD_SIZE is set and must agree
+    # with --gpus; without it bench.py starts the N ranks itself (fresh child
+    # processes, before anything here has touched torch or the GPU)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is not None and int(env_world) != args.gpus:
+            log(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}: refusing to measure "
+                f"{env_world} rank(s) as {args.gpus} GPU(s)")
+            sys.exit(2)
+    elif args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
 
@@ -554,6 +627,17 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     wall = kdist.reduce_max(wall, world)
 
+    # parity of the bytes just timed (each rank its own shard), after the timed region
+    T = {k: v for k, v in locals().items() if k in ("keys", "offs_np", "out", "hashes", "pos", "crc_out", "s_h", "s_ho",
+                                                     "s_io", "sorter", "geom", "text", "t_offs", "t_lens", "t_out",
+                                                     "t_cnt")}
+    try:
+        par = timed_parity(args.config, cfg, seed, T, args.parity_keys, rank) if args.parity_keys > 0 else None
+    except Exception as e:  # reported, never hidden: a failed check is not a pass
+        par = {"checked": 0, "mismatches": None, "error": repr(e)[:300]}
+    del T
+    per_rank = kdist.gather({"rank": rank, "kernel_ms": kern_ms, "keys": n, "parity": par}, world)
+
     units = cfg["tokens"] if cfg.get("ingest") else n * arity
     # keys for the f1/f3/f4 configs; a global batch counts its keys once
     n_hash = (n_global * arity if cfg.get("global_batch") else units * world) * args.steps
@@ -591,6 +675,18 @@ def main():
         "hashes_per_s_aggregate": n_hash / wall,
         "lds_roofline": lds_line(args.config, units, kern_ms),
     }
+    if par is not None:
+        pr = [p["parity"] for p in per_rank]
+        res["parity"] = {"checked": sum(p.get("checked") or 0 for p in pr),
+                         "mismatches": (None if any(p.get("mismatches") is None for p in pr)
+                                        else sum(p["mismatches"] for p in pr)),
+                         "against": pr[0].get("against", pr[0].get("error")),
+                         "sample": f"{args.parity_keys} random keys + first + last of each rank's timed output",
+                         **({"errors": [p["error"] for p in pr if "error" in p]} if any("error" in p for p in pr)
+                            else {})}
+    if world > 1:
+        res["per_gpu"] = [{"rank": p["rank"], "keys": p["keys"], "kernel_ms": p["kernel_ms"],
+                           "hashes_per_s": p["keys"] * arity / (p["kernel_ms"] * 1e-3)} for p in per_rank]
     res["roofline"]["guide_copy_peak"] = GUIDE_COPY_GBS
     res["roofline"]["frac_vs_guide_copy"] = achieved / GUIDE_COPY_GBS
     if rank == 0 and world == 1 and not args.no_copy_peak:
@@ -619,6 +715,87 @@ def main():
     kdist.finalize(world)
     if rank == 0:
         print(json.dumps(res), flush=True)
+
+
+def timed_parity(name, cfg, seed, T, k: int, rank: int) -> dict:
+    """Check this rank's output of the LAST timed launch (still in HBM) on a
+    sample of k keys plus the first and the last, against the compiled
+    reference (tests/bench_parity.py; the checker, called after the timed
+    region).  T holds the run's device tensors by name."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import bench_parity as bp  # checker only
+    from raikv_amd.workload import C3_SEEDS
+    n, L, arity = cfg["n"], cfg["key_len"], cfg["arity"]
+    t0 = time.perf_counter()
+    u64 = lambda t: t.cpu().numpy().view(np.uint64)
+
+    def gather_bytes(buf, starts, lens):
+        """the bytes of spans (starts, lens) of a device buffer, packed, + local offsets"""
+        lo = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        if lo[-1] == 0:
+            return np.zeros(0, np.uint8), lo.astype(np.uint64)
+        pos = np.repeat(np.asarray(starts, np.int64) - lo[:-1], lens) + np.arange(lo[-1], dtype=np.int64)
+        return buf[torch.from_numpy(pos).to(buf.device)].cpu().numpy(), lo.astype(np.uint64)
+
+    if cfg.get("sort"):
+        s_h, s_ho, s_io, geom = T["s_h"], T["s_ho"], T["s_io"], T["geom"]
+        # a marked duplicate's h1 is 0 (ctest.c:96-104): its slot is compared through its item's input pair
+        in_slots = ((s_h[s_io, 0] & int(geom.ht_mod_mask)) * int(geom.ht_mod_fraction)) >> int(geom.ht_mod_shift)
+        descents = int((in_slots[1:] < in_slots[:-1]).sum())
+        perm_ok = bool(torch.equal(torch.sort(s_io).values, torch.arange(n, device=s_io.device)))
+        zeroed = int((s_ho[:, 0] == 0).sum())
+        idx = torch.from_numpy(bp.sample_indices(n, k, seed=rank)).to(s_ho.device)
+        items = s_io[idx]
+        r = bp.ht_order(descents, perm_ok, u64(s_h[items]), u64(s_ho[idx]), int(T["sorter"].dups.item()), zeroed,
+                        (geom.ht_mod_mask, geom.ht_mod_fraction, geom.ht_mod_shift), u64(in_slots[idx]))
+    elif cfg.get("ingest"):
+        cnt = int(T["t_cnt"].item())
+        idx = bp.sample_indices(cnt, k, seed=rank)
+        ti = torch.from_numpy(idx).to(T["t_offs"].device)
+        o, ln = T["t_offs"][ti].cpu().numpy(), T["t_lens"][ti].cpu().numpy().astype(np.int64)
+        text = T["text"]
+        kb, lo = gather_bytes(text, o, ln)
+        toks = [kb[lo[j]:lo[j + 1]] for j in range(len(idx))]
+        tb = text.numel()
+        nb = torch.from_numpy(np.stack([o - 1, o + ln]).clip(0, tb - 1)).to(text.device)
+        nbv = text[nb].cpu().numpy().astype(np.int64)
+        before = np.where(o > 0, nbv[0], -1)
+        after = np.where(o + ln < tb, nbv[1], -1)
+        r = bp.spans(toks, before, after, u64(T["t_out"][ti]), seed)
+    elif cfg.get("crc"):
+        idx = bp.sample_indices(n, k, seed=rank)
+        ti = torch.from_numpy(idx).cuda()
+        if cfg["var"]:
+            offs_np = T["offs_np"]
+            kb, lo = gather_bytes(T["keys"], offs_np[idx], (offs_np[idx + 1] - offs_np[idx]).astype(np.int64))
+        else:
+            kb = T["keys"].view(n, L)[ti].cpu().numpy().reshape(-1)
+            lo = np.arange(len(idx) + 1, dtype=np.uint64) * np.uint64(L)
+        r = bp.crc_var(kb, lo, T["crc_out"][ti].cpu().numpy().view(np.uint32), 0)
+    elif cfg.get("positions"):
+        idx = bp.sample_indices(n, k, seed=rank)
+        ti = torch.from_numpy(idx).cuda()
+        g = F1_GEOM
+        r = bp.positions(u64(T["hashes"][ti]), u64(T["pos"][ti]),
+                         (g["map_size"], g["hash_entry_size"], g["hash_value_ratio"], g["cuckoo_buckets"],
+                          g["cuckoo_arity"]))
+        if cfg["positions"] == "fused":
+            rh = bp.meow_fixed(T["keys"].view(n, L)[ti].cpu().numpy(), L, u64(T["hashes"][ti]), [seed], fixup=True)
+            r["mismatches"] += rh["mismatches"]
+            r["against"] = f"hashes: {rh['against']}; positions: {r['against']}"
+    elif cfg["var"]:
+        idx = bp.sample_indices(n, k, seed=rank)
+        offs_np = T["offs_np"]
+        kb, lo = gather_bytes(T["keys"], offs_np[idx], (offs_np[idx + 1] - offs_np[idx]).astype(np.int64))
+        r = bp.meow_var(kb, lo, u64(T["out"][torch.from_numpy(idx).cuda()]), seed)
+    else:
+        idx = bp.sample_indices(n, k, seed=rank)
+        ti = torch.from_numpy(idx).cuda()
+        seeds = [seed] if arity == 1 else list(C3_SEEDS[:arity])
+        r = bp.meow_fixed(T["keys"].view(n, L)[ti].cpu().numpy(), L, u64(T["out"][ti]), seeds)
+    r["seconds"] = round(time.perf_counter() - t0, 2)
+    return r
 
 
 def copy_peak(alg_bytes):

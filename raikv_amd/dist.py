@@ -42,6 +42,26 @@ def reduce_max(x: float, world: int) -> float:
     return float(t.item())
 
 
+def gather(obj, world: int) -> list:
+    """Every rank's `obj` (a small JSON-able value), in rank order."""
+    if world <= 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def sum_int(x: int, world: int) -> int:
+    if world <= 1:
+        return int(x)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(x)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
+
+
 def finalize(world: int) -> None:
     if world > 1:
         import torch.distributed as dist
