@@ -13,7 +13,7 @@ HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/
             raikv_amd/csrc/bs_meow.hpp raikv_amd/csrc/kvh_var.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
 CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/host_latency tests/cpp/paths_gpu \
-             tools/copy_peak tools/fetch_calib tools/scatter2_probe
+             tools/copy_peak tools/fetch_calib tools/scatter2_probe tools/stream_forms tools/scatter2_real
 
 KV_LIB   := raikv_amd/libkvh_kv.so
 
@@ -79,6 +79,10 @@ tests/cpp/host_latency: tests/cpp/host_latency.cpp $(LIB) include/kvh.h
 tools/copy_peak: tools/copy_peak.hip
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
 
+# measurement: the streaming forms compared on one box after one settle
+tools/stream_forms: tools/stream_forms.hip
+	$(HIPCC) $(HIPFLAGS) -o $@ $<
+
 # measurement: FETCH_SIZE calibration for gather access patterns
 tools/fetch_calib: tools/fetch_calib.hip
 	$(HIPCC) $(HIPFLAGS) -o $@ $<
@@ -92,6 +96,13 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle cpptests clean experiments
+
+# f2: the real k_tw_scatter2 under ablations: ht_sort.hip
+# compiled into the probe, the product's other objects linked
+PROBE_OBJS := $(filter-out raikv_amd/csrc/ht_sort.o,$(OBJS))
+tools/scatter2_real: tools/scatter2_real.hip raikv_amd/csrc/ht_sort.hip $(PROBE_OBJS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) $(INC) -c -o tools/scatter2_real.o $<
+	$(HIPCC) $(HIPFLAGS) -o $@ tools/scatter2_real.o $(PROBE_OBJS)
 
 # f2 pass-2 write-pattern probe
 tools/scatter2_probe: tools/scatter2_probe.hip

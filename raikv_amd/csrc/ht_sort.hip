@@ -616,11 +616,13 @@ __device__ __forceinline__ void bk_bitonic(Rec* __restrict__ R, uint64_t len, co
 // Stable three-way partition of R[0, len) around the key of q (key64, h1,
 // h2) into T: T = [less | equal | greater], each part in its input order.
 // One workgroup, blocks of kSB records in order: per block, each class's
-// wave ballots and the wave counts give the positions; running totals carry
-// across blocks.  Returns the sizes of the less and equal parts.
+// wave ballots and the wave counts give the positions; the running totals
+// are kept in every thread's registers (all threads sum the same counts),
+// and the counts alternate between two LDS buffers, so a block costs one
+// barrier.  Returns the sizes of the less and equal parts.
 __device__ __forceinline__ void bk_partition3(const Rec* __restrict__ R, Rec* __restrict__ T, uint64_t len,
                                               const Rec& q, const HtGeom& g, uint32_t sb, uint64_t* n_less,
-                                              uint64_t* n_eq, uint32_t (&wc)[3][kSB / 64], uint64_t (&tot)[3]) {
+                                              uint64_t* n_eq, uint32_t (&wc)[2][3][kSB / 64]) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint64_t qk = sort_key64(g, sb, q.h1);
   auto cls = [&](const Rec& x) -> uint32_t {  // 0 less, 1 equal, 2 greater than q's key
@@ -643,10 +645,10 @@ __device__ __forceinline__ void bk_partition3(const Rec* __restrict__ R, Rec* __
   for (int q2 = 0; q2 < kSB / 64; q2++) { L0 += ws0[q2]; L1 += ws1[q2]; }
   *n_less = L0;
   *n_eq = L1;
-  if (tid == 0) { tot[0] = 0; tot[1] = L0; tot[2] = L0 + L1; }
-  __syncthreads();
+  uint64_t tot[3] = {0, L0, L0 + L1};
   // pass 2: stable scatter
-  for (uint64_t b0 = 0; b0 < len; b0 += kSB) {
+  uint32_t p = 0;
+  for (uint64_t b0 = 0; b0 < len; b0 += kSB, p ^= 1u) {
     const uint64_t t = b0 + tid;
     const bool v = t < len;
     Rec x;
@@ -657,43 +659,87 @@ __device__ __forceinline__ void bk_partition3(const Rec* __restrict__ R, Rec* __
     for (uint32_t k = 0; k < 3; k++) {
       const uint64_t m = __ballot(c == k);
       if (c == k) below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      if (lane == 0) wc[k][w] = (uint32_t)__popcll(m);
+      if (lane == 0) wc[p][k][w] = (uint32_t)__popcll(m);
     }
+    // one barrier: the next block writes the other buffer, and no thread can
+    // reach the block after that before every thread has passed this one's reads
     __syncthreads();
+    uint32_t before[3] = {0, 0, 0}, all[3] = {0, 0, 0};
+#pragma unroll
+    for (uint32_t q2 = 0; q2 < kSB / 64; q2++) {
+#pragma unroll
+      for (uint32_t k = 0; k < 3; k++) {
+        const uint32_t x2 = wc[p][k][q2];
+        before[k] += q2 < w ? x2 : 0u;
+        all[k] += x2;
+      }
+    }
     if (v) {
-      uint64_t pos = tot[c] + below;
-      for (uint32_t q2 = 0; q2 < w; q2++) pos += wc[c][q2];
-      T[pos] = x;
+      const uint64_t at = c == 0 ? tot[0] + before[0] : c == 1 ? tot[1] + before[1] : tot[2] + before[2];
+      T[at + below] = x;
     }
-    __syncthreads();
-    if (tid < 3) {
-      uint64_t s = 0;
-      for (int q2 = 0; q2 < kSB / 64; q2++) s += wc[tid][q2];
-      tot[tid] += s;
-    }
-    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) tot[k] += all[k];
   }
+  __syncthreads();
+}
+
+// The pivot of a k_bk_long partition: wave 0 samples 64 records spread over
+// R[0, len) and takes the (h1, h2) that occurs most often among them (ties:
+// the lowest lane; with no repeat, the middle sample).  A key holding a
+// share p of the range is the pivot unless it shows up in fewer samples than
+// some other key, which for p >= 10 % of a bucket is vanishingly rare
+// (64 draws), so a hot key goes to the equal part -- already ordered -- in
+// the first partition whatever its share (the middle record was
+// the hot key only with probability p).  Written to *q; ends with a barrier.
+__device__ __forceinline__ void bk_mode_pivot(const Rec* __restrict__ R, uint64_t len, Rec* q) {
+  const uint32_t tid = threadIdx.x;
+  if (tid < 64) {
+    const Rec s = R[(len * tid) >> 6];
+    uint32_t c = 0;
+    for (int j = 0; j < 64; j++) {
+      const uint64_t o1 = (uint64_t)__shfl((unsigned long long)s.h1, j, 64);
+      const uint64_t o2 = (uint64_t)__shfl((unsigned long long)s.h2, j, 64);
+      c += (o1 == s.h1 && o2 == s.h2) ? 1u : 0u;
+    }
+    uint32_t best = c;
+    for (int o = 32; o >= 1; o >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    const uint64_t m = __ballot(c == best);
+    const uint32_t pick = best > 1 ? (uint32_t)__builtin_ctzll(m) : 32u;
+    if (tid == pick) *q = s;
+  }
+  __syncthreads();
 }
 
 // Buckets B3 could not sort in LDS, one workgroup each.  A bucket already in
 // the full order (with the tile-stable two-pass scatter a bucket's records
 // arrive in input order, so a bucket holding one repeated key) skips the
 // network.  Otherwise, when `tmp` is given (the two-pass path: its first
-// record buffer is free by now), a stable three-way partition around the
-// bucket's middle record's key: the equal part is then already in order
-// (all one key, input order), and only the other two parts go through the
-// bitonic network -- a hot key repeated millions of times (the KVH_DEDUP
-// case) among a bucket's ordinary keys costs two passes plus the
-// network over the ordinary keys instead of O(R log^2 R) over all of them
-// on one workgroup.  Without `tmp`, the whole bucket through the network.
+// record buffer is free by now), a quicksort of stable three-way partitions
+// around the sampled-mode pivot (bk_mode_pivot): each equal part is final
+// (one key, input order), the less and greater parts are partitioned again
+// while longer than kBkNet records, and the parts at or below it go through
+// the bitonic network.  A hot key repeated millions of times (the KVH_DEDUP
+// case) among a bucket's ordinary keys, or several of them,
+// costs a few passes instead of O(R log^2 R) network steps on one
+// workgroup.  The smaller part is taken first (stack depth <= log2 R) and a
+// bucket gets at most kBkParts partitions before the network takes the
+// rest, so the loop ends on any input.  Without `tmp`, the whole bucket
+// through the network.
+constexpr uint64_t kBkNet = 2048;   // parts at or below this size: bitonic network in LDS (64 KiB)
+constexpr int kBkStack = 40;        // > log2 of any bucket length
+constexpr int kBkParts = 256;       // partitions per bucket before the (global) network takes over
+
 __global__ void __launch_bounds__(kSB)
 k_bk_long(Rec* __restrict__ recs, Rec* __restrict__ tmp, const uint32_t* __restrict__ cnt,
           const uint32_t* __restrict__ start, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
           uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
           const uint32_t* __restrict__ novf, const uint32_t* __restrict__ ovf) {
   __shared__ uint32_t wsum[kSB / 64];
-  __shared__ uint32_t wc[3][kSB / 64];
-  __shared__ uint64_t tot[3];
+  __shared__ uint32_t wc[2][3][kSB / 64];
+  __shared__ Rec pivot;
+  __shared__ uint64_t st_lo[kBkStack], st_len[kBkStack];
+  __shared__ Rec S[kBkNet];
   const uint32_t count = *novf, tid = threadIdx.x;
   uint32_t d = 0;
   for (uint32_t r = blockIdx.x; r < count; r += gridDim.x) {
@@ -705,13 +751,47 @@ k_bk_long(Rec* __restrict__ recs, Rec* __restrict__ tmp, const uint32_t* __restr
     if (block_sum(unordered, wsum)) {
       if (tmp) {
         Rec* Tm = tmp + start[b];
-        const Rec q = R[len / 2];
-        uint64_t nl = 0, ne = 0;
-        bk_partition3(R, Tm, len, q, g, sb, &nl, &ne, wc, tot);
-        for (uint64_t t = tid; t < len; t += kSB) R[t] = Tm[t];
+        // workgroup-uniform stack of parts (offset, length); thread 0 writes,
+        // every thread reads after the barrier that follows
+        int sp = 1, parts = 0;
+        if (tid == 0) { st_lo[0] = 0; st_len[0] = len; }
         __syncthreads();
-        bk_bitonic(R, nl, g, sb);
-        bk_bitonic(R + nl + ne, len - nl - ne, g, sb);
+        while (sp > 0) {
+          sp--;
+          const uint64_t lo = st_lo[sp], l = st_len[sp];
+          __syncthreads();
+          if (l <= kBkNet) {  // the part in LDS, the network there, back
+            for (uint64_t t = tid; t < l; t += kSB) S[t] = R[lo + t];
+            __syncthreads();
+            bk_bitonic(S, l, g, sb);
+            for (uint64_t t = tid; t < l; t += kSB) R[lo + t] = S[t];
+            __syncthreads();
+            continue;
+          }
+          if (parts >= kBkParts || sp + 2 > kBkStack) {
+            bk_bitonic(R + lo, l, g, sb);
+            __syncthreads();
+            continue;
+          }
+          parts++;
+          bk_mode_pivot(R + lo, l, &pivot);
+          const Rec q = pivot;
+          uint64_t nl = 0, ne = 0;
+          bk_partition3(R + lo, Tm + lo, l, q, g, sb, &nl, &ne, wc);
+          for (uint64_t t = tid; t < l; t += kSB) R[lo + t] = Tm[lo + t];
+          const uint64_t ng = l - nl - ne;
+          // push the larger part first, so the smaller one is taken next
+          const bool less_first = nl >= ng;
+          const uint64_t a_lo = less_first ? lo : lo + nl + ne, a_len = less_first ? nl : ng;
+          const uint64_t b_lo = less_first ? lo + nl + ne : lo, b_len = less_first ? ng : nl;
+          if (tid == 0) {
+            int s = sp;
+            if (a_len > 1) { st_lo[s] = a_lo; st_len[s] = a_len; s++; }
+            if (b_len > 1) { st_lo[s] = b_lo; st_len[s] = b_len; s++; }
+          }
+          sp += (a_len > 1) + (b_len > 1);
+          __syncthreads();
+        }
       } else {
         bk_bitonic(R, len, g, sb);
       }
@@ -1034,10 +1114,18 @@ k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start
   }
 }
 
+// MODE 0 is the product.  The others exist for tools/scatter2_real.hip
+// (the round-4 attribution of this kernel's WRITE_SIZE) and
+// are never launched by the library: 1 stores to `dummy` (same offsets, a
+// buffer nothing reads), 2 replaces the recA/bA loads by values made from the
+// position (same digits, no loads), 3 loads recA/bA non-temporally, 4 stores
+// non-temporally.
+template <int MODE>
 __global__ void __launch_bounds__(kTwT)
 k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
               const uint32_t* __restrict__ cnt1, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
-              const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, R24* __restrict__ rec) {
+              const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, R24* __restrict__ rec,
+              R24* __restrict__ dummy) {
   __shared__ TwShared S;
   const uint32_t tid = threadIdx.x, nb2 = 1u << B2, j = xcd_tile(blockIdx.x, gridDim.x);
   uint32_t d1, p0, p1;
@@ -1051,8 +1139,19 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
     v[k] = p < p1;
     dg[k] = 0;
     if (v[k]) {
-      r[k] = recA[p];
-      dg[k] = bA[p] & (nb2 - 1);
+      if constexpr (MODE == 2) {
+        r[k].h1 = p; r[k].h2 = ~(uint64_t)p; r[k].item = p;
+        dg[k] = (p * 2654435761u >> 9) & (nb2 - 1);
+      } else if constexpr (MODE == 3) {
+        const uint64_t* q = (const uint64_t*)(recA + p);
+        r[k].h1 = __builtin_nontemporal_load(q);
+        r[k].h2 = __builtin_nontemporal_load(q + 1);
+        r[k].item = __builtin_nontemporal_load(q + 2);
+        dg[k] = __builtin_nontemporal_load(bA + p) & (nb2 - 1);
+      } else {
+        r[k] = recA[p];
+        dg[k] = bA[p] & (nb2 - 1);
+      }
     }
   }
   if (tid < nb2) S.gofs[tid] = start[(d1 << B2) | tid] + H2[(uint64_t)j * nb2 + tid];
@@ -1067,10 +1166,15 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
   // one 8-byte word per lane: a store instruction covers ~21 whole
   // consecutive records (512 B) instead of the same third of 64 records
   const uint64_t* sw = (const uint64_t*)S.stage;
+  R24* dst = MODE == 1 ? dummy : rec;
   for (uint32_t w = tid; w < 3 * (p1 - p0); w += kTwT) {
     const uint32_t p = w / 3, part = w - 3 * p;
     const uint32_t d = S.dig[p];
-    ((uint64_t*)(rec + (uint64_t)S.gofs[d] + (p - S.lstart[d])))[part] = sw[w];
+    uint64_t* a = ((uint64_t*)(dst + (uint64_t)S.gofs[d] + (p - S.lstart[d]))) + part;
+    if constexpr (MODE == 4)
+      __builtin_nontemporal_store(sw[w], a);
+    else
+      *a = sw[w];
   }
 }
 
@@ -1221,9 +1325,9 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       hipLaunchKernelGGL(k_tw_start2, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
                          nb1, B2, start);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_tw_scatter2, dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA, (const uint16_t*)bA,
+      hipLaunchKernelGGL(k_tw_scatter2<0>, dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA, (const uint16_t*)bA,
                          (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
-                         (const uint32_t*)H2, (const uint32_t*)start, recB);
+                         (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
       if ((rc = launch_done())) return rc;
       if (small_b)
         hipLaunchKernelGGL((k_bk_sort<8000, 12, R24>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,

@@ -23,6 +23,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <atomic>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <condition_variable>
@@ -347,19 +348,51 @@ std::unique_lock<std::mutex> pick_pipe(int dev, HostPipe** P) {
   return std::unique_lock<std::mutex>(g_pipe[dev][0].mu);
 }
 
-// [p, p + bytes) is page-locked host memory (kvh_host_alloc, hipHostMalloc,
-// or kvh_host_register of a range holding it): its first AND last byte are
-// (a range registered only in part takes the bounce buffers, never a DMA
-// past the registered extent).
+// Page-locked ranges made through this API (kvh_host_alloc,
+// kvh_host_register), by base: a batch lying inside ONE of them is DMA'd
+// directly.
+std::mutex g_pin_mu;
+std::map<uintptr_t, size_t> g_pin_ranges;
+void pin_track(const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_ranges[(uintptr_t)p] = bytes;
+}
+void pin_untrack(const void* p) {
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_ranges.erase((uintptr_t)p);
+}
+
 bool pinned_byte(const void* p) {
   hipPointerAttribute_t a;
   const bool pin = hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost;
   (void)hipGetLastError();
   return pin;
 }
+
+// [p, p + bytes) may be DMA'd without a bounce copy: it lies inside one range
+// registered or allocated through this API, or (page-locked memory from
+// elsewhere, e.g. hipHostMalloc) both its ends are page-locked AND the
+// runtime's allocation holding p covers the whole range.  Two registrations
+// with a pageable gap between them therefore take the bounce buffers, never a
+// DMA across the gap; so does a range registered only in part.
 bool is_pinned(const void* p, size_t bytes) {
   if (!bytes) return true;
-  return pinned_byte(p) && (bytes == 1 || pinned_byte((const uint8_t*)p + bytes - 1));
+  const uintptr_t a = (uintptr_t)p;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_ranges.upper_bound(a);
+    if (it != g_pin_ranges.begin()) {
+      --it;
+      if (a >= it->first && a - it->first <= it->second && bytes <= it->second - (a - it->first)) return true;
+    }
+  }
+  if (!pinned_byte(p) || (bytes > 1 && !pinned_byte((const uint8_t*)p + bytes - 1))) return false;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  const bool ok = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess;
+  (void)hipGetLastError();
+  const uintptr_t b = (uintptr_t)base;
+  return ok && size && a >= b && a - b <= size && bytes <= size - (a - b);
 }
 
 // One host batch through H2D -> kernel -> D2H on the current device.
@@ -444,8 +477,11 @@ int host_pipeline(const uint8_t* keys, uint32_t key_len, const uint64_t* offs, s
     if (var && !pin_f) { memcpy(P->hoff[0], offs, 8 * (n + 1)); fsrc = P->hoff[0]; }
     uint64_t* dst = pin_o ? out : P->ho[0];
     if ((nbytes && (e = hipMemcpyAsync(P->dk[0], src, nbytes, hipMemcpyHostToDevice, P->s_k)) != hipSuccess) ||
-        (var && (e = hipMemcpyAsync(P->doff[0], fsrc, 8 * (n + 1), hipMemcpyHostToDevice, P->s_k)) != hipSuccess))
-      return hip_err(e);
+        (var && (e = hipMemcpyAsync(P->doff[0], fsrc, 8 * (n + 1), hipMemcpyHostToDevice, P->s_k)) != hipSuccess)) {
+      rc = hip_err(e);
+      (void)hipStreamSynchronize(P->s_k);  // a copy already queued may still read hk[0]
+      return rc;
+    }
     rc = var ? kvh_meow128_var((const uint8_t*)((uintptr_t)P->dk[0] - (uintptr_t)kb0), P->doff[0], n, s1, s2,
                                P->dout[0], flags, P->s_k)
              : kvh_meow128_fixed(P->dk[0], key_len, n, s1, s2, P->dout[0], flags, P->s_k);
@@ -704,11 +740,13 @@ int kvh_shard_bounds(const uint64_t* offsets, size_t n, int nshards, size_t* bou
 int kvh_host_register(void* p, size_t bytes) {
   if (!p || !bytes) return set_err(KVH_EINVAL);
   const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterDefault);
+  if (e == hipSuccess) pin_track(p, bytes);
   return e == hipSuccess ? set_err(0) : hip_err(e);
 }
 
 int kvh_host_unregister(void* p) {
   if (!p) return set_err(KVH_EINVAL);
+  pin_untrack(p);
   const hipError_t e = hipHostUnregister(p);
   return e == hipSuccess ? set_err(0) : hip_err(e);
 }
@@ -717,11 +755,13 @@ int kvh_host_alloc(void** p, size_t bytes) {
   if (!p) return set_err(KVH_EINVAL);
   *p = nullptr;
   const hipError_t e = hipHostMalloc(p, bytes ? bytes : 1, 0);
+  if (e == hipSuccess) pin_track(*p, bytes ? bytes : 1);
   return e == hipSuccess ? set_err(0) : hip_err(e);
 }
 
 int kvh_host_free(void* p) {
   if (!p) return set_err(0);
+  pin_untrack(p);
   const hipError_t e = hipHostFree(p);
   return e == hipSuccess ? set_err(0) : hip_err(e);
 }
@@ -945,7 +985,7 @@ int kvh_set_tuning(int k, int value) {
     case 2: return set(g_tune_generic, value ? 1 : 0);
     case 3: if (value < 0 || value > 8 || value == 5 || value == 6 || value == 7) return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) && 
+    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) && value != 44 &&
                 !(g_exp.var_knob && g_exp.var_knob(value)))
               return KVH_EINVAL;
             return set(g_tune_var, value);

@@ -298,7 +298,8 @@ int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, ui
 }
 
 // Default (NT, U) per length from tools/tune.py and tools/len_sweep.py
-// sweeps; knobs 0 and 3 select the others.
+// sweeps; knobs 0 and 3 select the others (a pair with no instance at this
+// length runs the length's default).
 template <int L>
 int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
                     uint32_t flags, hipStream_t st, int cus) {
@@ -319,8 +320,9 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
       case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
       case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
       case 208: return launch_k<L, 2, 8>(keys, n, s1, s2, out, flags, st, cus);
-      default: return set_err(KVH_EINVAL);
+      default: break;  // a knob pair without an instance: this length's default
     }
+    return launch_k<L, 4, (L == 16 ? 4 : 2)>(keys, n, s1, s2, out, flags, st, cus);
   } else {
     // per-length defaults (NT, keys per lane) from tools/len_sweep.py over
     // 100M keys (profiles/r03/len_sweep_*.jsonl): 24 B NT4/U4, 40-48 B
@@ -338,7 +340,7 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
       case 203: if constexpr (L >= 40) return launch_k<L, 2, 3>(keys, n, s1, s2, out, flags, st, cus); break;
       default: break;
     }
-    return set_err(KVH_EINVAL);
+    return launch_k<L, dnt, dkpl>(keys, n, s1, s2, out, flags, st, cus);  // no instance: the default
   }
 }
 

@@ -440,6 +440,10 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       hipLaunchKernelGGL((k_var9<2, 12, 192, true>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1,
                          seed2, out, flags);
       return launch_done();
+    case 44:  // round-4 A/B: four tables at 16 copies in the same 64 KiB (LdsTab<5>)
+      hipLaunchKernelGGL((k_var9<5, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
+                         out, flags);
+      return launch_done();
     default:
       break;
   }

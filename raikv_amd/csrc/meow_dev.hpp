@@ -46,17 +46,26 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // ---------------------------------------------------------------- tables
 // LDS-resident, bank-replicated tables.  NT = 4: Td0..Td3 (128 KiB);
 // NT = 2: Td0, Td1 (64 KiB), Td2/Td3 lookups reuse them rotated by 16.
+// NT = 5 (the round-4 A/B layout): Td0..Td3 with 16 copies each in the same
+// 64 KiB -- the four-table round (6 VALU per column instead of 7) at a 2-way
+// bank conflict per lookup (lanes l and l + 16 of a ds_read_b32 lane group
+// share a copy).  Byte address  x<<8 | t<<6 | (lane&15)<<2.
 template <int NT>
 struct LdsTab {
-  static constexpr int kWords = NT * 8192;
+  static constexpr int kTabs = NT == 5 ? 4 : NT;
+  static constexpr int kCopies = NT == 5 ? 16 : 32;
+  static constexpr int kWords = kTabs * 256 * kCopies;
   const uint32_t* lds;
-  uint32_t lw[NT];
+  uint32_t lw[kTabs];
 
   __device__ __forceinline__ explicit LdsTab(const uint32_t* p) : lds(p) {
-    const uint32_t lane = (threadIdx.x & 31u) << 2;
 #pragma unroll
-    for (int t = 0; t < NT; t++)
-      lw[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | lane;
+    for (int t = 0; t < kTabs; t++) {
+      if constexpr (NT == 5)
+        lw[t] = ((uint32_t)t << 6) | ((threadIdx.x & 15u) << 2);
+      else
+        lw[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | ((threadIdx.x & 31u) << 2);
+    }
   }
   __device__ __forceinline__ uint32_t ld(uint32_t byteaddr) const {
     return *(const uint32_t*)((const char*)lds + byteaddr);
@@ -67,7 +76,7 @@ struct LdsTab {
 
   // Td0[a.b0] ^ Td1[b.b1] ^ Td2[c.b2] ^ Td3[d.b3] ^ k  (v_bitop3 0x96 = 3-way XOR)
   __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
-    if constexpr (NT == 4) {
+    if constexpr (kTabs == 4) {
       const uint32_t t0 = ld(__builtin_amdgcn_perm(a, lw[0], sel<0>()));
       const uint32_t t1 = ld(__builtin_amdgcn_perm(b, lw[1], sel<1>()));
       const uint32_t t2 = ld(__builtin_amdgcn_perm(c, lw[2], sel<2>()));
@@ -86,9 +95,9 @@ struct LdsTab {
   // rotation (one v_bitop3) saves the separate XOR of k, so a key used in
   // several rounds (an absorbed chunk twice, the Mixer up to six times) is
   // rotated once.  With four tables the key is used as it is.
-  __device__ __forceinline__ static uint32_t prep(uint32_t k) { return NT == 4 ? k : rotl32(k, 16); }
+  __device__ __forceinline__ static uint32_t prep(uint32_t k) { return kTabs == 4 ? k : rotl32(k, 16); }
   __device__ __forceinline__ uint32_t colk(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t kp) const {
-    if constexpr (NT == 4) {
+    if constexpr (kTabs == 4) {
       return col(a, b, c, d, kp);
     } else {
       const uint32_t t0 = ld(__builtin_amdgcn_perm(a, lw[0], sel<0>()));
@@ -102,10 +111,11 @@ struct LdsTab {
 
 // fill the replicated tables; dword index i = addr >> 2 decodes to
 // copy = i & 31, table = ((i>>14)&1)*2 + ((i>>5)&1), x = (i>>6) & 255
+// (NT = 5: copy = i & 15, table = (i>>4) & 3, x = (i>>6) & 255)
 template <int NT>
 __device__ __forceinline__ void fill_tables(uint32_t* lds) {
   for (uint32_t i = threadIdx.x; i < (uint32_t)LdsTab<NT>::kWords; i += blockDim.x) {
-    const uint32_t t = (((i >> 14) & 1u) << 1) | ((i >> 5) & 1u);
+    const uint32_t t = NT == 5 ? (i >> 4) & 3u : (((i >> 14) & 1u) << 1) | ((i >> 5) & 1u);
     const uint32_t x = (i >> 6) & 255u;
     lds[i] = rotl32(c_td0.v[x], 8 * (int)t);
   }

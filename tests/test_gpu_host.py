@@ -173,27 +173,73 @@ def test_partially_registered_buffers_take_the_bounce_path(kvh):
             assert kvh.lib.kvh_host_unregister(r.ctypes.data) == 0
 
 
+def test_two_registrations_with_a_pageable_gap_bounce(kvh):
+    """a buffer made of two separate kvh_host_register ranges with
+    a pageable page between them has both ends page-locked, but must not be
+    DMA'd as one range (the DMA would run through the gap's missing mapping):
+    the pipeline's own registry sees two registrations and bounces it.  One
+    chunk and several chunks, keys and output split the same way."""
+    n = 200_003
+    keys, offs = zipf_batch(n, 23, lead=1)
+    want = dev_hash_var(kvh, keys, offs, STATIC)
+    page = 4096
+    raw = np.empty(keys.nbytes + 4 * page, dtype=np.uint8)
+    start = (-raw.ctypes.data) % page
+    kv = raw[start:start + keys.nbytes]
+    kv[:] = keys
+    out_raw = np.empty(n * 16 + 4 * page, dtype=np.uint8)
+    ostart = (-out_raw.ctypes.data) % page
+    out = out_raw[ostart:ostart + n * 16].view(np.uint64).reshape(n, 2)
+    regs = []
+    for a in (kv, out.reshape(-1).view(np.uint8)):
+        base = a.ctypes.data
+        tail = (a.nbytes // page - 2) * page  # pages [3, end) registered, page 2 left pageable
+        assert tail > page
+        assert kvh.lib.kvh_host_register(base, 2 * page) == 0
+        assert kvh.lib.kvh_host_register(base + 3 * page, a.nbytes - 3 * page) == 0
+        regs += [base, base + 3 * page]
+    pm = kvh.lib.kvh_set_tuning(15, 1)
+    try:
+        for mib in (1, 64):
+            kvh.lib.kvh_set_tuning(15, mib)
+            out[:] = 0
+            rc = kvh.lib.kvh_meow128_var_host(kv.ctypes.data, offs.ctypes.data, n, C.c_uint64(STATIC[0]),
+                                              C.c_uint64(STATIC[1]), out.ctypes.data, 0)
+            assert rc == 0
+            np.testing.assert_array_equal(out, want)
+    finally:
+        kvh.lib.kvh_set_tuning(15, pm)
+        for r in regs:
+            assert kvh.lib.kvh_host_unregister(r) == 0
+
+
+@pytest.mark.parametrize("tiny", ["default", 0], ids=["tiny_path", "one_chunk_dma"])
 @pytest.mark.parametrize("n", [1, 8, 64, 1024, 16384])
-def test_one_chunk_batches_at_raikv_sizes(kvh, n):
+def test_one_chunk_batches_at_raikv_sizes(kvh, n, tiny):
     """raikv's own batch sizes (8 keys per prefetch pipe, ev_net.h:442; 16K
-    frags per ctest batch, ctest.c:34) take the one-chunk path: pinned and
-    pageable, fixed and variable length, against the device-resident kernel
-    and the oracle."""
-    rng = np.random.default_rng(n)
-    kb = rng.integers(0, 256, n * 16, dtype=np.uint8)
-    want = kvh.meow128_fixed(torch.from_numpy(kb).cuda(), 16, STATIC).cpu().numpy().view(np.uint64)
-    np.testing.assert_array_equal(kvh.meow128_fixed_host(kb, 16, STATIC), want)
-    hk = kvh.host_empty(kb.shape, np.uint8)
-    hk[:] = kb
-    ho = kvh.host_empty((n, 2), np.uint64)
-    kvh.meow128_fixed_host(hk, 16, STATIC, out=ho)
-    np.testing.assert_array_equal(ho, want)
-    keys, offs = zipf_batch(n, 100 + n, lead=2)
-    got = kvh.meow128_var_host(keys, offs, STATIC)
-    np.testing.assert_array_equal(got, dev_hash_var(kvh, keys, offs, STATIC))
-    m = min(n, 500)
-    sub = keys[int(offs[0]):int(offs[m])]
-    np.testing.assert_array_equal(got[:m], orc_var(ORC, sub, offs[:m + 1] - offs[0], STATIC))
+    frags per ctest batch, ctest.c:34): with knob 21 at its default these
+    take the zero-copy k_tiny path, with knob 21 = 0 the one-chunk DMA path
+    (same-stream H2D, kernel, D2H).  Pinned and pageable, fixed
+    and variable length, against the device-resident kernel and the oracle."""
+    prev = kvh.lib.kvh_set_tuning(21, 16384 if tiny == "default" else 0)
+    try:
+        rng = np.random.default_rng(n)
+        kb = rng.integers(0, 256, n * 16, dtype=np.uint8)
+        want = kvh.meow128_fixed(torch.from_numpy(kb).cuda(), 16, STATIC).cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(kvh.meow128_fixed_host(kb, 16, STATIC), want)
+        hk = kvh.host_empty(kb.shape, np.uint8)
+        hk[:] = kb
+        ho = kvh.host_empty((n, 2), np.uint64)
+        kvh.meow128_fixed_host(hk, 16, STATIC, out=ho)
+        np.testing.assert_array_equal(ho, want)
+        keys, offs = zipf_batch(n, 100 + n, lead=2)
+        got = kvh.meow128_var_host(keys, offs, STATIC)
+        np.testing.assert_array_equal(got, dev_hash_var(kvh, keys, offs, STATIC))
+        m = min(n, 500)
+        sub = keys[int(offs[0]):int(offs[m])]
+        np.testing.assert_array_equal(got[:m], orc_var(ORC, sub, offs[:m + 1] - offs[0], STATIC))
+    finally:
+        kvh.lib.kvh_set_tuning(21, prev)
 
 
 def test_multi_device_pool_reused(kvh):

@@ -64,6 +64,26 @@ def test_fixed_fast_kernels_both_table_layouts(kvh, nt):
         kvh.lib.kvh_set_tuning(0, prev)
 
 
+@pytest.mark.parametrize("kpl", [1, 2, 3, 4, 8])
+def test_fixed_every_keys_per_lane_knob(kvh, kpl):
+    """every keys-per-lane knob value kvh_set_tuning accepts hashes
+    every fast length; a (tables, keys per lane) pair without a kernel
+    instance at a length runs that length's default instead of failing."""
+    prev = kvh.lib.kvh_set_tuning(3, kpl)
+    try:
+        assert prev >= 0
+        for nt in (4, 2):
+            pnt = kvh.lib.kvh_set_tuning(0, nt)
+            try:
+                for L in (8, 16, 24, 32, 40, 48, 56, 64):
+                    g = golden(f"fixed_{L}.npz")
+                    np.testing.assert_array_equal(u64(kvh.meow128_fixed(dev(g["keys"]), L, STATIC)), g["out"])
+            finally:
+                kvh.lib.kvh_set_tuning(0, pnt)
+    finally:
+        kvh.lib.kvh_set_tuning(3, prev)
+
+
 def test_all_lengths_0_300_all_paths(kvh):
     g = golden("lengths.npz")
     keys, seeds, out = g["keys"], g["seeds"], g["out"]

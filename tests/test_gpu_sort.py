@@ -249,6 +249,56 @@ def test_hot_key_bound(kvh):
     assert dt < 0.5, dt
 
 
+@pytest.mark.parametrize("inb,hots", [(1_100_000, (900_000,)), (900_000, (600_000, 500_000)),
+                                      (1_000_000, (1_000_000,)), (800_000, (400_000, 400_000, 400_000))],
+                         ids=["one_hot_45pct", "two_hot_30_25pct", "one_hot_50pct", "three_hot_20pct"])
+def test_hot_keys_minority_of_bucket(kvh, inb, hots):
+    """hot keys that are NOT the majority of their bucket, and
+    several hot keys in one bucket.  `inb` distinct pairs whose h1 share the
+    hot keys' top bits (one oversized bucket), the hot keys (`hots` copies
+    each, 20-50 % of that bucket), 4M ordinary pairs elsewhere.  Each
+    partition of the bucket takes the sampled-mode pivot, so every hot key
+    lands in an equal part (already ordered) whatever its share, and the
+    ordinary records are partitioned down to LDS-sized parts.  Output
+    identical to the radix engine; every hot key contiguous, in input order,
+    all but its last copy marked; well under a second."""
+    import time
+    n = 4_000_000 + inb + sum(hots)
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(17)
+    base = 0x0123_4567_89ab_0000
+    h = torch.randint(0, 2**62, (n, 2), dtype=torch.int64, device="cuda", generator=gen)
+    perm = torch.randperm(n, device="cuda", generator=gen)
+    sel = perm[:inb]
+    h[sel, 0] = base + torch.randint(0, 1 << 16, (inb,), dtype=torch.int64, device="cuda", generator=gen)
+    hot, at = [], inb
+    for k, m in enumerate(hots):
+        sel = perm[at:at + m]
+        at += m
+        h[sel, 0] = base + 0x1000 * (k + 1)
+        h[sel, 1] = 0x7777 + k
+        hot.append((base + 0x1000 * (k + 1), 0x7777 + k, m))
+    g = kvh.HtGeom.from_map(64 << 30, 64, 1.0, 4, 4)
+    srt = kvh.HtSorter(g, n)
+    srt.sort(h, dedup=True)  # warm
+    torch.cuda.synchronize()
+    t0 = time.time()
+    oh, oi = srt.sort(h, dedup=True)
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    dups = int(srt.dups.item())
+    with _engine(kvh, 0, 1):
+        rh, ri = srt.sort(h, dedup=True)
+        rd = int(srt.dups.item())
+    assert torch.equal(oh, rh) and torch.equal(oi, ri) and dups == rd >= sum(m - 1 for _, _, m in hot)
+    for h1, h2, m in hot:
+        idx = torch.nonzero((h[oi, 0] == h1) & (h[oi, 1] == h2)).flatten()
+        assert idx.numel() == m and int(idx[-1] - idx[0]) == m - 1  # contiguous
+        assert bool((oi[idx][1:] > oi[idx][:-1]).all())  # input order
+        assert int((oh[idx, 0] == 0).sum()) == m - 1  # all but the last marked
+    assert dt < 0.5, dt
+
+
 def test_full_size_properties(kvh):
     """100M fixed-up hashes of C1 keys with 1% duplicates into a 64 GiB
     table: output slots non-decreasing, items a permutation, rows equal the

@@ -1,0 +1,178 @@
+// tools/stream_forms.hip -- which streaming form reaches the highest HBM rate
+// for the key-hash traffic shape on this box (measurement infrastructure for
+// DESIGN.md §4.3; not part of the product).
+//
+// Every form moves the same bytes: n 16-byte items read and n written (the C1
+// traffic, 32 B per key; default n = 100M = 3.2 GB).  After one common settle
+// (the k_fixed-shaped copy launched for settle_ms) the forms
+// run interleaved, `rounds` times `reps` launches each; per form the median
+// rate over rounds is printed, with the engine clock each form ran at,
+// measured inside the kernel: one lane of every 64th workgroup reads the
+// shader clock (clock64) and the constant wall clock (wall_clock64) at its
+// start and end and adds the deltas to two counters (vector atomics).
+//
+// Forms:
+//   chunk<U>/g   wave-chunked (wave w owns runs of 64*U consecutive items, every
+//                load/store instruction a contiguous 1 KiB), nt loads and
+//                stores, grid = g workgroups of 1024 per CU -- k_fixed's and
+//                tools/copy_peak's shape at U=4, g=1
+//   f4           the guide's float4 copy: one item per thread, 256-thread
+//                workgroups, plain loads/stores (MI355X_MICROARCH.md: 6.29 TB/s)
+//   f4nt         the same with nt loads/stores
+//   memcpy       hipMemcpyAsync device-to-device
+//
+// usage: stream_forms [n_items=100000000] [settle_ms=500] [rounds=5] [reps=20]
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+struct Clk {
+  unsigned long long dclk, dwall, samples;
+};
+
+__device__ inline void clk_begin(uint64_t& c0, uint64_t& w0) {
+  c0 = clock64();
+  w0 = wall_clock64();
+}
+__device__ inline void clk_end(Clk* ck, uint64_t c0, uint64_t w0) {
+  const uint64_t c1 = clock64(), w1 = wall_clock64();
+  atomicAdd(&ck->dclk, (unsigned long long)(c1 - c0));
+  atomicAdd(&ck->dwall, (unsigned long long)(w1 - w0));
+  atomicAdd(&ck->samples, 1ull);
+}
+
+template <int U>
+__global__ void __launch_bounds__(1024) chunk(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
+                                              Clk* ck) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6, last = n - 1;
+  for (uint64_t b = wave * 64 * U; b < n; b += nw * 64 * U) {
+    v4u X[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      X[u] = __builtin_nontemporal_load(in + (j < last ? j : last));
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      v4u v = X[u];
+      v.x ^= 0x9e3779b9u;
+      __builtin_nontemporal_store(v, out + (j < last ? j : last));
+    }
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
+template <bool NT>
+__global__ void __launch_bounds__(256) f4copy(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
+                                              Clk* ck) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    v4u v = NT ? __builtin_nontemporal_load(in + i) : in[i];
+    v.x ^= 0x9e3779b9u;
+    if (NT)
+      __builtin_nontemporal_store(v, out + i);
+    else
+      out[i] = v;
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+struct Form {
+  const char* name;
+  int kind;  // 0 chunk, 1 f4, 2 f4nt, 3 memcpy
+  int U, g;
+};
+
+int main(int argc, char** argv) {
+  const uint64_t n = argc > 1 ? strtoull(argv[1], 0, 10) : 100000000ull;
+  const double settle_ms = argc > 2 ? atof(argv[2]) : 500.0;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 5;
+  const int reps = argc > 4 ? atoi(argv[4]) : 20;
+  int cus = 0, wall_khz = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  CK(hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, 0));
+  v4u *in = nullptr, *out = nullptr;
+  Clk* ck = nullptr;
+  CK(hipMalloc(&in, n * 16));
+  CK(hipMalloc(&out, n * 16));
+  CK(hipMalloc(&ck, sizeof(Clk)));
+  CK(hipMemset(in, 1, n * 16));
+  const std::vector<Form> forms = {
+      {"chunk4_g1 (k_fixed/copy_peak shape)", 0, 4, 1}, {"chunk4_g2", 0, 4, 2}, {"chunk8_g1", 0, 8, 1},
+      {"chunk2_g2", 0, 2, 2}, {"chunk4_g8", 0, 4, 8},   {"f4 (guide float4 copy)", 1, 0, 0},
+      {"f4nt", 2, 0, 0},      {"memcpy_d2d", 3, 0, 0}};
+  auto launch = [&](const Form& f) {
+    if (f.kind == 0) {
+      const dim3 grid(cus * f.g), block(1024);
+      if (f.U == 2) hipLaunchKernelGGL(chunk<2>, grid, block, 0, 0, in, out, n, ck);
+      if (f.U == 4) hipLaunchKernelGGL(chunk<4>, grid, block, 0, 0, in, out, n, ck);
+      if (f.U == 8) hipLaunchKernelGGL(chunk<8>, grid, block, 0, 0, in, out, n, ck);
+    } else if (f.kind == 1 || f.kind == 2) {
+      const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+      if (f.kind == 1) hipLaunchKernelGGL(f4copy<false>, grid, block, 0, 0, in, out, n, ck);
+      else hipLaunchKernelGGL(f4copy<true>, grid, block, 0, 0, in, out, n, ck);
+    } else {
+      CK(hipMemcpyAsync(out, in, n * 16, hipMemcpyDeviceToDevice, 0));
+    }
+  };
+  auto t0 = std::chrono::steady_clock::now();
+  int settle = 0;
+  for (;;) {
+    launch(forms[0]);
+    CK(hipDeviceSynchronize());
+    settle++;
+    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() >= settle_ms) break;
+  }
+  std::vector<std::vector<double>> rate(forms.size()), ghz(forms.size());
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int r = 0; r < rounds; r++) {
+    for (size_t f = 0; f < forms.size(); f++) {
+      launch(forms[f]);  // one untimed launch at this form's load
+      CK(hipMemset(ck, 0, sizeof(Clk)));
+      CK(hipEventRecord(a, 0));
+      for (int k = 0; k < reps; k++) launch(forms[f]);
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      Clk h;
+      CK(hipMemcpy(&h, ck, sizeof(Clk), hipMemcpyDeviceToHost));
+      rate[f].push_back(32.0 * (double)n / (ms / reps * 1e-3) / 1e12);
+      ghz[f].push_back(h.dwall ? (double)h.dclk / (double)h.dwall * wall_khz * 1e-6 : 0.0);
+    }
+  }
+  auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+  printf("{\"items\": %llu, \"bytes_per_launch\": %llu, \"settle_launches\": %d, \"rounds\": %d, \"reps\": %d, "
+         "\"cus\": %d, \"wall_clock_khz\": %d, \"forms\": [",
+         (unsigned long long)n, (unsigned long long)(32 * n), settle, rounds, reps, cus, wall_khz);
+  for (size_t f = 0; f < forms.size(); f++) {
+    const auto mm = std::minmax_element(rate[f].begin(), rate[f].end());
+    printf("%s{\"form\": \"%s\", \"TBps_median\": %.3f, \"TBps_min\": %.3f, \"TBps_max\": %.3f, "
+           "\"clock_GHz_median\": %.3f}",
+           f ? ", " : "", forms[f].name, med(rate[f]), *mm.first, *mm.second, med(ghz[f]));
+  }
+  printf("]}\n");
+  CK(hipFree(in));
+  CK(hipFree(out));
+  CK(hipFree(ck));
+  return 0;
+}
