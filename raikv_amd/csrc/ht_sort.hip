@@ -585,6 +585,169 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
   }
 }
 
+// B3r (round 4): k_bk_sort's order and marks, with the bucket's records
+// read ONCE and kept in registers.  k_bk_sort reads each record twice -- its
+// key field first, the whole record in sorted order at the end -- and that
+// final gather misses L2 (≈9 MB of buckets in flight per XCD against 4 MB:
+// FETCH 4.0 GB raw for 2.4 GB of records).  Here thread t owns records
+// t, t + 1024, ... (their three words in 3 x PER registers: the three loads
+// of a record slot fetch the same lines, so every byte a line brings is
+// used), files their sort keys, the LDS counting sort runs as in k_bk_sort,
+// and the records leave in three rounds, one field per round: the owners
+// write the field into LDS (aliasing the sort arrays), each thread reads it
+// for its sorted positions and stores it coalesced.  The duplicate test takes
+// the successor's field from the same LDS round.  Runs of equal digit still
+// compare ties through global memory (rare, and those lines are L2-hot).
+template <uint32_t CAP, int D>
+__global__ void __launch_bounds__(kBkT, 1)
+k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
+           uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
+           uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
+           uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
+  static_assert(CAP % kBkT == 0, "records per thread");
+  constexpr uint32_t PER = CAP / kBkT;
+  constexpr uint32_t nd = 1u << D, per = nd / kBkT;
+  struct SortArrays {
+    uint32_t K[CAP];       // key64 bits [B, B + 32) of each record
+    uint16_t dig[CAP];     // its top D bits
+    uint32_t hist[nd];     // digit counts -> starts -> ends
+  };
+  union Lds {
+    SortArrays s;
+    uint64_t X[CAP];  // one field of every record, in record order
+  };
+  __shared__ Lds u;
+  __shared__ uint16_t ord[CAP];  // sorted position -> record
+  __shared__ uint32_t wsum[kBkT / 64], wmax[kBkT / 64];
+  uint32_t* K = u.s.K;
+  uint16_t* dig = u.s.dig;
+  uint32_t* hist = u.s.hist;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t d_total = 0;
+  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t R = cnt[b], base = start[b];
+    if (R == 0) continue;
+    if (R > CAP) {
+      if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+      continue;
+    }
+    const R24* rb = recs + base;
+    uint64_t f0[PER], f1[PER], f2[PER];  // h1, h2, item of records tid + j * kBkT
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tid + j * kBkT;
+      f0[j] = f1[j] = f2[j] = 0;
+      if (r < R) {
+        const R24 x = rb[r];
+        f0[j] = x.h1; f1[j] = x.h2; f2[j] = x.item;
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tid + j * kBkT;
+      if (r < R) {
+        const uint32_t k32 = (uint32_t)((sort_key64(g, sb, f0[j]) << B) >> 32);
+        K[r] = k32;
+        dig[r] = (uint16_t)(k32 >> (32 - D));
+        atomicAdd(&hist[k32 >> (32 - D)], 1u);
+      }
+    }
+    __syncthreads();
+    {  // exclusive scan of the digit counts, and the longest run
+      uint32_t v[per], s = 0, mx = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { v[j] = hist[tid * per + j]; s += v[j]; mx = max(mx, v[j]); }
+      uint32_t inc = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+      if (lane == 63) wsum[w] = inc;
+      if (lane == 0) wmax[w] = mx;
+      __syncthreads();
+      uint32_t wo = 0, bm = 0;
+      for (uint32_t q = 0; q < kBkT / 64; q++) {
+        if (q < w) wo += wsum[q];
+        bm = max(bm, wmax[q]);
+      }
+      if (bm > kBkRun) {  // a run too long for insertion sort: the bitonic path
+        if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+        __syncthreads();
+        continue;
+      }
+      uint32_t run = wo + inc - s;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < R; t += kBkT) ord[atomicAdd(&hist[dig[t]], 1u)] = (uint16_t)t;
+    __syncthreads();
+    // runs of equal digit (hist[d] is now the end of digit d): full order
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) {
+      const uint32_t d = tid * per + j;
+      const uint32_t e = hist[d], s0 = d ? hist[d - 1] : 0u;
+      for (uint32_t a = s0 + 1; a < e; a++) {
+        const uint16_t x = ord[a];
+        const uint32_t kx = K[x];
+        uint32_t c = a;
+        while (c > s0) {
+          const uint16_t y = ord[c - 1];
+          const uint32_t ky = K[y];
+          const bool lt = kx != ky ? kx < ky : bk_less_at(g, sb, rb[x], rb[y], x, y);
+          if (!lt) break;
+          ord[c] = y;
+          c--;
+        }
+        ord[c] = x;
+      }
+    }
+    __syncthreads();  // ord final; the sort arrays are free for the field rounds
+    uint64_t h1v[PER];
+    uint32_t eq1 = 0;  // bit j: sorted position tid + j * kBkT has the same h1 as its successor
+#pragma unroll
+    for (uint32_t f = 0; f < 3; f++) {
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t r = tid + j * kBkT;
+        if (r < R) u.X[r] = f == 0 ? f0[j] : f == 1 ? f1[j] : f2[j];
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t p = tid + j * kBkT;
+        if (p < R) {
+          const uint64_t v = u.X[ord[p]];
+          const bool eq = f < 2 && dedup && p + 1 < R && u.X[ord[p + 1 < R ? p + 1 : p]] == v;
+          if (f == 0) {
+            h1v[j] = v;
+            eq1 |= (eq ? 1u : 0u) << j;
+          } else if (f == 1) {
+            const bool dup = eq && ((eq1 >> j) & 1u);
+            d_total += dup ? 1u : 0u;
+            uint64_t* o = h_out + 2 * ((uint64_t)base + p);
+            o[0] = dup ? 0ull : h1v[j];
+            o[1] = v;
+          } else if (items_out) {
+            items_out[(uint64_t)base + p] = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (dedup && dups) {
+    const uint32_t t = block_sum<kBkT>(d_total, wsum);
+    if (tid == 0 && t) atomicAdd(dups, (unsigned long long)t);
+  }
+}
+
 // all-ascending bitonic network over R[0, len) by the full order (every
 // comparator puts the smaller record at the lower index, so the pad to a
 // power of two is virtual); one workgroup
@@ -1119,7 +1282,7 @@ k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start
 // are never launched by the library: 1 stores to `dummy` (same offsets, a
 // buffer nothing reads), 2 replaces the recA/bA loads by values made from the
 // position (same digits, no loads), 3 loads recA/bA non-temporally, 4 stores
-// non-temporally.
+// non-temporally, 5 reads the records as coalesced 8-byte words (bit-exact).
 template <int MODE>
 __global__ void __launch_bounds__(kTwT)
 k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
@@ -1133,13 +1296,29 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
   R24 r[kTwPer];
   uint32_t dg[kTwPer], pos[kTwPer];
   bool v[kTwPer];
+  // MODE 5: the tile's records read as 8-byte words, word w = tid + m * kTwT
+  // (every load instruction a contiguous 512 B), placed by the record
+  // positions the rank publishes in LDS
+  constexpr int kW = 3 * kTwPer;
+  uint64_t wd[MODE == 5 ? kW : 1];
+  const uint32_t nwords = 3 * (p1 - p0);
+  if constexpr (MODE == 5) {
+    const uint64_t* src = (const uint64_t*)(recA + p0);
+#pragma unroll
+    for (int m = 0; m < kW; m++) {
+      const uint32_t w = tid + (uint32_t)m * kTwT;
+      wd[m] = w < nwords ? src[w] : 0ull;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < kTwPer; k++) {
     const uint32_t p = p0 + (uint32_t)k * kTwT + tid;
     v[k] = p < p1;
     dg[k] = 0;
     if (v[k]) {
-      if constexpr (MODE == 2) {
+      if constexpr (MODE == 5) {
+        dg[k] = bA[p] & (nb2 - 1);
+      } else if constexpr (MODE == 2) {
         r[k].h1 = p; r[k].h2 = ~(uint64_t)p; r[k].item = p;
         dg[k] = (p * 2654435761u >> 9) & (nb2 - 1);
       } else if constexpr (MODE == 3) {
@@ -1156,12 +1335,28 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
   }
   if (tid < nb2) S.gofs[tid] = start[(d1 << B2) | tid] + H2[(uint64_t)j * nb2 + tid];
   tw_rank(dg, v, S, pos);
+  if constexpr (MODE == 5) {
 #pragma unroll
-  for (int k = 0; k < kTwPer; k++)
-    if (v[k]) {
-      S.stage[pos[k]] = r[k];
-      S.dig[pos[k]] = (uint8_t)dg[k];
+    for (int k = 0; k < kTwPer; k++)
+      if (v[k]) {
+        S.bkt[(uint32_t)k * kTwT + tid] = (uint16_t)pos[k];  // record -> its staged position
+        S.dig[pos[k]] = (uint8_t)dg[k];
+      }
+    __syncthreads();
+    uint64_t* sw5 = (uint64_t*)S.stage;
+#pragma unroll
+    for (int m = 0; m < kW; m++) {
+      const uint32_t w = tid + (uint32_t)m * kTwT, q = w / 3u;
+      if (w < nwords) sw5[3u * S.bkt[q] + (w - 3u * q)] = wd[m];
     }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kTwPer; k++)
+      if (v[k]) {
+        S.stage[pos[k]] = r[k];
+        S.dig[pos[k]] = (uint8_t)dg[k];
+      }
+  }
   __syncthreads();
   // one 8-byte word per lane: a store instruction covers ~21 whole
   // consecutive records (512 B) instead of the same third of 64 records
@@ -1329,7 +1524,11 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                          (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
                          (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
       if ((rc = launch_done())) return rc;
-      if (small_b)
+      if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 1)
+        hipLaunchKernelGGL((k_bk_sortr<7168, 12>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
+                           (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
+                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      else if (small_b)
         hipLaunchKernelGGL((k_bk_sort<8000, 12, R24>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                            items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
@@ -1456,7 +1655,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
 
 }  // namespace
 
-namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; std::atomic<int> g_tune_sort_b3{0}; } }
 
 extern "C" {
 

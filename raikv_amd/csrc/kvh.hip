@@ -985,7 +985,7 @@ int kvh_set_tuning(int k, int value) {
     case 2: return set(g_tune_generic, value ? 1 : 0);
     case 3: if (value < 0 || value > 8 || value == 5 || value == 6 || value == 7) return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) && value != 44 &&
+    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) && value != 44 && value != 45 &&
                 !(g_exp.var_knob && g_exp.var_knob(value)))
               return KVH_EINVAL;
             return set(g_tune_var, value);
@@ -999,6 +999,7 @@ int kvh_set_tuning(int k, int value) {
     case 20: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_engine, value);
     case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
     case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_cap, value);
+    case 23: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_b3, value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }

@@ -256,7 +256,7 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 // register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
 // more take wide_window (input order, u64 offsets and lengths).
 
-template <int NT, int NW, int KF, bool PF = false, bool PKY = true>
+template <int NT, int NW, int KF, bool PF = false, bool PKY = true, bool CL = false>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags) {
@@ -373,11 +373,11 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
         const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
         const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
         Blk h;
-        if (al) h = meow_a<true, 48, PF, PKY>(p, kl, safe, K, T);
-        else if (cm == 48) h = meow_a<false, 48, PF, PKY>(p, kl, safe, K, T);
-        else if (cm == 32) h = meow_a<false, 32, PF, PKY>(p, kl, safe, K, T);
-        else if (cm == 16) h = meow_a<false, 16, PF, PKY>(p, kl, safe, K, T);
-        else h = meow_a<false, 0, PF, PKY>(p, kl, safe, K, T);
+        if (al) h = meow_a<true, 48, PF, PKY, CL>(p, kl, safe, K, T);
+        else if (cm == 48) h = meow_a<false, 48, PF, PKY, CL>(p, kl, safe, K, T);
+        else if (cm == 32) h = meow_a<false, 32, PF, PKY, CL>(p, kl, safe, K, T);
+        else if (cm == 16) h = meow_a<false, 16, PF, PKY, CL>(p, kl, safe, K, T);
+        else h = meow_a<false, 0, PF, PKY, CL>(p, kl, safe, K, T);
         stage[rc.y & 255u] = fix ? fixup(h) : h;
       }
     }
@@ -439,6 +439,10 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
     case 25:
       hipLaunchKernelGGL((k_var9<2, 12, 192, true>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1,
                          seed2, out, flags);
+      return launch_done();
+    case 45:  // round-4 A/B: clamped group loads (AChunks::chunk_cl)
+      hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
+                         (uint64_t)n, seed1, seed2, out, flags);
       return launch_done();
     case 44:  // round-4 A/B: four tables at 16 copies in the same 64 KiB (LdsTab<5>)
       hipLaunchKernelGGL((k_var9<5, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,

@@ -462,6 +462,23 @@ struct AChunks {
     }
     return r;
   }
+  // chunk(i) without the zero fill (round 4, knob 7 = 45): with `safe`, a
+  // group past the key's last one is read as that last group instead of
+  // being zeroed -- no per-load compare and exec split.  Bit-exact: the bytes
+  // such a group feeds lie past the key, and meow_a only uses them in the
+  // partial piece (masked to t bytes) or in pieces of states whose lane does
+  // not take them (bsel on C); see meow_a.
+  __device__ __forceinline__ Blk chunk_cl(uint64_t i) const {
+    if (safe) {
+      const uint32_t il = lim ? (uint32_t)((lim - 1) >> 4) : 0u;
+      const uint32_t j = (uint32_t)i < il ? (uint32_t)i : il;
+      const u32x4_a4 v = g[j];
+      Blk r;
+      r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
+      return r;
+    }
+    return chunk(i);
+  }
   __device__ __forceinline__ Blk piece(const Blk& A, const Blk& B) const {
     Blk r;
     r.w[0] = __builtin_amdgcn_alignbyte(A.w[1], A.w[0], bs);
@@ -515,13 +532,14 @@ __device__ __forceinline__ auto f_short(const KGet& K, int i, int) -> decltype(K
 template <class KGet>
 __device__ __forceinline__ Blk f_short(const KGet& K, int i, long) { return K.F(i); }
 
-template <bool AL, int CM, bool PF, bool PKY = false, class Tab, class KGet, class LenT = uint32_t>
+template <bool AL, int CM, bool PF, bool PKY = false, bool CL = false, class Tab, class KGet, class LenT = uint32_t>
 __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const KGet& K, const Tab& T) {
   constexpr bool P0 = AL || CM >= 16, P1 = AL || CM >= 32, P2 = AL || CM >= 48;  // state touched by some lane
   const LenT nb = L >> 6;
   const uint32_t C = (uint32_t)L & 48, t = (uint32_t)L & 15;
   const bool first = nb == 0;
   const AChunks A(p, L, safe);
+  auto ch = [&](uint64_t i) { if constexpr (CL) return A.chunk_cl(i); else return A.chunk(i); };
   const Blk M = K.M();
   // PKY: keys used in more than one round go through LdsTab::prep once
   PKey MP{};
@@ -538,15 +556,15 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
   };
   Blk S0 = bxor(ramp(0), M), S1 = bxor(ramp(1), M), S2 = bxor(ramp(2), M), S3 = bxor(ramp(3), M);
   // groups 4nb .. 4nb+4 (the trail's) once the blocks are absorbed
-  Blk c0 = A.chunk(0), c1, c2 = bzero(), c3 = bzero(), c4 = bzero();
+  Blk c0 = ch(0), c1, c2 = bzero(), c3 = bzero(), c4 = bzero();
   if constexpr (AL && PF) {
     // one block ahead: block b's rounds run while block b+1's groups (and,
     // in the last block, the trail's) are in flight
-    c1 = A.chunk(1); c2 = A.chunk(2); c3 = A.chunk(3); c4 = A.chunk(4);
+    c1 = ch(1); c2 = ch(2); c3 = ch(3); c4 = ch(4);
     if (!first) {
 #define KVH_BLOCK(FIRST)                                                                                   \
   {                                                                                                        \
-    const Blk n1 = A.chunk(i + 5), n2 = A.chunk(i + 6), n3 = A.chunk(i + 7), n4 = A.chunk(i + 8);         \
+    const Blk n1 = ch(i + 5), n2 = ch(i + 6), n3 = ch(i + 7), n4 = ch(i + 8);         \
     const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);     \
     if (FIRST) {                                                                                           \
       S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);                           \
@@ -571,7 +589,7 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
     if constexpr (AL) {
       if (!first) {
         {
-          const Blk c1 = A.chunk(1), c2 = A.chunk(2), c3 = A.chunk(3), c4 = A.chunk(4);
+          const Blk c1 = ch(1), c2 = ch(2), c3 = ch(3), c4 = ch(4);
           const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
           c0 = c4;
           S0 = aesdec(bxor(K.F(0), k0), k0, T); S1 = aesdec(bxor(K.F(1), k1), k1, T);
@@ -579,7 +597,7 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
         }
         for (LenT b = 1; b < nb; b++) {
           const uint64_t i = 4 * (uint64_t)b;
-          const Blk c1 = A.chunk(i + 1), c2 = A.chunk(i + 2), c3 = A.chunk(i + 3), c4 = A.chunk(i + 4);
+          const Blk c1 = ch(i + 1), c2 = ch(i + 2), c3 = ch(i + 3), c4 = ch(i + 4);
           const Blk k0 = A.piece(c0, c1), k1 = A.piece(c1, c2), k2 = A.piece(c2, c3), k3 = A.piece(c3, c4);
           c0 = c4;
           S0 = ad2(S0, k0); S1 = ad2(S1, k1);
@@ -590,10 +608,10 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
     // trail pieces: groups 4nb .. 4nb + CM/16 + 1; piece j feeds state j,
     // the partial piece C/16 (t bytes) state 3
     const uint64_t i0 = 4 * (uint64_t)nb;
-    c1 = A.chunk(i0 + 1);
-    if constexpr (CM >= 16) c2 = A.chunk(i0 + 2);
-    if constexpr (CM >= 32) c3 = A.chunk(i0 + 3);
-    if constexpr (CM >= 48) c4 = A.chunk(i0 + 4);
+    c1 = ch(i0 + 1);
+    if constexpr (CM >= 16) c2 = ch(i0 + 2);
+    if constexpr (CM >= 32) c3 = ch(i0 + 3);
+    if constexpr (CM >= 48) c4 = ch(i0 + 4);
   }
   const Blk q0 = A.piece(c0, c1);
   Blk q1 = bzero(), q2 = bzero(), q3 = bzero();

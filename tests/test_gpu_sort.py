@@ -34,24 +34,30 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
 
 
-ENGINES = [(0, 0), (0, 2), (0, 1), (33, 0)]
-ENGINE_IDS = ["bucketed2", "bucketed1", "radix_u32", "radix_u64"]
+ENGINES = [(0, 0, 0), (0, 0, 1), (0, 2, None), (0, 1, None), (33, 0, None)]
+ENGINE_IDS = ["bucketed2", "bucketed2_sortr", "bucketed1", "radix_u32", "radix_u64"]
 
 
 class _engine:
     """knob 20 = 0 two-pass bucketed (the default), 2 one-pass bucketed, 1
     radix; knob 17 = 33 forces the radix engine on u64 keys over slot + 33 h1
-    bits (0: u32 keys when the prefix fits 31 bits)."""
+    bits (0: u32 keys when the prefix fits 31 bits); knob 23 picks the
+    two-pass path's bucket sort (0 k_bk_sort, 1 the register-resident
+    k_bk_sortr)."""
 
-    def __init__(self, kvh, sort_bits, engine):
-        self.kvh, self.v = kvh, (sort_bits, engine)
+    def __init__(self, kvh, sort_bits, engine, b3=None):
+        self.kvh, self.v, self.b3 = kvh, (sort_bits, engine), b3
 
     def __enter__(self):
         self.prev = (self.kvh.lib.kvh_set_tuning(17, self.v[0]), self.kvh.lib.kvh_set_tuning(20, self.v[1]))
+        if self.b3 is not None:
+            self.prev_b3 = self.kvh.lib.kvh_set_tuning(23, self.b3)
 
     def __exit__(self, *a):
         self.kvh.lib.kvh_set_tuning(17, self.prev[0])
         self.kvh.lib.kvh_set_tuning(20, self.prev[1])
+        if self.b3 is not None:
+            self.kvh.lib.kvh_set_tuning(23, self.prev_b3)
 
 
 @pytest.mark.parametrize("eng", ENGINES, ids=ENGINE_IDS)
@@ -182,7 +188,14 @@ def test_engines_agree(kvh, n, map_size):
         res["cap"] = (oh.clone(), oi.clone(), int(srt.dups.item()))
     finally:
         kvh.lib.kvh_set_tuning(22, prev)
-    for e in (2, 1, "cap"):
+    # the register-resident bucket sort (knob 23 = 1)
+    prev = kvh.lib.kvh_set_tuning(23, 1)
+    try:
+        oh, oi = srt.sort(h, items=items, dedup=True)
+        res["sortr"] = (oh.clone(), oi.clone(), int(srt.dups.item()))
+    finally:
+        kvh.lib.kvh_set_tuning(23, prev)
+    for e in (2, 1, "cap", "sortr"):
         assert torch.equal(res[0][0], res[e][0]) and torch.equal(res[0][1], res[e][1]) and res[0][2] == res[e][2], e
     if n <= 65537:
         og = orc_geom(ORC, map_size, 64, 1.0, 4, 4)

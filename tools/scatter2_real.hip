@@ -14,6 +14,7 @@
 //   2  no recA/bA loads (records and digits made from the position)
 //   3  non-temporal recA/bA loads
 //   4  non-temporal stores
+//   5  the records read as coalesced 8-byte words (checked bit-exact too)
 // Run it under rocprofv3 --pmc WRITE_SIZE FETCH_SIZE: each mode is its own
 // kernel instance in the summary.  Prints one JSON line with the timings.
 //
@@ -89,7 +90,7 @@ int main(int argc, char** argv) {
 #define S2(M) hipLaunchKernelGGL(k_tw_scatter2<M>, dim3(ntB), dim3(kTwT), 0, 0, recA, bA, tbs, cnt1, start1, nb1, B2, \
                                  H2, start, recB, dummy)
     switch (m) { case 0: S2(0); break; case 1: S2(1); break; case 2: S2(2); break; case 3: S2(3); break;
-                 default: S2(4); break; }
+                 case 4: S2(4); break; default: S2(5); break; }
 #undef S2
   };
   // fidelity: mode 0 reproduces the sort's own pass-2 output
@@ -104,10 +105,21 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(b.data(), recB + off, 24 * m, hipMemcpyDeviceToHost));
     same = memcmp(a.data(), b.data(), 24 * m) == 0;
   }
+  // mode 5 (coalesced word loads) must be bit-exact too
+  CK(hipMemset(recB, 0, 24 * n));
+  launch(5);
+  CK(hipDeviceSynchronize());
+  bool same5 = true;
+  for (uint64_t off = 0; off < n && same5; off += n / 7 + 1) {
+    const uint64_t m = std::min<uint64_t>(1000000, n - off);
+    CK(hipMemcpy(a.data(), want + off, 24 * m, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), recB + off, 24 * m, hipMemcpyDeviceToHost));
+    same5 = memcmp(a.data(), b.data(), 24 * m) == 0;
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int modes = 5;
+  const int modes = 6;
   std::vector<double> ms(modes, 0.0);
   for (int r = 0; r < reps; r++)
     for (int m = 0; m < modes; m++) {
@@ -121,8 +133,8 @@ int main(int argc, char** argv) {
     }
   printf("{\"n\": %llu, \"B\": %u, \"B2\": %u, \"tiles\": %u, \"record_bytes\": %llu, \"mode0_equals_sort\": %s, "
          "\"ms\": {\"0_product\": %.4f, \"1_dummy_stores\": %.4f, \"2_no_loads\": %.4f, \"3_nt_loads\": %.4f, "
-         "\"4_nt_stores\": %.4f}}\n",
+         "\"4_nt_stores\": %.4f, \"5_word_loads\": %.4f}, \"mode5_equals_sort\": %s}\n",
          (unsigned long long)n, B, B2, ntiles, (unsigned long long)(24 * n), same ? "true" : "false", ms[0], ms[1],
-         ms[2], ms[3], ms[4]);
-  return same ? 0 : 6;
+         ms[2], ms[3], ms[4], ms[5], same5 ? "true" : "false");
+  return same && same5 ? 0 : 6;
 }
