@@ -1277,12 +1277,19 @@ k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start
   }
 }
 
-// MODE 0 is the product.  The others exist for tools/scatter2_real.hip
-// (the round-4 attribution of this kernel's WRITE_SIZE) and
-// are never launched by the library: 1 stores to `dummy` (same offsets, a
-// buffer nothing reads), 2 replaces the recA/bA loads by values made from the
-// position (same digits, no loads), 3 loads recA/bA non-temporally, 4 stores
-// non-temporally, 5 reads the records as coalesced 8-byte words (bit-exact).
+// MODE selects how a tile's records are read; the library launches MODE 3.
+// tools/scatter2_real.hip ran every mode on the real
+// pass-2 inputs (profiles/r04/s1/s2real*.json): with plain 24-byte record
+// loads (MODE 0, the round-3 kernel) the stride-24 load instructions pull
+// their lines through L2 and push out the tile runs' partially written
+// lines before their neighbours complete them, so each boundary line is
+// written back twice: WRITE_SIZE 4.72 GB for 2.4 GB of records, 1.75 ms.
+// Non-temporal loads (3) or coalesced 8-byte word loads (5) leave the dirty
+// lines in place: 2.34 / 2.35 GB and 1.03 / 1.07 ms, bit-exact.  1 stores to
+// `dummy` (same offsets; still 4.7 GB: not the destination), 2 makes records
+// from the position without loading (2.17 GB, 0.90 ms: the floor), 4 stores
+// non-temporally (5.06 GB), 6 = 5 with non-temporal loads.  Only 0, 3, 5, 6
+// give the product's output; 1, 2, 4 are attribution probes.
 template <int MODE>
 __global__ void __launch_bounds__(kTwT)
 k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
@@ -1300,14 +1307,17 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
   // (every load instruction a contiguous 512 B), placed by the record
   // positions the rank publishes in LDS
   constexpr int kW = 3 * kTwPer;
-  uint64_t wd[MODE == 5 ? kW : 1];
+  uint64_t wd[MODE == 5 || MODE == 6 ? kW : 1];
   const uint32_t nwords = 3 * (p1 - p0);
-  if constexpr (MODE == 5) {
+  if constexpr (MODE == 5 || MODE == 6) {
     const uint64_t* src = (const uint64_t*)(recA + p0);
 #pragma unroll
     for (int m = 0; m < kW; m++) {
       const uint32_t w = tid + (uint32_t)m * kTwT;
-      wd[m] = w < nwords ? src[w] : 0ull;
+      if constexpr (MODE == 6)
+        wd[m] = w < nwords ? __builtin_nontemporal_load(src + w) : 0ull;
+      else
+        wd[m] = w < nwords ? src[w] : 0ull;
     }
   }
 #pragma unroll
@@ -1316,8 +1326,8 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
     v[k] = p < p1;
     dg[k] = 0;
     if (v[k]) {
-      if constexpr (MODE == 5) {
-        dg[k] = bA[p] & (nb2 - 1);
+      if constexpr (MODE == 5 || MODE == 6) {
+        dg[k] = (MODE == 6 ? __builtin_nontemporal_load(bA + p) : bA[p]) & (nb2 - 1);
       } else if constexpr (MODE == 2) {
         r[k].h1 = p; r[k].h2 = ~(uint64_t)p; r[k].item = p;
         dg[k] = (p * 2654435761u >> 9) & (nb2 - 1);
@@ -1335,7 +1345,7 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
   }
   if (tid < nb2) S.gofs[tid] = start[(d1 << B2) | tid] + H2[(uint64_t)j * nb2 + tid];
   tw_rank(dg, v, S, pos);
-  if constexpr (MODE == 5) {
+  if constexpr (MODE == 5 || MODE == 6) {
 #pragma unroll
     for (int k = 0; k < kTwPer; k++)
       if (v[k]) {
@@ -1520,7 +1530,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       hipLaunchKernelGGL(k_tw_start2, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
                          nb1, B2, start);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_tw_scatter2<0>, dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA, (const uint16_t*)bA,
+      hipLaunchKernelGGL(k_tw_scatter2<3>, dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA, (const uint16_t*)bA,
                          (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
                          (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
       if ((rc = launch_done())) return rc;

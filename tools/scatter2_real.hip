@@ -15,6 +15,8 @@
 //   3  non-temporal recA/bA loads
 //   4  non-temporal stores
 //   5  the records read as coalesced 8-byte words (checked bit-exact too)
+//   6  5 with non-temporal loads
+// (the library launches mode 3 since round 4; mode 0 is the round-3 kernel)
 // Run it under rocprofv3 --pmc WRITE_SIZE FETCH_SIZE: each mode is its own
 // kernel instance in the summary.  Prints one JSON line with the timings.
 //
@@ -90,7 +92,7 @@ int main(int argc, char** argv) {
 #define S2(M) hipLaunchKernelGGL(k_tw_scatter2<M>, dim3(ntB), dim3(kTwT), 0, 0, recA, bA, tbs, cnt1, start1, nb1, B2, \
                                  H2, start, recB, dummy)
     switch (m) { case 0: S2(0); break; case 1: S2(1); break; case 2: S2(2); break; case 3: S2(3); break;
-                 case 4: S2(4); break; default: S2(5); break; }
+                 case 4: S2(4); break; case 5: S2(5); break; default: S2(6); break; }
 #undef S2
   };
   // fidelity: mode 0 reproduces the sort's own pass-2 output
@@ -119,7 +121,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int modes = 6;
+  const int modes = 7;
   std::vector<double> ms(modes, 0.0);
   for (int r = 0; r < reps; r++)
     for (int m = 0; m < modes; m++) {
@@ -133,8 +135,8 @@ int main(int argc, char** argv) {
     }
   printf("{\"n\": %llu, \"B\": %u, \"B2\": %u, \"tiles\": %u, \"record_bytes\": %llu, \"mode0_equals_sort\": %s, "
          "\"ms\": {\"0_product\": %.4f, \"1_dummy_stores\": %.4f, \"2_no_loads\": %.4f, \"3_nt_loads\": %.4f, "
-         "\"4_nt_stores\": %.4f, \"5_word_loads\": %.4f}, \"mode5_equals_sort\": %s}\n",
+         "\"4_nt_stores\": %.4f, \"5_word_loads\": %.4f, \"6_word_loads_nt\": %.4f}, \"mode5_equals_sort\": %s}\n",
          (unsigned long long)n, B, B2, ntiles, (unsigned long long)(24 * n), same ? "true" : "false", ms[0], ms[1],
-         ms[2], ms[3], ms[4], ms[5], same5 ? "true" : "false");
+         ms[2], ms[3], ms[4], ms[5], ms[6], same5 ? "true" : "false");
   return same && same5 ? 0 : 6;
 }

@@ -20,6 +20,10 @@
 //                workgroups, plain loads/stores (MI355X_MICROARCH.md: 6.29 TB/s)
 //   f4nt         the same with nt loads/stores
 //   memcpy       hipMemcpyAsync device-to-device
+//   chunk_pf     the chunk form with the next chunk's loads issued before
+//                this chunk's stores
+//   chunk_xi     the chunk form with chunks dealt round-robin over workgroups
+//   f4u<U>       one-shot grid, U items per thread, nt
 //
 // usage: stream_forms [n_items=100000000] [settle_ms=500] [rounds=5] [reps=20]
 #include <hip/hip_runtime.h>
@@ -73,6 +77,99 @@ __global__ void __launch_bounds__(1024) chunk(const v4u* __restrict__ in, v4u* _
   if (probe) clk_end(ck, c0, w0);
 }
 
+// chunk form with the next chunk's loads issued before this chunk's stores
+// (software-pipelined: the wait for chunk c + 1's data does not sit behind
+// chunk c's stores)
+template <int U>
+__global__ void __launch_bounds__(1024) chunk_pf(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
+                                                 Clk* ck) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6, last = n - 1, step = nw * 64 * U;
+  uint64_t b = wave * 64 * U;
+  v4u X[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t j = b + 64 * u + lane;
+    X[u] = __builtin_nontemporal_load(in + (j < last ? j : last));
+  }
+  for (; b < n; b += step) {
+    v4u Y[U];
+    const uint64_t bn = b + step;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = bn + 64 * u + lane;
+      Y[u] = __builtin_nontemporal_load(in + (j < last ? j : last));
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      v4u v = X[u];
+      v.x ^= 0x9e3779b9u;
+      __builtin_nontemporal_store(v, out + (j < last ? j : last));
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) X[u] = Y[u];
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
+// chunk form with chunks dealt to workgroups round-robin (chunk k of a pass
+// -> workgroup k % G, so consecutive 1 KiB-per-instruction runs go to
+// consecutive workgroups, i.e. to different XCDs, as the one-item-per-thread
+// grid does)
+template <int U>
+__global__ void __launch_bounds__(1024) chunk_xi(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
+                                                 Clk* ck) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  const uint64_t G = gridDim.x, wib = threadIdx.x >> 6, lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+  const uint64_t chunk0 = wib * G + blockIdx.x, nw = G * wpb, last = n - 1;
+  for (uint64_t c = chunk0; c * 64 * U < n; c += nw) {
+    const uint64_t b = c * 64 * U;
+    v4u X[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      X[u] = __builtin_nontemporal_load(in + (j < last ? j : last));
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      v4u v = X[u];
+      v.x ^= 0x9e3779b9u;
+      __builtin_nontemporal_store(v, out + (j < last ? j : last));
+    }
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
+// one-shot grid, U items per thread (non-persistent, 256-thread workgroups)
+template <int U>
+__global__ void __launch_bounds__(256) f4u(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n, Clk* ck) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  const uint64_t b = (uint64_t)blockIdx.x * 256 * U + (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
+  v4u X[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t j = b + 64 * u;
+    if (j < n) X[u] = __builtin_nontemporal_load(in + j);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t j = b + 64 * u;
+    v4u v = X[u];
+    v.x ^= 0x9e3779b9u;
+    if (j < n) __builtin_nontemporal_store(v, out + j);
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
 template <bool NT>
 __global__ void __launch_bounds__(256) f4copy(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
                                               Clk* ck) {
@@ -96,7 +193,7 @@ __global__ void __launch_bounds__(256) f4copy(const v4u* __restrict__ in, v4u* _
 
 struct Form {
   const char* name;
-  int kind;  // 0 chunk, 1 f4, 2 f4nt, 3 memcpy
+  int kind;  // 0 chunk, 1 f4, 2 f4nt, 3 memcpy, 4 chunk_pf, 5 chunk_xi, 6 f4u
   int U, g;
 };
 
@@ -117,7 +214,9 @@ int main(int argc, char** argv) {
   const std::vector<Form> forms = {
       {"chunk4_g1 (k_fixed/copy_peak shape)", 0, 4, 1}, {"chunk4_g2", 0, 4, 2}, {"chunk8_g1", 0, 8, 1},
       {"chunk2_g2", 0, 2, 2}, {"chunk4_g8", 0, 4, 8},   {"f4 (guide float4 copy)", 1, 0, 0},
-      {"f4nt", 2, 0, 0},      {"memcpy_d2d", 3, 0, 0}};
+      {"f4nt", 2, 0, 0},      {"memcpy_d2d", 3, 0, 0},  {"chunk4_pf_g1 (next chunk's loads before stores)", 4, 4, 1},
+      {"chunk2_pf_g1", 4, 2, 1}, {"chunk4_xi_g1 (chunks round-robin over workgroups)", 5, 4, 1},
+      {"f4u4nt (one-shot grid, 4 items per thread)", 6, 4, 0}, {"f4u2nt", 6, 2, 0}};
   auto launch = [&](const Form& f) {
     if (f.kind == 0) {
       const dim3 grid(cus * f.g), block(1024);
@@ -128,6 +227,16 @@ int main(int argc, char** argv) {
       const dim3 grid((unsigned)((n + 255) / 256)), block(256);
       if (f.kind == 1) hipLaunchKernelGGL(f4copy<false>, grid, block, 0, 0, in, out, n, ck);
       else hipLaunchKernelGGL(f4copy<true>, grid, block, 0, 0, in, out, n, ck);
+    } else if (f.kind == 4) {
+      const dim3 grid(cus * f.g), block(1024);
+      if (f.U == 2) hipLaunchKernelGGL(chunk_pf<2>, grid, block, 0, 0, in, out, n, ck);
+      else hipLaunchKernelGGL(chunk_pf<4>, grid, block, 0, 0, in, out, n, ck);
+    } else if (f.kind == 5) {
+      hipLaunchKernelGGL(chunk_xi<4>, dim3(cus * f.g), dim3(1024), 0, 0, in, out, n, ck);
+    } else if (f.kind == 6) {
+      const dim3 grid((unsigned)((n + 256 * f.U - 1) / (256 * f.U))), block(256);
+      if (f.U == 2) hipLaunchKernelGGL(f4u<2>, grid, block, 0, 0, in, out, n, ck);
+      else hipLaunchKernelGGL(f4u<4>, grid, block, 0, 0, in, out, n, ck);
     } else {
       CK(hipMemcpyAsync(out, in, n * 16, hipMemcpyDeviceToDevice, 0));
     }
