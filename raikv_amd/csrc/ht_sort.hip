@@ -598,15 +598,15 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
 // for its sorted positions and stores it coalesced.  The duplicate test takes
 // the successor's field from the same LDS round.  Runs of equal digit still
 // compare ties through global memory (rare, and those lines are L2-hot).
-template <uint32_t CAP, int D>
-__global__ void __launch_bounds__(kBkT, 1)
+template <uint32_t CAP, int D, int T = kBkT>
+__global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD (512 threads x 2 per CU spill: 87 VGPRs)
 k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
            uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
            uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
            uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
-  static_assert(CAP % kBkT == 0, "records per thread");
-  constexpr uint32_t PER = CAP / kBkT;
-  constexpr uint32_t nd = 1u << D, per = nd / kBkT;
+  static_assert(CAP % T == 0, "records per thread");
+  constexpr uint32_t PER = CAP / T;
+  constexpr uint32_t nd = 1u << D, per = nd / T;
   struct SortArrays {
     uint32_t K[CAP];       // key64 bits [B, B + 32) of each record
     uint16_t dig[CAP];     // its top D bits
@@ -618,7 +618,7 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
   };
   __shared__ Lds u;
   __shared__ uint16_t ord[CAP];  // sorted position -> record
-  __shared__ uint32_t wsum[kBkT / 64], wmax[kBkT / 64];
+  __shared__ uint32_t wsum[T / 64], wmax[T / 64];
   uint32_t* K = u.s.K;
   uint16_t* dig = u.s.dig;
   uint32_t* hist = u.s.hist;
@@ -632,14 +632,16 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       continue;
     }
     const R24* rb = recs + base;
-    uint64_t f0[PER], f1[PER], f2[PER];  // h1, h2, item of records tid + j * kBkT
+    uint64_t f0[PER], f1[PER], f2[PER];  // h1, h2, item of records tid + j * T
 #pragma unroll
     for (uint32_t j = 0; j < PER; j++) {
-      const uint32_t r = tid + j * kBkT;
+      const uint32_t r = tid + j * T;
       f0[j] = f1[j] = f2[j] = 0;
-      if (r < R) {
-        const R24 x = rb[r];
-        f0[j] = x.h1; f1[j] = x.h2; f2[j] = x.item;
+      if (r < R) {  // non-temporal: read once, and they must not push the outputs out of L2
+        const uint64_t* q = (const uint64_t*)(rb + r);
+        f0[j] = __builtin_nontemporal_load(q);
+        f1[j] = __builtin_nontemporal_load(q + 1);
+        f2[j] = __builtin_nontemporal_load(q + 2);
       }
     }
 #pragma unroll
@@ -647,12 +649,158 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < PER; j++) {
-      const uint32_t r = tid + j * kBkT;
+      const uint32_t r = tid + j * T;
       if (r < R) {
         const uint32_t k32 = (uint32_t)((sort_key64(g, sb, f0[j]) << B) >> 32);
         K[r] = k32;
         dig[r] = (uint16_t)(k32 >> (32 - D));
         atomicAdd(&hist[k32 >> (32 - D)], 1u);
+      }
+    }
+    __syncthreads();
+    {  // exclusive scan of the digit counts, and the longest run
+      uint32_t v[per], s = 0, mx = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { v[j] = hist[tid * per + j]; s += v[j]; mx = max(mx, v[j]); }
+      uint32_t inc = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+      if (lane == 63) wsum[w] = inc;
+      if (lane == 0) wmax[w] = mx;
+      __syncthreads();
+      uint32_t wo = 0, bm = 0;
+      for (uint32_t q = 0; q < T / 64; q++) {
+        if (q < w) wo += wsum[q];
+        bm = max(bm, wmax[q]);
+      }
+      if (bm > kBkRun) {  // a run too long for insertion sort: the bitonic path
+        if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+        __syncthreads();
+        continue;
+      }
+      uint32_t run = wo + inc - s;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < R; t += T) ord[atomicAdd(&hist[dig[t]], 1u)] = (uint16_t)t;
+    __syncthreads();
+    // runs of equal digit (hist[d] is now the end of digit d): full order
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) {
+      const uint32_t d = tid * per + j;
+      const uint32_t e = hist[d], s0 = d ? hist[d - 1] : 0u;
+      for (uint32_t a = s0 + 1; a < e; a++) {
+        const uint16_t x = ord[a];
+        const uint32_t kx = K[x];
+        uint32_t c = a;
+        while (c > s0) {
+          const uint16_t y = ord[c - 1];
+          const uint32_t ky = K[y];
+          const bool lt = kx != ky ? kx < ky : bk_less_at(g, sb, rb[x], rb[y], x, y);
+          if (!lt) break;
+          ord[c] = y;
+          c--;
+        }
+        ord[c] = x;
+      }
+    }
+    __syncthreads();  // ord final; the sort arrays are free for the field rounds
+    uint64_t h1v[PER];
+    uint32_t eq1 = 0;  // bit j: sorted position tid + j * T has the same h1 as its successor
+#pragma unroll
+    for (uint32_t f = 0; f < 3; f++) {
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t r = tid + j * T;
+        if (r < R) u.X[r] = f == 0 ? f0[j] : f == 1 ? f1[j] : f2[j];
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t p = tid + j * T;
+        if (p < R) {
+          const uint64_t v = u.X[ord[p]];
+          const bool eq = f < 2 && dedup && p + 1 < R && u.X[ord[p + 1 < R ? p + 1 : p]] == v;
+          if (f == 0) {
+            h1v[j] = v;
+            eq1 |= (eq ? 1u : 0u) << j;
+          } else if (f == 1) {
+            const bool dup = eq && ((eq1 >> j) & 1u);
+            d_total += dup ? 1u : 0u;
+            uint64_t* o = h_out + 2 * ((uint64_t)base + p);
+            o[0] = dup ? 0ull : h1v[j];
+            o[1] = v;
+          } else if (items_out) {
+            items_out[(uint64_t)base + p] = v;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (dedup && dups) {
+    const uint32_t t = block_sum<T>(d_total, wsum);
+    if (tid == 0 && t) atomicAdd(dups, (unsigned long long)t);
+  }
+}
+
+// B3r2: k_bk_sortr at two workgroups per CU, so one workgroup's loads run
+// under the other's LDS phases (k_bk_sortr at one per CU serialises them:
+// 1.75 ms, no better than k_bk_sort's re-fetching gather).  To fit two
+// 1024-thread workgroups (≤ 64 VGPRs, ≤ 80 KiB of LDS each) the h1 words go
+// straight into the LDS field array X, where the sort reads them (its key
+// and digit recomputed from h1 instead of kept: ht_mod is a multiply and a
+// shift), D = 11 digit bits (8 KiB of counts), and only h2 and the item
+// stay in registers until their rounds.
+template <uint32_t CAP, int D>
+__global__ void __launch_bounds__(kBkT, 8)  // 8 waves per SIMD: two 1024-thread workgroups per CU
+k_bk_sortr2(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
+            uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
+            uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
+            uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
+  static_assert(CAP % kBkT == 0, "records per thread");
+  constexpr uint32_t PER = CAP / kBkT;
+  constexpr uint32_t nd = 1u << D, per = nd / kBkT;
+  __shared__ uint64_t X[CAP];      // h1 of every record (the sort's input), then h2, then the item
+  __shared__ uint32_t hist[nd];    // digit counts -> starts -> ends
+  __shared__ uint16_t ord[CAP];    // sorted position -> record
+  __shared__ uint32_t wsum[kBkT / 64], wmax[kBkT / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto k32_of = [&](uint64_t h1) { return (uint32_t)((sort_key64(g, sb, h1) << B) >> 32); };
+  uint32_t d_total = 0;
+  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t R = cnt[b], base = start[b];
+    if (R == 0) continue;
+    if (R > CAP) {
+      if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+      continue;
+    }
+    const R24* rb = recs + base;
+    // the thread index laundered per bucket: otherwise the compiler hoists
+    // every per-slot address out of the bucket loop and spills them
+    uint32_t tl = tid;
+    asm volatile("" : "+v"(tl));
+    uint64_t f1[PER], f2[PER];  // h2 and item of records tid + j * kBkT
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tl + j * kBkT;
+      f1[j] = f2[j] = 0;
+      if (r < R) {  // non-temporal: the record lines are not reused (and must not evict the outputs)
+        const uint64_t* q = (const uint64_t*)(rb + r);
+        const uint64_t h1 = __builtin_nontemporal_load(q);
+        f1[j] = __builtin_nontemporal_load(q + 1);
+        f2[j] = __builtin_nontemporal_load(q + 2);
+        X[r] = h1;
+        atomicAdd(&hist[k32_of(h1) >> (32 - D)], 1u);
       }
     }
     __syncthreads();
@@ -686,7 +834,7 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
     }
     __syncthreads();
-    for (uint32_t t = tid; t < R; t += kBkT) ord[atomicAdd(&hist[dig[t]], 1u)] = (uint16_t)t;
+    for (uint32_t t = tid; t < R; t += kBkT) ord[atomicAdd(&hist[k32_of(X[t]) >> (32 - D)], 1u)] = (uint16_t)t;
     __syncthreads();
     // runs of equal digit (hist[d] is now the end of digit d): full order
 #pragma unroll
@@ -695,11 +843,11 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       const uint32_t e = hist[d], s0 = d ? hist[d - 1] : 0u;
       for (uint32_t a = s0 + 1; a < e; a++) {
         const uint16_t x = ord[a];
-        const uint32_t kx = K[x];
+        const uint32_t kx = k32_of(X[x]);
         uint32_t c = a;
         while (c > s0) {
           const uint16_t y = ord[c - 1];
-          const uint32_t ky = K[y];
+          const uint32_t ky = k32_of(X[y]);
           const bool lt = kx != ky ? kx < ky : bk_less_at(g, sb, rb[x], rb[y], x, y);
           if (!lt) break;
           ord[c] = y;
@@ -708,31 +856,35 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
         ord[c] = x;
       }
     }
-    __syncthreads();  // ord final; the sort arrays are free for the field rounds
-    uint64_t h1v[PER];
+    __syncthreads();
+    // field rounds: h1 (already in X), h2, item.  The h1 word of each output
+    // pair is stored in the first round and zeroed in the second for a marked
+    // duplicate (ctest.c:96-104), so no h1 stays in a register
     uint32_t eq1 = 0;  // bit j: sorted position tid + j * kBkT has the same h1 as its successor
 #pragma unroll
     for (uint32_t f = 0; f < 3; f++) {
+      if (f > 0) {
 #pragma unroll
-      for (uint32_t j = 0; j < PER; j++) {
-        const uint32_t r = tid + j * kBkT;
-        if (r < R) u.X[r] = f == 0 ? f0[j] : f == 1 ? f1[j] : f2[j];
+        for (uint32_t j = 0; j < PER; j++) {
+          const uint32_t r = tl + j * kBkT;
+          if (r < R) X[r] = f == 1 ? f1[j] : f2[j];
+        }
+        __syncthreads();
       }
-      __syncthreads();
 #pragma unroll
       for (uint32_t j = 0; j < PER; j++) {
-        const uint32_t p = tid + j * kBkT;
+        const uint32_t p = tl + j * kBkT;
         if (p < R) {
-          const uint64_t v = u.X[ord[p]];
-          const bool eq = f < 2 && dedup && p + 1 < R && u.X[ord[p + 1 < R ? p + 1 : p]] == v;
+          const uint64_t v = X[ord[p]];
+          const bool eq = f < 2 && dedup && p + 1 < R && X[ord[p + 1 < R ? p + 1 : p]] == v;
+          uint64_t* o = h_out + 2 * ((uint64_t)base + p);
           if (f == 0) {
-            h1v[j] = v;
+            o[0] = v;
             eq1 |= (eq ? 1u : 0u) << j;
           } else if (f == 1) {
             const bool dup = eq && ((eq1 >> j) & 1u);
             d_total += dup ? 1u : 0u;
-            uint64_t* o = h_out + 2 * ((uint64_t)base + p);
-            o[0] = dup ? 0ull : h1v[j];
+            if (dup) o[0] = 0ull;
             o[1] = v;
           } else if (items_out) {
             items_out[(uint64_t)base + p] = v;
@@ -1534,7 +1686,11 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                          (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
                          (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
       if ((rc = launch_done())) return rc;
-      if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 1)
+      if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 2)
+        hipLaunchKernelGGL((k_bk_sortr2<7168, 11>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0,
+                           st, (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
+                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      else if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 1)
         hipLaunchKernelGGL((k_bk_sortr<7168, 12>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                            items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
@@ -1665,7 +1821,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
 
 }  // namespace
 
-namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; std::atomic<int> g_tune_sort_b3{0}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; std::atomic<int> g_tune_sort_b3{1}; } }
 
 extern "C" {
 

@@ -24,6 +24,8 @@
 //                this chunk's stores
 //   chunk_xi     the chunk form with chunks dealt round-robin over workgroups
 //   f4u<U>       one-shot grid, U items per thread, nt
+//   chunk_dyn    persistent chunk form taking chunks from a global counter
+//                (all of them, or the last 12.5 % after a static share)
 //
 // usage: stream_forms [n_items=100000000] [settle_ms=500] [rounds=5] [reps=20]
 #include <hip/hip_runtime.h>
@@ -147,6 +149,47 @@ __global__ void __launch_bounds__(1024) chunk_xi(const v4u* __restrict__ in, v4u
   if (probe) clk_end(ck, c0, w0);
 }
 
+// persistent chunk form with dynamic chunk assignment: after its static
+// share (the first `stat` chunk rounds), a wave takes G chunks at a time from
+// a global counter -- do faster XCDs/CUs absorb the tail, as a one-shot
+// grid's dispatcher lets them?
+template <int U, int G>
+__global__ void __launch_bounds__(1024) chunk_dyn(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
+                                                  Clk* ck, unsigned long long* ctr, uint64_t stat) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6, last = n - 1;
+  const uint64_t nch = (n + 64 * U - 1) / (64 * U);
+  auto body = [&](uint64_t c) {
+    const uint64_t b = c * 64 * U;
+    v4u X[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      X[u] = __builtin_nontemporal_load(in + (j < last ? j : last));
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t j = b + 64 * u + lane;
+      v4u v = X[u];
+      v.x ^= 0x9e3779b9u;
+      __builtin_nontemporal_store(v, out + (j < last ? j : last));
+    }
+  };
+  const uint64_t sc = stat * nw < nch ? stat * nw : nch;  // chunks dealt statically
+  for (uint64_t c = wave; c < sc; c += nw) body(c);
+  for (;;) {
+    uint64_t g0 = 0;
+    if (lane == 0) g0 = atomicAdd(ctr, (unsigned long long)G);
+    g0 = __shfl(g0, 0, 64) + sc;
+    if (g0 >= nch) break;
+    for (uint64_t c = g0; c < g0 + G && c < nch; c++) body(c);
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
 // one-shot grid, U items per thread (non-persistent, 256-thread workgroups)
 template <int U>
 __global__ void __launch_bounds__(256) f4u(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n, Clk* ck) {
@@ -154,6 +197,33 @@ __global__ void __launch_bounds__(256) f4u(const v4u* __restrict__ in, v4u* __re
   uint64_t c0 = 0, w0 = 0;
   if (probe) clk_begin(c0, w0);
   const uint64_t b = (uint64_t)blockIdx.x * 256 * U + (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
+  v4u X[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t j = b + 64 * u;
+    if (j < n) X[u] = __builtin_nontemporal_load(in + j);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint64_t j = b + 64 * u;
+    v4u v = X[u];
+    v.x ^= 0x9e3779b9u;
+    if (j < n) __builtin_nontemporal_store(v, out + j);
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
+// f4u with the workgroup -> block mapping scrambled (a bijection): the same
+// one-shot dispatch, but the blocks in flight no longer form one compact
+// address window
+template <int U>
+__global__ void __launch_bounds__(256) f4u_scr(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
+                                               Clk* ck) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  const uint64_t G = gridDim.x, blk = ((uint64_t)blockIdx.x * 2654435761ull) % G;  // odd multiplier, G odd
+  const uint64_t b = blk * 256 * U + (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
   v4u X[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -193,7 +263,7 @@ __global__ void __launch_bounds__(256) f4copy(const v4u* __restrict__ in, v4u* _
 
 struct Form {
   const char* name;
-  int kind;  // 0 chunk, 1 f4, 2 f4nt, 3 memcpy, 4 chunk_pf, 5 chunk_xi, 6 f4u
+  int kind;  // 0 chunk, 1 f4, 2 f4nt, 3 memcpy, 4 chunk_pf, 5 chunk_xi, 6 f4u, 7 chunk_dyn (g = static rounds)
   int U, g;
 };
 
@@ -210,13 +280,18 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&in, n * 16));
   CK(hipMalloc(&out, n * 16));
   CK(hipMalloc(&ck, sizeof(Clk)));
+  unsigned long long* ctr = nullptr;
+  CK(hipMalloc(&ctr, 8));
   CK(hipMemset(in, 1, n * 16));
   const std::vector<Form> forms = {
       {"chunk4_g1 (k_fixed/copy_peak shape)", 0, 4, 1}, {"chunk4_g2", 0, 4, 2}, {"chunk8_g1", 0, 8, 1},
       {"chunk2_g2", 0, 2, 2}, {"chunk4_g8", 0, 4, 8},   {"f4 (guide float4 copy)", 1, 0, 0},
       {"f4nt", 2, 0, 0},      {"memcpy_d2d", 3, 0, 0},  {"chunk4_pf_g1 (next chunk's loads before stores)", 4, 4, 1},
       {"chunk2_pf_g1", 4, 2, 1}, {"chunk4_xi_g1 (chunks round-robin over workgroups)", 5, 4, 1},
-      {"f4u4nt (one-shot grid, 4 items per thread)", 6, 4, 0}, {"f4u2nt", 6, 2, 0}};
+      {"f4u4nt (one-shot grid, 4 items per thread)", 6, 4, 0}, {"f4u2nt", 6, 2, 0},
+      {"chunk4_dyn_all (every chunk from a counter, 4 per grab)", 7, 4, 0},
+      {"chunk4_dyn_tail (87.5% static, then the counter)", 7, 4, 83},
+      {"f4u4nt_scrambled (one-shot, blocks in a scrambled order)", 8, 4, 0}};
   auto launch = [&](const Form& f) {
     if (f.kind == 0) {
       const dim3 grid(cus * f.g), block(1024);
@@ -233,6 +308,13 @@ int main(int argc, char** argv) {
       else hipLaunchKernelGGL(chunk_pf<4>, grid, block, 0, 0, in, out, n, ck);
     } else if (f.kind == 5) {
       hipLaunchKernelGGL(chunk_xi<4>, dim3(cus * f.g), dim3(1024), 0, 0, in, out, n, ck);
+    } else if (f.kind == 8) {
+      uint32_t G = (uint32_t)((n + 256 * 4 - 1) / (256 * 4));
+      G |= 1u;  // odd; gcd(G, 2654435761) = 1 at the default n (a bijection)
+      hipLaunchKernelGGL(f4u_scr<4>, dim3(G), dim3(256), 0, 0, in, out, n, ck);
+    } else if (f.kind == 7) {
+      CK(hipMemsetAsync(ctr, 0, 8, 0));
+      hipLaunchKernelGGL((chunk_dyn<4, 4>), dim3(cus), dim3(1024), 0, 0, in, out, n, ck, ctr, (uint64_t)f.g);
     } else if (f.kind == 6) {
       const dim3 grid((unsigned)((n + 256 * f.U - 1) / (256 * f.U))), block(256);
       if (f.U == 2) hipLaunchKernelGGL(f4u<2>, grid, block, 0, 0, in, out, n, ck);
