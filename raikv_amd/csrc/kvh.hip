@@ -158,6 +158,41 @@ int device_cus(int* cus) {
   return 0;
 }
 
+// Ticket counters for the in-order streaming kernels (k_fixed_q): two
+// words per (device, stream), zero between launches -- the kernel's last
+// workgroup puts them back to zero as it exits, so no memset precedes a
+// launch and graph capture sees one kernel.  Launches on one stream are
+// serialised, so a stream's pair is never used by two kernels at once.
+struct TicketPool {
+  std::vector<unsigned long long*> chunks;  // 256 pairs each
+  std::vector<std::pair<hipStream_t, unsigned long long*>> by_stream;
+  size_t used = 0;
+};
+std::vector<TicketPool> g_tickets;
+
+int stream_tickets(hipStream_t st, unsigned long long** tk) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  std::lock_guard<std::mutex> g(g_mu);
+  if ((int)g_tickets.size() <= dev) g_tickets.resize(dev + 1);
+  TicketPool& P = g_tickets[dev];
+  for (auto& sp : P.by_stream)
+    if (sp.first == st) { *tk = sp.second; return 0; }
+  constexpr size_t kPairs = 256;
+  if (P.used == P.chunks.size() * kPairs) {
+    unsigned long long* c = nullptr;
+    if ((e = hipMalloc((void**)&c, kPairs * 2 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
+    if ((e = hipMemset(c, 0, kPairs * 2 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
+    P.chunks.push_back(c);
+  }
+  unsigned long long* p = P.chunks[P.used / kPairs] + 2 * (P.used % kPairs);
+  P.used++;
+  P.by_stream.emplace_back(st, p);
+  *tk = p;
+  return 0;
+}
+
 int launch_done() {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(e);
@@ -184,6 +219,7 @@ using Knob = std::atomic<int>;
 namespace kvh {
 namespace rt {
 Knob g_tune_nt{0};        // tables per LDS: 2 or 4 (0 = per-length default)
+Knob g_tune_order{0};     // knob 24: fixed-length chunk order: 0 = static per wave (k_fixed); 1/2/3 = in address order from a ticket counter, 1/4/16 workgroup-rounds per ticket (k_fixed_q); 4 = the same without the per-ticket barrier (k_fixed_qw)
 Knob g_tune_wgmul{1};     // workgroups per CU multiplier
 Knob g_tune_generic{0};   // force the generic kernel
 Knob g_tune_kpl{0};       // keys per lane per chunk in k_fixed (0 = per-length default)
@@ -1000,6 +1036,7 @@ int kvh_set_tuning(int k, int value) {
     case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
     case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_cap, value);
     case 23: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_b3, value);
+    case 24: if (value < 0 || value > 4) return KVH_EINVAL; return set(g_tune_order, value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }

@@ -68,6 +68,146 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
   }
 }
 
+// k_fixed with the chunks taken IN ADDRESS ORDER (round 4, knob 24 = 1, the
+// default).  A workgroup-iteration (16 waves x 64U keys) is one ticket from a
+// per-stream counter (stream_tickets), the next ticket fetched one iteration
+// ahead, so the chunks in flight on the whole chip form one compact address
+// window, as a one-shot grid's do.  k_fixed's static order lets waves drift
+// apart over a launch and the window spreads: on the same 3.2 GB the static
+// persistent copy streams 5.2-5.4 TB/s, in-order tickets 6.7 TB/s, and a
+// one-shot grid 6.2-6.5 TB/s but only 5.2 with its blocks scrambled
+// (tools/stream_forms.hip, profiles/r04/s4-s5/).  The last workgroup to exit
+// puts the counter pair back to zero.
+template <int L, int NT, bool A16, int U, int R = 1>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_q(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out,
+          uint32_t flags, unsigned long long* __restrict__ tk) {
+  constexpr int NC = Plan<L>::NC;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ unsigned long long tkl[2];
+  fill_tables<NT>(lds);
+  if (threadIdx.x == 0) tkl[0] = atomicAdd(tk, 1ull);
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint64_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t per_it = (uint64_t)(blockDim.x >> 6) * 64 * U * R;  // keys per ticket: R rounds of the 16 waves
+  const uint64_t last = n - 1;
+  for (uint32_t it = 0;; it++) {
+    const uint64_t t = tkl[it & 1];
+    if (threadIdx.x == 0) tkl[(it + 1) & 1] = atomicAdd(tk, 1ull);
+    if (t * per_it >= n) break;  // workgroup-uniform
+#pragma unroll 1
+    for (int r = 0; r < R; r++) {
+      const uint64_t b = t * per_it + ((uint64_t)r * (blockDim.x >> 6) + wv) * 64 * U;
+      if (b < n) {  // wave-uniform
+        Blk D[U][NC];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t j = b + 64 * u + lane;
+          load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
+        }
+        Blk h[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint64_t j = b + 64 * u + lane;
+          store_h<true>(out, j < last ? j : last, h[u], fix);
+        }
+      }
+    }
+    __syncthreads();  // tkl[(it + 1) & 1] written before it is read; tkl[it & 1] read before it is rewritten
+  }
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(tk + 1, 1ull) == (unsigned long long)gridDim.x - 1) {  // every other workgroup is done with tk
+      atomicExch(tk, 0ull);
+      atomicExch(tk + 1, 0ull);
+    }
+  }
+}
+
+// k_fixed_qw: the same in-order tickets without the per-ticket barrier.  The
+// workgroup's waves take chunks one at a time from an LDS counter; the
+// global ticket for chunks 16j .. 16j+15 of the workgroup is fetched by the
+// wave that takes chunk 16(j-2) and published in a 16-slot LDS ring with its
+// index as a tag, so each wave runs at its own pace (its loads under the
+// other waves' rounds, as in k_fixed) while the chip's chunks in flight stay
+// one address window.  A wave whose ticket is not yet published sleeps on the
+// tag (it was fetched two tickets ahead, so this is rare).
+template <int L, int NT, bool A16, int U>
+__global__ void __launch_bounds__(kBlock)
+k_fixed_qw(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out,
+           uint32_t flags, unsigned long long* __restrict__ tk) {
+  constexpr int NC = Plan<L>::NC, kRing = 16;
+  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  __shared__ unsigned long long ring[kRing];
+  __shared__ uint32_t tag[kRing];
+  __shared__ uint32_t lk;
+  fill_tables<NT>(lds);
+  if (threadIdx.x < kRing) tag[threadIdx.x] = 0;  // tag = ticket index + 1 (0: none yet); only grows
+  if (threadIdx.x == 0) lk = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ring[0] = atomicAdd(tk, 1ull);
+    ring[1] = atomicAdd(tk, 1ull);
+    tag[0] = 1;
+    tag[1] = 2;
+  }
+  __syncthreads();
+  const LdsTab<NT> T(lds);
+  const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
+  const bool fix = (flags & KVH_FIXUP) != 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint64_t last = n - 1, per_chunk = 64 * U;
+  for (;;) {
+    uint32_t k = 0;
+    if (lane == 0) k = atomicAdd(&lk, 1u);
+    k = __builtin_amdgcn_readfirstlane(k);
+    const uint32_t j = k / wpb, s = k - j * wpb;
+    if (s == 0 && lane == 0) {  // this ticket's first taker fetches the one two ahead
+      const unsigned long long g = atomicAdd(tk, 1ull);
+      ring[(j + 2) % kRing] = g;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __hip_atomic_store(&tag[(j + 2) % kRing], j + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // tags only grow, so this wait ends whatever the interleaving (a slot
+    // overtaken by ticket j + 16 would need 14 tickets -- 224 chunks -- handed
+    // out while this wave sits between its LDS atomic and this load)
+    while (__hip_atomic_load(&tag[j % kRing], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < j + 1)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint64_t t = ring[j % kRing];
+    const uint64_t b = (t * wpb + s) * per_chunk;
+    if (b >= n) break;  // wave-uniform: every later chunk of this wave lies further on
+    Blk D[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t jj = b + 64 * u + lane;
+      load_fixed<L, A16, true>(keys + (jj < last ? jj : last) * L, D[u]);
+    }
+    Blk h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint64_t jj = b + 64 * u + lane;
+      store_h<true>(out, jj < last ? jj : last, h[u], fix);
+    }
+  }
+  __syncthreads();  // every wave of this workgroup is past its last ticket use
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(tk + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
+      atomicExch(tk, 0ull);
+      atomicExch(tk + 1, 0ull);
+    }
+  }
+}
+
 // Multi-seed (config C3, kv_hash_meow128_4_same_length_4_seed with one key
 // in all slots, key_hash.c:1891-1937): LA = 2, 4 or 8 lanes per key, lane l
 // hashes under seed (l & (LA-1)).  The output slot of (key i, seed a) is
@@ -156,6 +296,22 @@ int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t
              hipStream_t st, int cus) {
   const bool a16 = ((uintptr_t)keys & 15) == 0;
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
+  if (const int ord = knob(g_tune_order); ord != 0) {
+    unsigned long long* tk = nullptr;
+    if (int rc = stream_tickets(st, &tk)) return rc;
+#define KVH_Q(A, R) hipLaunchKernelGGL((k_fixed_q<L, NT, A, U, R>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, \
+                                       out, flags, tk)
+    if (ord == 4) {
+      if (a16)
+        hipLaunchKernelGGL((k_fixed_qw<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags, tk);
+      else
+        hipLaunchKernelGGL((k_fixed_qw<L, NT, false, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags,
+                           tk);
+    } else if (a16) { if (ord == 1) KVH_Q(true, 1); else if (ord == 2) KVH_Q(true, 4); else KVH_Q(true, 16); }
+    else { if (ord == 1) KVH_Q(false, 1); else if (ord == 2) KVH_Q(false, 4); else KVH_Q(false, 16); }
+#undef KVH_Q
+    return launch_done();
+  }
   if (a16)
     hipLaunchKernelGGL((k_fixed<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
   else

@@ -194,6 +194,8 @@ int hip_err(hipError_t e);
 int device_cus(int* cus);
 // hipGetLastError after a launch -> 0 or the recorded error
 int launch_done();
+// the (device, stream)'s ticket counter pair for the in-order streaming kernels (kvh.hip)
+int stream_tickets(hipStream_t st, unsigned long long** tk);
 // variable-length CRC32C kernel: 3 = length-sorted windows on 16-copy tables (default), 1 = on 32-copy
 // tables, 0 = lane per key in input order
 // (tuning knobs are atomics: kvh_set_tuning may run concurrently with launches)
@@ -218,6 +220,7 @@ extern std::atomic<int> g_tune_tok;
 // the generic kernel, keys per lane, multi-seed lanes per key,
 // variable-length kernel.
 extern std::atomic<int> g_tune_nt, g_tune_wgmul, g_tune_generic, g_tune_kpl, g_tune_ms_lanes, g_tune_var;
+extern std::atomic<int> g_tune_order;  // knob 24: fixed-length chunks in address order from tickets (1) or static (0)
 inline int knob(const std::atomic<int>& k) { return k.load(std::memory_order_relaxed); }
 // workgroups of kBlock threads for n items: wg_per_cu per CU (times knob 1), at most one per kBlock items
 inline uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {

@@ -84,6 +84,58 @@ def test_fixed_every_keys_per_lane_knob(kvh, kpl):
         kvh.lib.kvh_set_tuning(3, prev)
 
 
+@pytest.mark.parametrize("order", [1, 2, 3, 4])
+def test_fixed_in_order_tickets(kvh, order):
+    """k_fixed_q (knob 24 = 1/2/3: 1/4/16 workgroup-rounds per ticket) and k_fixed_qw (4): chunks
+    taken in address order from a per-stream ticket counter that the last
+    workgroup resets.  Equal to the static-order kernel (knob 24 = 0, the
+    default) and the oracle over ragged sizes
+    (one key, under one workgroup-iteration, ragged last chunks), over many
+    launches in a row on one stream (the reset), and with launches on two
+    streams in flight at once (separate counters)."""
+    rng = np.random.default_rng(24)
+    prev_order = kvh.lib.kvh_set_tuning(24, order)
+    try:
+        _tickets_cases(kvh, rng)
+    finally:
+        kvh.lib.kvh_set_tuning(24, prev_order)
+
+
+def _tickets_cases(kvh, rng):
+    for L in (16, 32, 64, 24):
+        for n in (1, 63, 4095, 4097, 65536 * 3 + 5, 1_000_003):
+            kb = rng.integers(0, 256, n * L, dtype=np.uint8)
+            t = dev(kb)
+            got = u64(kvh.meow128_fixed(t, L, STATIC))
+            prev = kvh.lib.kvh_set_tuning(24, 0)
+            try:
+                stat = u64(kvh.meow128_fixed(t, L, STATIC))
+            finally:
+                kvh.lib.kvh_set_tuning(24, prev)
+            np.testing.assert_array_equal(got, stat, err_msg=f"L={L} n={n}")
+            m = min(n, 3000)
+            np.testing.assert_array_equal(got[:m], orc_fixed(ORC, kb[:m * L], L, STATIC))
+            np.testing.assert_array_equal(got[-m:], orc_fixed(ORC, kb[(n - m) * L:], L, STATIC))
+    # many launches in a row: every one must start from a zero counter
+    n = 2_000_003
+    t = torch.randint(0, 256, (n * 16,), dtype=torch.uint8, device="cuda")
+    want = kvh.meow128_fixed(t, 16, STATIC)
+    outs = [torch.empty_like(want) for _ in range(50)]
+    for o in outs:
+        kvh.meow128_fixed(t, 16, STATIC, out=o)
+    torch.cuda.synchronize()
+    assert all(torch.equal(o, want) for o in outs)
+    # two streams at once
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    o1, o2 = torch.empty_like(want), torch.empty_like(want)
+    torch.cuda.synchronize()
+    for _ in range(10):
+        kvh.meow128_fixed(t, 16, STATIC, out=o1, stream=s1)
+        kvh.meow128_fixed(t, 16, STATIC, out=o2, stream=s2)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, want) and torch.equal(o2, want)
+
+
 def test_all_lengths_0_300_all_paths(kvh):
     g = golden("lengths.npz")
     keys, seeds, out = g["keys"], g["seeds"], g["out"]

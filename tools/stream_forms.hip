@@ -26,6 +26,9 @@
 //   f4u<U>       one-shot grid, U items per thread, nt
 //   chunk_dyn    persistent chunk form taking chunks from a global counter
 //                (all of them, or the last 12.5 % after a static share)
+//   f4u_scr      f4u with the blocks in a scrambled order
+//   chunk_q      persistent workgroups taking workgroup-iterations in address
+//                order from one counter per XCD (q8) or one global one (q1)
 //
 // usage: stream_forms [n_items=100000000] [settle_ms=500] [rounds=5] [reps=20]
 #include <hip/hip_runtime.h>
@@ -190,6 +193,50 @@ __global__ void __launch_bounds__(1024) chunk_dyn(const v4u* __restrict__ in, v4
   if (probe) clk_end(ck, c0, w0);
 }
 
+// persistent workgroups taking whole workgroup-iterations (one chunk per
+// wave) IN ADDRESS ORDER from a counter, the next ticket fetched one
+// iteration ahead: the chunks in flight stay one compact window, as in a
+// one-shot grid.  NQ = 8: one counter and one contiguous eighth of the array
+// per XCD (workgroup b on XCD b % 8); NQ = 1: one global counter.
+template <int U, int NQ>
+__global__ void __launch_bounds__(1024) chunk_q(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n,
+                                                Clk* ck, unsigned long long* ctr) {
+  const bool probe = (blockIdx.x & 63) == 0 && threadIdx.x == 0;
+  uint64_t c0 = 0, w0 = 0;
+  if (probe) clk_begin(c0, w0);
+  __shared__ unsigned long long tk[2];
+  const uint32_t tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, wpb = blockDim.x >> 6;
+  const uint64_t last = n - 1, nch = (n + 64 * U - 1) / (64 * U);
+  const uint32_t q = NQ == 1 ? 0u : blockIdx.x % NQ;
+  const uint64_t c_lo = nch * q / NQ, c_hi = nch * (q + 1) / NQ;
+  if (tid == 0) tk[0] = atomicAdd(ctr + q, 1ull);
+  __syncthreads();
+  for (uint32_t it = 0;; it++) {
+    const uint64_t t = tk[it & 1];
+    if (tid == 0) tk[(it + 1) & 1] = atomicAdd(ctr + q, 1ull);
+    const uint64_t c = c_lo + t * wpb + wv;
+    if (c_lo + t * wpb >= c_hi) break;  // workgroup-uniform
+    if (c < c_hi) {
+      const uint64_t b = c * 64 * U;
+      v4u X[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t j = b + 64 * u + lane;
+        X[u] = __builtin_nontemporal_load(in + (j < last ? j : last));
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t j = b + 64 * u + lane;
+        v4u v = X[u];
+        v.x ^= 0x9e3779b9u;
+        __builtin_nontemporal_store(v, out + (j < last ? j : last));
+      }
+    }
+    __syncthreads();
+  }
+  if (probe) clk_end(ck, c0, w0);
+}
+
 // one-shot grid, U items per thread (non-persistent, 256-thread workgroups)
 template <int U>
 __global__ void __launch_bounds__(256) f4u(const v4u* __restrict__ in, v4u* __restrict__ out, uint64_t n, Clk* ck) {
@@ -281,7 +328,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&out, n * 16));
   CK(hipMalloc(&ck, sizeof(Clk)));
   unsigned long long* ctr = nullptr;
-  CK(hipMalloc(&ctr, 8));
+  CK(hipMalloc(&ctr, 64));
   CK(hipMemset(in, 1, n * 16));
   const std::vector<Form> forms = {
       {"chunk4_g1 (k_fixed/copy_peak shape)", 0, 4, 1}, {"chunk4_g2", 0, 4, 2}, {"chunk8_g1", 0, 8, 1},
@@ -291,7 +338,10 @@ int main(int argc, char** argv) {
       {"f4u4nt (one-shot grid, 4 items per thread)", 6, 4, 0}, {"f4u2nt", 6, 2, 0},
       {"chunk4_dyn_all (every chunk from a counter, 4 per grab)", 7, 4, 0},
       {"chunk4_dyn_tail (87.5% static, then the counter)", 7, 4, 83},
-      {"f4u4nt_scrambled (one-shot, blocks in a scrambled order)", 8, 4, 0}};
+      {"f4u4nt_scrambled (one-shot, blocks in a scrambled order)", 8, 4, 0},
+      {"chunk4_q8 (in-order tickets, one counter per XCD)", 9, 4, 8},
+      {"chunk4_q1 (in-order tickets, one global counter)", 9, 4, 1},
+      {"chunk8_q8", 9, 8, 8}};
   auto launch = [&](const Form& f) {
     if (f.kind == 0) {
       const dim3 grid(cus * f.g), block(1024);
@@ -308,6 +358,11 @@ int main(int argc, char** argv) {
       else hipLaunchKernelGGL(chunk_pf<4>, grid, block, 0, 0, in, out, n, ck);
     } else if (f.kind == 5) {
       hipLaunchKernelGGL(chunk_xi<4>, dim3(cus * f.g), dim3(1024), 0, 0, in, out, n, ck);
+    } else if (f.kind == 9) {
+      CK(hipMemsetAsync(ctr, 0, 64, 0));
+      if (f.g == 8 && f.U == 4) hipLaunchKernelGGL((chunk_q<4, 8>), dim3(cus), dim3(1024), 0, 0, in, out, n, ck, ctr);
+      else if (f.g == 8) hipLaunchKernelGGL((chunk_q<8, 8>), dim3(cus), dim3(1024), 0, 0, in, out, n, ck, ctr);
+      else hipLaunchKernelGGL((chunk_q<4, 1>), dim3(cus), dim3(1024), 0, 0, in, out, n, ck, ctr);
     } else if (f.kind == 8) {
       uint32_t G = (uint32_t)((n + 256 * 4 - 1) / (256 * 4));
       G |= 1u;  // odd; gcd(G, 2654435761) = 1 at the default n (a bijection)
