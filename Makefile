@@ -10,7 +10,7 @@ SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/kvh_fixed.hip raikv_amd/csrc/k
 OBJS     := $(SRCS:.hip=.o)
 HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/csrc/kvh_internal.hpp \
             raikv_amd/csrc/ht_pos.hpp raikv_amd/csrc/bs_prelude.hpp raikv_amd/csrc/bs_aes.hpp \
-            raikv_amd/csrc/bs_meow.hpp raikv_amd/csrc/kvh_var.hpp include/kvh.h include/raikv_amd/key_hash.hpp
+            raikv_amd/csrc/bs_meow.hpp raikv_amd/csrc/kvh_var.hpp raikv_amd/csrc/tickets.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
 CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/host_latency tests/cpp/paths_gpu \
              tools/copy_peak tools/fetch_calib tools/scatter2_probe tools/stream_forms tools/scatter2_real

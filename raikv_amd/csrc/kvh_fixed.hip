@@ -15,6 +15,7 @@
 #include "meow_dev.hpp"
 #include "kvh_internal.hpp"
 #include "kvh_var.hpp"
+#include "tickets.hpp"
 #include "../../include/kvh.h"
 
 using namespace kvh;
@@ -83,8 +84,10 @@ __global__ void __launch_bounds__(kBlock)
 k_fixed_q(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out,
           uint32_t flags, unsigned long long* __restrict__ tk) {
   constexpr int NC = Plan<L>::NC;
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  __shared__ unsigned long long tkl[2];
+  struct Smem { uint32_t tab[LdsTab<NT>::kWords]; unsigned long long tkl[2]; };  // tables first
+  __shared__ Smem sm;
+  uint32_t* lds = sm.tab;
+  unsigned long long* tkl = sm.tkl;
   fill_tables<NT>(lds);
   if (threadIdx.x == 0) tkl[0] = atomicAdd(tk, 1ull);
   __syncthreads();
@@ -129,83 +132,47 @@ k_fixed_q(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2
   }
 }
 
-// k_fixed_qw: the same in-order tickets without the per-ticket barrier.  The
-// workgroup's waves take chunks one at a time from an LDS counter; the
-// global ticket for chunks 16j .. 16j+15 of the workgroup is fetched by the
-// wave that takes chunk 16(j-2) and published in a 16-slot LDS ring with its
-// index as a tag, so each wave runs at its own pace (its loads under the
-// other waves' rounds, as in k_fixed) while the chip's chunks in flight stay
-// one address window.  A wave whose ticket is not yet published sleeps on the
-// tag (it was fetched two tickets ahead, so this is rare).
+// k_fixed_qw: the same in-order tickets without the per-ticket barrier
+// (tickets.hpp: each wave takes chunks one at a time through an LDS counter
+// and a ring of prefetched workgroup tickets), so each wave runs at its own
+// pace -- its loads under the other waves' rounds, as in k_fixed -- while
+// the chip's chunks in flight stay one address window.
 template <int L, int NT, bool A16, int U>
 __global__ void __launch_bounds__(kBlock)
 k_fixed_qw(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out,
            uint32_t flags, unsigned long long* __restrict__ tk) {
-  constexpr int NC = Plan<L>::NC, kRing = 16;
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  __shared__ unsigned long long ring[kRing];
-  __shared__ uint32_t tag[kRing];
-  __shared__ uint32_t lk;
+  constexpr int NC = Plan<L>::NC;
+  // one LDS object, tables first (a lookup address is the v_perm result itself)
+  struct Smem { uint32_t tab[LdsTab<NT>::kWords]; WaveTickets W; };
+  __shared__ Smem sm;
+  uint32_t* lds = sm.tab;
+  WaveTickets& W = sm.W;
   fill_tables<NT>(lds);
-  if (threadIdx.x < kRing) tag[threadIdx.x] = 0;  // tag = ticket index + 1 (0: none yet); only grows
-  if (threadIdx.x == 0) lk = 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    ring[0] = atomicAdd(tk, 1ull);
-    ring[1] = atomicAdd(tk, 1ull);
-    tag[0] = 1;
-    tag[1] = 2;
-  }
-  __syncthreads();
+  wt_init(W, tk);
   const LdsTab<NT> T(lds);
   const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
   const bool fix = (flags & KVH_FIXUP) != 0;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint64_t last = n - 1, per_chunk = 64 * U;
+  const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
+  const uint64_t last = n - 1;
   for (;;) {
-    uint32_t k = 0;
-    if (lane == 0) k = atomicAdd(&lk, 1u);
-    k = __builtin_amdgcn_readfirstlane(k);
-    const uint32_t j = k / wpb, s = k - j * wpb;
-    if (s == 0 && lane == 0) {  // this ticket's first taker fetches the one two ahead
-      const unsigned long long g = atomicAdd(tk, 1ull);
-      ring[(j + 2) % kRing] = g;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __hip_atomic_store(&tag[(j + 2) % kRing], j + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // tags only grow, so this wait ends whatever the interleaving (a slot
-    // overtaken by ticket j + 16 would need 14 tickets -- 224 chunks -- handed
-    // out while this wave sits between its LDS atomic and this load)
-    while (__hip_atomic_load(&tag[j % kRing], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < j + 1)
-      __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const uint64_t t = ring[j % kRing];
-    const uint64_t b = (t * wpb + s) * per_chunk;
-    if (b >= n) break;  // wave-uniform: every later chunk of this wave lies further on
+    const uint64_t b = wt_next(W, tk, wpb) * (64 * U);
+    if (b >= n) break;  // wave-uniform: the wave's later chunks lie further on
     Blk D[U][NC];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t jj = b + 64 * u + lane;
-      load_fixed<L, A16, true>(keys + (jj < last ? jj : last) * L, D[u]);
+      const uint64_t j = b + 64 * u + lane;
+      load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
     }
     Blk h[U];
 #pragma unroll
     for (int u = 0; u < U; u++) h[u] = meow_ct<L>(D[u], K, T);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t jj = b + 64 * u + lane;
-      store_h<true>(out, jj < last ? jj : last, h[u], fix);
+      const uint64_t j = b + 64 * u + lane;
+      store_h<true>(out, j < last ? j : last, h[u], fix);
     }
   }
-  __syncthreads();  // every wave of this workgroup is past its last ticket use
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(tk + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
-      atomicExch(tk, 0ull);
-      atomicExch(tk + 1, 0ull);
-    }
-  }
+  wt_done(tk);
 }
 
 // Multi-seed (config C3, kv_hash_meow128_4_same_length_4_seed with one key

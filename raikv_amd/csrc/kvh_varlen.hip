@@ -15,6 +15,7 @@
 #include "meow_dev.hpp"
 #include "kvh_internal.hpp"
 #include "kvh_var.hpp"
+#include "tickets.hpp"
 #include "../../include/kvh.h"
 
 using namespace kvh;
@@ -256,10 +257,10 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 // register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
 // more take wide_window (input order, u64 offsets and lengths).
 
-template <int NT, int NW, int KF, bool PF = false, bool PKY = true, bool CL = false>
+template <int NT, int NW, int KF, bool PF = false, bool PKY = true, bool CL = false, bool Q = false>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
-       uint64_t* __restrict__ out, uint32_t flags) {
+       uint64_t* __restrict__ out, uint32_t flags, unsigned long long* __restrict__ tk = nullptr) {
   // per wave: the hash stage (4 KiB); while sorting it holds the bucket counts
   // (first KiB) and the sorted records (last 2 KiB), which each lane then
   // takes into registers (its four sorted positions) before hashes land
@@ -267,9 +268,10 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
   // one LDS object, tables first: a lookup address is then the v_perm result
   // itself (a table at a nonzero base costs one v_add per lookup)
   constexpr int kTabB = LdsTab<NT>::kWords * 4, kFullB = kLT * (int)sizeof(VConst9), kKfB = KF * 64;
-  constexpr int kBytes = kTabB + kFullB + kKfB + NW * AREA;
+  constexpr int kTkB = Q ? (int)sizeof(WaveTickets) : 0;  // the ticket ring, last
+  constexpr int kBytes = kTabB + kFullB + kKfB + NW * AREA + kTkB;
   static_assert(kBytes <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint32_t smem[kBytes / 4];
+  __shared__ __attribute__((aligned(16))) uint32_t smem[(kBytes + 3) / 4];
   uint32_t* lds = smem;
   VConst9* kfull = (VConst9*)((uint8_t*)smem + kTabB);
   Blk* kf = (Blk*)((uint8_t*)smem + kTabB + kFullB);
@@ -300,7 +302,10 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
   const uint64_t nwin = (n + WIN - 1) / WIN;
   const uint64_t gw = (uint64_t)blockIdx.x * NW + wv, tw = (uint64_t)gridDim.x * NW;
   const uint64_t kend = offs[n];  // the buffer holds every byte up to the last key's end
-  for (uint64_t w = gw; w < nwin; w += tw) {
+  // Q (knob 7 = 46): windows in address order through wave tickets (tickets.hpp)
+  WaveTickets& WT = *(WaveTickets*)((uint8_t*)smem + kBytes - kTkB);
+  if constexpr (Q) wt_init(WT, tk);
+  for (uint64_t w = Q ? wt_next(WT, tk, NW) : gw; w < nwin; w = Q ? wt_next(WT, tk, NW) : w + tw) {
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
     const uint64_t ws = offs[i0];
@@ -389,6 +394,7 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     }
     wave_sync();  // stage and records reused by the next window
   }
+  if constexpr (Q) wt_done(tk);
 }
 
 }  // namespace
@@ -440,6 +446,13 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       hipLaunchKernelGGL((k_var9<2, 12, 192, true>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1,
                          seed2, out, flags);
       return launch_done();
+    case 46: {  // round-4 A/B: windows in address order (wave tickets)
+      unsigned long long* tk = nullptr;
+      if (int rc = stream_tickets(st, &tk)) return rc;
+      hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
+                         (uint64_t)n, seed1, seed2, out, flags, tk);
+      return launch_done();
+    }
     case 45:  // round-4 A/B: clamped group loads (AChunks::chunk_cl)
       hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
                          (uint64_t)n, seed1, seed2, out, flags);

@@ -1,0 +1,79 @@
+// tickets.hpp -- in-address-order work assignment for the persistent
+// streaming kernels (round 4).
+//
+// A persistent kernel that hands each wave a static sequence of chunks lets
+// the waves drift apart over a launch, and the chip's active address set
+// spreads: on MI355X a static-order copy streams 5.2-5.4 TB/s where the same
+// copy taking its chunks in address order streams 6.7 (tools/stream_forms.hip).
+// WaveTickets keeps the order without a workgroup barrier per step: the
+// workgroup's waves take items one at a time from an LDS counter; the global
+// ticket covering items [wpb j, wpb (j + 1)) of the workgroup (wpb = waves per
+// workgroup) is fetched from the launch's counter pair by the wave that takes
+// item wpb (j - 2), and published in a 16-slot LDS ring with j + 1 as its tag.
+// The counter pair belongs to one (device, stream) (rt::stream_tickets), is
+// zero at launch, and the last workgroup to finish puts it back to zero.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kvh {
+
+struct WaveTickets {
+  static constexpr int kRing = 16;
+  unsigned long long ring[kRing];
+  uint32_t tag[kRing];  // ticket index + 1 of the slot's ticket (0: none yet); only grows
+  uint32_t lk;          // next item of this workgroup
+};
+
+// every thread of the workgroup; ends with a barrier
+__device__ __forceinline__ void wt_init(WaveTickets& W, unsigned long long* tk) {
+  if (threadIdx.x < WaveTickets::kRing) W.tag[threadIdx.x] = 0;
+  if (threadIdx.x == 0) W.lk = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    W.ring[0] = atomicAdd(tk, 1ull);
+    W.ring[1] = atomicAdd(tk, 1ull);
+    W.tag[0] = 1;
+    W.tag[1] = 2;
+  }
+  __syncthreads();
+}
+
+// the wave's next global item index (wave-uniform); items are handed out in
+// address order across the whole launch, `wpb` per ticket
+__device__ __forceinline__ uint64_t wt_next(WaveTickets& W, unsigned long long* tk, uint32_t wpb) {
+  constexpr int R = WaveTickets::kRing;
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t k = 0;
+  if (lane == 0) k = atomicAdd(&W.lk, 1u);
+  k = __builtin_amdgcn_readfirstlane(k);
+  const uint32_t j = k / wpb, s = k - j * wpb;
+  if (s == 0 && lane == 0) {  // this ticket's first taker fetches the one two ahead
+    const unsigned long long g = atomicAdd(tk, 1ull);
+    W.ring[(j + 2) % R] = g;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __hip_atomic_store(&W.tag[(j + 2) % R], j + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  // tags only grow, so this wait ends whatever the interleaving (a slot
+  // overtaken by ticket j + 16 would need 14 tickets handed out while this
+  // wave sits between its LDS atomic and this load)
+  while (__hip_atomic_load(&W.tag[j % R], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < j + 1)
+    __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return W.ring[j % R] * wpb + s;
+}
+
+// every thread of the workgroup, after its last wt_next: the last workgroup
+// to get here resets the launch's counter pair
+__device__ __forceinline__ void wt_done(unsigned long long* tk) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(tk + 1, 1ull) == (unsigned long long)gridDim.x - 1) {
+      atomicExch(tk, 0ull);
+      atomicExch(tk + 1, 0ull);
+    }
+  }
+}
+
+}  // namespace kvh
