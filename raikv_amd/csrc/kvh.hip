@@ -219,12 +219,12 @@ using Knob = std::atomic<int>;
 namespace kvh {
 namespace rt {
 Knob g_tune_nt{0};        // tables per LDS: 2 or 4 (0 = per-length default)
-Knob g_tune_order{0};     // knob 24: fixed-length chunk order: 0 = static per wave (k_fixed); 1/2/3 = in address order from a ticket counter, 1/4/16 workgroup-rounds per ticket (k_fixed_q); 4 = the same without the per-ticket barrier (k_fixed_qw)
+Knob g_tune_order{0};     // knob 24: fixed-length chunk order: 0 = per-length default; 1 = static per wave (k_fixed); 2 = in address order through wave tickets (k_fixed_qw); 3/4/5 = in address order, one workgroup barrier per ticket of 1/4/16 rounds (k_fixed_q)
 Knob g_tune_wgmul{1};     // workgroups per CU multiplier
 Knob g_tune_generic{0};   // force the generic kernel
 Knob g_tune_kpl{0};       // keys per lane per chunk in k_fixed (0 = per-length default)
 Knob g_tune_ms_lanes{1};  // multi-seed: 1 = lanes-per-key kernel, 0 = one lane per key
-Knob g_tune_var{23};      // var-length kernel: 23 = k_var9 (16 waves; 24 = 12 waves, 25 = 12 waves + block prefetch); 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic
+Knob g_tune_var{46};      // var-length kernel: 46 = k_var9 with windows in address order (wave tickets); 23 = k_var9 static order (16 waves; 24 = 12 waves, 25 = 12 waves + block prefetch); 44 four tables x 16 copies, 45 clamped loads; 13 = k_var6 windows sorted by 16-byte length class; 7 = by exact length; 0 = unsorted k_generic
 }  // namespace rt
 }  // namespace kvh
 
@@ -1036,7 +1036,7 @@ int kvh_set_tuning(int k, int value) {
     case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
     case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_cap, value);
     case 23: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_b3, value);
-    case 24: if (value < 0 || value > 4) return KVH_EINVAL; return set(g_tune_order, value);
+    case 24: if (value < 0 || value > 5) return KVH_EINVAL; return set(g_tune_order, value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }

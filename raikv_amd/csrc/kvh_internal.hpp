@@ -220,7 +220,7 @@ extern std::atomic<int> g_tune_tok;
 // the generic kernel, keys per lane, multi-seed lanes per key,
 // variable-length kernel.
 extern std::atomic<int> g_tune_nt, g_tune_wgmul, g_tune_generic, g_tune_kpl, g_tune_ms_lanes, g_tune_var;
-extern std::atomic<int> g_tune_order;  // knob 24: fixed-length chunks in address order from tickets (1) or static (0)
+extern std::atomic<int> g_tune_order;  // knob 24: fixed-length chunk order (0 per-length default, 1 static, 2 wave tickets, 3-5 workgroup tickets)
 inline int knob(const std::atomic<int>& k) { return k.load(std::memory_order_relaxed); }
 // workgroups of kBlock threads for n items: wg_per_cu per CU (times knob 1), at most one per kBlock items
 inline uint32_t grid_for(uint64_t n, int cus, int wg_per_cu) {

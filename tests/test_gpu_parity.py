@@ -84,12 +84,12 @@ def test_fixed_every_keys_per_lane_knob(kvh, kpl):
         kvh.lib.kvh_set_tuning(3, prev)
 
 
-@pytest.mark.parametrize("order", [1, 2, 3, 4])
+@pytest.mark.parametrize("order", [0, 2, 3, 4, 5])
 def test_fixed_in_order_tickets(kvh, order):
-    """k_fixed_q (knob 24 = 1/2/3: 1/4/16 workgroup-rounds per ticket) and k_fixed_qw (4): chunks
-    taken in address order from a per-stream ticket counter that the last
-    workgroup resets.  Equal to the static-order kernel (knob 24 = 0, the
-    default) and the oracle over ragged sizes
+    """Knob 24: 0 the per-length default, 2 k_fixed_qw (wave tickets), 3/4/5
+    k_fixed_q (1/4/16 workgroup-rounds per ticket): chunks taken in address
+    order from a per-stream ticket counter that the last workgroup resets.
+    Equal to the static-order kernel (knob 24 = 1) and the oracle over ragged sizes
     (one key, under one workgroup-iteration, ragged last chunks), over many
     launches in a row on one stream (the reset), and with launches on two
     streams in flight at once (separate counters)."""
@@ -102,12 +102,12 @@ def test_fixed_in_order_tickets(kvh, order):
 
 
 def _tickets_cases(kvh, rng):
-    for L in (16, 32, 64, 24):
+    for L in (16, 32, 64, 24, 8, 40):
         for n in (1, 63, 4095, 4097, 65536 * 3 + 5, 1_000_003):
             kb = rng.integers(0, 256, n * L, dtype=np.uint8)
             t = dev(kb)
             got = u64(kvh.meow128_fixed(t, L, STATIC))
-            prev = kvh.lib.kvh_set_tuning(24, 0)
+            prev = kvh.lib.kvh_set_tuning(24, 1)
             try:
                 stat = u64(kvh.meow128_fixed(t, L, STATIC))
             finally:

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""A/B of the fixed-length chunk order (kvh_set_tuning(24, v): 0 = static
-per-wave order, k_fixed; 1/2/3 = in address order from a ticket counter,
-k_fixed_q with 1/4/16 workgroup-rounds per ticket) on the C1 / C4 / C64 shapes, one process, interleaved
+"""A/B of the fixed-length chunk order (kvh_set_tuning(24, v), knob 24:
+1 = static per-wave order, k_fixed; 2 = wave tickets, k_fixed_qw;
+3/4/5 = k_fixed_q with 1/4/16 workgroup-rounds per ticket; 0 = the per-length
+default) on the C1 / C4 / C64 shapes and the other multiples of 8, one process, interleaved
 rounds after a 500 ms settle, outputs asserted equal.  One JSON line per
 (shape, order)."""
 import json, os, sys, time
@@ -11,20 +12,28 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import raikv_amd as kvh  # noqa: E402
 
 torch.cuda.set_device(0)
-shapes = [(16, 100_000_000), (32, 125_000_000), (64, 100_000_000)]
+shapes = [(16, 100_000_000), (32, 125_000_000), (64, 100_000_000), (8, 100_000_000), (24, 100_000_000),
+          (40, 100_000_000), (48, 100_000_000), (56, 100_000_000), ("c3", 50_000_000)]
 if len(sys.argv) > 1:
     shapes = [s for s in shapes if str(s[0]) in sys.argv[1].split(",")]
+from raikv_amd.workload import C3_SEEDS  # noqa: E402
 st = torch.cuda.current_stream()
-VS = [int(x) for x in os.environ.get("ORDERS", "0,1,2,3").split(",")]
+VS = [int(x) for x in os.environ.get("ORDERS", "1,2").split(",")]
+NAMES = {0: "default", 1: "static", 2: "wave_tickets", 3: "tickets_r1", 4: "tickets_r4", 5: "tickets_r16"}
 g = torch.Generator(device="cuda")
 g.manual_seed(7)
 for L, n in shapes:
+    c3 = L == "c3"  # C3: 32-byte keys, arity-4 multi-seed (k_fixed_lanes)
+    if c3:
+        L = 32
     keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
-    out = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    out = torch.empty((n, 4, 2) if c3 else (n, 2), dtype=torch.int64, device="cuda")
+    hash_ = (lambda: kvh.meow128_multiseed(keys, L, list(C3_SEEDS), out=out)) if c3 else \
+        (lambda: kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out))
     ref = None
     for v in VS:
         kvh.lib.kvh_set_tuning(24, v)
-        kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out)
+        hash_()
         torch.cuda.synchronize()
         if ref is None:
             ref = out.clone()
@@ -33,26 +42,26 @@ for L, n in shapes:
     del ref
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
-        kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out)
+        hash_()
         torch.cuda.synchronize()
     res = {v: [] for v in VS}
     for r in range(6):
         for v in VS:
             kvh.lib.kvh_set_tuning(24, v)
-            kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out)
+            hash_()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
             for a, b in ev:
                 a.record(st)
-                kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out)
+                hash_()
                 b.record(st)
             torch.cuda.synchronize()
             res[v] += [a.elapsed_time(b) for a, b in ev]
     kvh.lib.kvh_set_tuning(24, 0)
     for v in VS:
         ms = float(np.median(res[v]))
-        print(json.dumps({"key_len": L, "n": n, "order": ["static", "tickets_r1", "tickets_r4", "tickets_r16", "wave_tickets"][v],
+        print(json.dumps({"key_len": L, "n": n, "arity": 4 if c3 else 1, "order": NAMES[v],
                           "median_ms": ms,
-                          "min_ms": float(np.min(res[v])), "G_hash_s": n / ms / 1e6,
-                          "alg_TBps": n * (L + 16) / ms / 1e9}), flush=True)
+                          "min_ms": float(np.min(res[v])), "G_hash_s": n * (4 if c3 else 1) / ms / 1e6,
+                          "alg_TBps": n * (L + 16 * (4 if c3 else 1)) / ms / 1e9}), flush=True)
     del keys, out
     torch.cuda.empty_cache()
