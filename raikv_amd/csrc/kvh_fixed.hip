@@ -69,8 +69,8 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
   }
 }
 
-// k_fixed with the chunks taken IN ADDRESS ORDER (round 4, knob 24 = 1, the
-// default).  A workgroup-iteration (16 waves x 64U keys) is one ticket from a
+// k_fixed with the chunks taken IN ADDRESS ORDER (round 4, knob 24 = 3/4/5;
+// k_fixed_qw below is the default form).  A workgroup-iteration (16 waves x 64U keys) is one ticket from a
 // per-stream counter (stream_tickets), the next ticket fetched one iteration
 // ahead, so the chunks in flight on the whole chip form one compact address
 // window, as a one-shot grid's do.  k_fixed's static order lets waves drift
