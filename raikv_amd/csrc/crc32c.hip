@@ -28,6 +28,7 @@
 #include <mutex>
 #include <vector>
 #include "kvh_internal.hpp"
+#include "tickets.hpp"
 #include "../../include/kvh.h"
 
 using namespace kvh;
@@ -140,19 +141,24 @@ __device__ __forceinline__ uint32_t crc_key(const uint8_t* p, uint64_t len, uint
 // Compile-time length: every piece of the U keys of a chunk is loaded
 // before the first table step (U*ceil(L/16) 16-byte loads per lane in
 // flight), then the slice-by-4 chains run.
-template <int L, int U>
+template <int L, int U, bool Q = false>
 __global__ void __launch_bounds__(kBlock)
 k_crc_fixed_ct(const uint8_t* __restrict__ keys, uint64_t n, const uint32_t* __restrict__ seeds, uint32_t seed,
-               uint32_t* __restrict__ out) {
+               uint32_t* __restrict__ out, unsigned long long* __restrict__ tk = nullptr) {
   constexpr int NP = (L + 15) / 16;
-  __shared__ uint32_t lds[kWords];
+  // one LDS object, tables first; Q: chunks in address order through wave tickets (knob 24, tickets.hpp)
+  struct Smem { uint32_t tab[kWords]; WaveTickets W; };
+  __shared__ Smem sm;
+  uint32_t* lds = sm.tab;
   fill_crc(lds);
   __syncthreads();
+  if constexpr (Q) wt_init(sm.W, tk);
   const CrcLds T(lds);
   const uint64_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
-  for (uint64_t b = wave * 64 * U; b < n; b += step) {
+  for (uint64_t b = Q ? wt_next(sm.W, tk, blockDim.x >> 6) * (64 * U) : wave * 64 * U; b < n;
+       b = Q ? wt_next(sm.W, tk, blockDim.x >> 6) * (64 * U) : b + step) {
     Blk D[U][NP];
     uint32_t r[U];
 #pragma unroll
@@ -184,6 +190,7 @@ k_crc_fixed_ct(const uint8_t* __restrict__ keys, uint64_t n, const uint32_t* __r
       if (j < n) __builtin_nontemporal_store(r[u], out + j);
     }
   }
+  if constexpr (Q) wt_done(tk);
 }
 
 template <int U>
@@ -523,11 +530,20 @@ int kvh_crc_c_fixed(const void* keys, uint32_t key_len, size_t n, const uint32_t
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   const uint8_t* k = (const uint8_t*)keys;
+  // chunk order (knob 24): wave tickets (in address order) unless 1 = static
+  unsigned long long* tk = nullptr;
+  const bool q = knob(g_tune_order) != 1;
+  if (q)
+    if ((rc = stream_tickets(st, &tk))) return rc;
   switch (key_len) {
 #define KVH_CRC_L(Lv, Uv)                                                                                   \
   case Lv:                                                                                                  \
-    hipLaunchKernelGGL((k_crc_fixed_ct<Lv, Uv>), dim3(grid_crc((n + Uv - 1) / Uv, cus)), dim3(kBlock), 0, st, k, \
-                       (uint64_t)n, seeds, seed, out);                                                       \
+    if (q)                                                                                                  \
+      hipLaunchKernelGGL((k_crc_fixed_ct<Lv, Uv, true>), dim3(grid_crc((n + Uv - 1) / Uv, cus)), dim3(kBlock), 0, \
+                         st, k, (uint64_t)n, seeds, seed, out, tk);                                          \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k_crc_fixed_ct<Lv, Uv>), dim3(grid_crc((n + Uv - 1) / Uv, cus)), dim3(kBlock), 0, st, k, \
+                         (uint64_t)n, seeds, seed, out, nullptr);                                            \
     return launch_done();
     KVH_CRC_L(4, 8) KVH_CRC_L(8, 8) KVH_CRC_L(12, 8) KVH_CRC_L(16, 8) KVH_CRC_L(24, 4) KVH_CRC_L(32, 4)
     KVH_CRC_L(48, 2) KVH_CRC_L(64, 2)

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include "kvh_internal.hpp"
 #include "ht_pos.hpp"
+#include "tickets.hpp"
 #include "../../include/kvh.h"
 
 using namespace kvh;
@@ -149,14 +150,18 @@ k_positions(const uint64_t* __restrict__ hashes, uint64_t n, HtGeom g, void* __r
 // Fused epilogue on k_fixed's body (kvh.hip): the hash is fixed up
 // (KeyFragment::hash, hash_entry.h:84-85) because KeyCtx::set_key_hash
 // feeds the fixed-up h1 to ht_mod (key_ctx.cpp:97-105).
-template <int L, int NT, int A, bool P32, typename W, int U>
+template <int L, int NT, int A, bool P32, typename W, int U, bool Q = false>
 __global__ void __launch_bounds__(kFusedBlock)
 k_fixed_pos(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2, HtGeom g,
-            uint64_t* __restrict__ out, void* __restrict__ pos) {
+            uint64_t* __restrict__ out, void* __restrict__ pos, unsigned long long* __restrict__ tk = nullptr) {
   constexpr int NC = Plan<L>::NC;
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+  // one LDS object, tables first; Q: chunks in address order through wave tickets (knob 24, tickets.hpp)
+  struct Smem { uint32_t tab[LdsTab<NT>::kWords]; WaveTickets Wt; };
+  __shared__ Smem sm;
+  uint32_t* lds = sm.tab;
   fill_tables<NT>(lds);
   __syncthreads();
+  if constexpr (Q) wt_init(sm.Wt, tk);
   const LdsTab<NT> T(lds);
   const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
   const uint64_t lane = threadIdx.x & 63;
@@ -166,7 +171,8 @@ k_fixed_pos(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t 
   const bool keep = out != nullptr;
   constexpr bool PAIR = kPairRec<A, P32>;
   const uint64_t kofs = chunk_key(lane, PAIR);
-  for (uint64_t b = wave * 64 * U; b < n; b += step) {
+  for (uint64_t b = Q ? wt_next(sm.Wt, tk, blockDim.x >> 6) * (64 * U) : wave * 64 * U; b < n;
+       b = Q ? wt_next(sm.Wt, tk, blockDim.x >> 6) * (64 * U) : b + step) {
     Blk D[U][NC];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -189,6 +195,7 @@ k_fixed_pos(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t 
         store_pos<A, P32, W>(pos, j, q);
     }
   }
+  if constexpr (Q) wt_done(tk);
 }
 
 // ------------------------------------------------------------ host side
@@ -233,7 +240,11 @@ template <int A, bool P32>
 void launch_positions(const uint64_t* h, uint64_t n, HtGeom g, void* pos, hipStream_t st, int cus) {
   constexpr int U = 4;
   const uint64_t need = (n + kPosBlock * U - 1) / (kPosBlock * U);
-  const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)cus * 8));
+  // no LDS to fill, so the in-address-order form is simply a one-shot grid
+  // (the dispatcher hands blocks out in order); knob 24 = 1
+  // restores the persistent grid of 8 blocks per CU
+  const uint64_t grid = std::max<uint64_t>(
+      1, knob(g_tune_order) == 1 ? std::min<uint64_t>(need, (uint64_t)cus * 8) : std::min<uint64_t>(need, 1u << 30));
   if (narrow(g))
     hipLaunchKernelGGL((k_positions<A, P32, uint32_t, U>), dim3((uint32_t)grid), dim3(kPosBlock), 0, st, h, n, g,
                        pos);
@@ -259,29 +270,39 @@ int positions_a(uint32_t a, const uint64_t* h, uint64_t n, HtGeom g, void* pos, 
 }
 
 template <int L, int A, bool P32>
-void launch_fused(const uint8_t* k, uint64_t n, uint64_t s1, uint64_t s2, HtGeom g, uint64_t* out, void* pos,
-                  hipStream_t st, int cus) {
+int launch_fused(const uint8_t* k, uint64_t n, uint64_t s1, uint64_t s2, HtGeom g, uint64_t* out, void* pos,
+                 hipStream_t st, int cus) {
   constexpr int NT = 2, U = 2;
   const uint64_t need = (n + kFusedBlock - 1) / kFusedBlock;
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)cus * 2));
-  if (narrow(g))
-    hipLaunchKernelGGL((k_fixed_pos<L, NT, A, P32, uint32_t, U>), dim3((uint32_t)grid), dim3(kFusedBlock), 0, st, k,
-                       n, s1, s2, g, out, pos);
-  else if constexpr (!P32)
-    hipLaunchKernelGGL((k_fixed_pos<L, NT, A, P32, uint64_t, U>), dim3((uint32_t)grid), dim3(kFusedBlock), 0, st, k,
-                       n, s1, s2, g, out, pos);
+  // chunk order (knob 24): wave tickets (in address order) unless 1 = static
+  unsigned long long* tk = nullptr;
+  const bool q = knob(g_tune_order) != 1;
+  if (q)
+    if (int rc = stream_tickets(st, &tk)) return rc;
+#define KVH_FP(Wt, Qv) hipLaunchKernelGGL((k_fixed_pos<L, NT, A, P32, Wt, U, Qv>), dim3((uint32_t)grid), \
+                                          dim3(kFusedBlock), 0, st, k, n, s1, s2, g, out, pos, tk)
+  if (narrow(g)) {
+    if (q) KVH_FP(uint32_t, true); else KVH_FP(uint32_t, false);
+  } else if constexpr (!P32) {
+    if (q) KVH_FP(uint64_t, true); else KVH_FP(uint64_t, false);
+  }
+#undef KVH_FP
+  return 0;
 }
 
 template <int L, bool P32>
 int fused_a(uint32_t a, const uint8_t* k, uint64_t n, uint64_t s1, uint64_t s2, HtGeom g, uint64_t* out,
             void* pos, hipStream_t st, int cus) {
+  int rc = 0;
   switch (a) {
-    case 1: launch_fused<L, 1, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
-    case 2: launch_fused<L, 2, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
-    case 4: launch_fused<L, 4, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
-    case 8: launch_fused<L, 8, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
+    case 1: rc = launch_fused<L, 1, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
+    case 2: rc = launch_fused<L, 2, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
+    case 4: rc = launch_fused<L, 4, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
+    case 8: rc = launch_fused<L, 8, P32>(k, n, s1, s2, g, out, pos, st, cus); break;
     default: return set_err(KVH_EINVAL);
   }
+  if (rc) return rc;
   return launch_done();
 }
 

@@ -270,10 +270,11 @@ int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t
   const bool a16 = ((uintptr_t)keys & 15) == 0;
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
   // chunk order (knob 24): wave tickets (in address order)
-  // by default up to 32-byte keys, where they measured 7-11 % faster; the
-  // static order above that (64 B: 6 % slower with tickets)
+  // by default where they measured faster (8-32 B: 5-11 %, 48 / 56 B: 3 / 6 %,
+  // profiles/r04/s10/order_ab.jsonl); the static order at 40 and 64 B (4 / 5 %
+  // slower with tickets)
   int ord = knob(g_tune_order);
-  if (ord == 0) ord = L <= 32 ? 2 : 1;
+  if (ord == 0) ord = (L <= 32 || L == 48 || L == 56) ? 2 : 1;
   if (ord != 1) {
     unsigned long long* tk = nullptr;
     if (int rc = stream_tickets(st, &tk)) return rc;

@@ -9,7 +9,10 @@
 // workgroup's waves take items one at a time from an LDS counter; the global
 // ticket covering items [wpb j, wpb (j + 1)) of the workgroup (wpb = waves per
 // workgroup) is fetched from the launch's counter pair by the wave that takes
-// item wpb (j - 2), and published in a 16-slot LDS ring with j + 1 as its tag.
+// item wpb (j - 2), and published in a 16-slot LDS ring with j + 1 as its tag;
+// a slot is rewritten (with ticket j + 16) only after all wpb takers of
+// ticket j have read it (per-slot read counts), so a wave that stalls between
+// taking its item and reading the ring still reads its own ticket.
 // The counter pair belongs to one (device, stream) (rt::stream_tickets), is
 // zero at launch, and the last workgroup to finish puts it back to zero.
 #pragma once
@@ -22,12 +25,13 @@ struct WaveTickets {
   static constexpr int kRing = 16;
   unsigned long long ring[kRing];
   uint32_t tag[kRing];  // ticket index + 1 of the slot's ticket (0: none yet); only grows
+  uint32_t rd[kRing];   // reads of the slot so far (wpb per ticket it has held)
   uint32_t lk;          // next item of this workgroup
 };
 
 // every thread of the workgroup; ends with a barrier
 __device__ __forceinline__ void wt_init(WaveTickets& W, unsigned long long* tk) {
-  if (threadIdx.x < WaveTickets::kRing) W.tag[threadIdx.x] = 0;
+  if (threadIdx.x < WaveTickets::kRing) { W.tag[threadIdx.x] = 0; W.rd[threadIdx.x] = 0; }
   if (threadIdx.x == 0) W.lk = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -49,18 +53,24 @@ __device__ __forceinline__ uint64_t wt_next(WaveTickets& W, unsigned long long* 
   k = __builtin_amdgcn_readfirstlane(k);
   const uint32_t j = k / wpb, s = k - j * wpb;
   if (s == 0 && lane == 0) {  // this ticket's first taker fetches the one two ahead
+    const uint32_t jn = j + 2, sl = jn % R;
     const unsigned long long g = atomicAdd(tk, 1ull);
-    W.ring[(j + 2) % R] = g;
+    // the slot's previous ticket (jn - R) read by all its takers first; they
+    // wait on nothing later than their own ticket, so this wait ends
+    if (jn >= (uint32_t)R)
+      while (__hip_atomic_load(&W.rd[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (jn / R) * wpb)
+        __builtin_amdgcn_s_sleep(1);
+    W.ring[sl] = g;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __hip_atomic_store(&W.tag[(j + 2) % R], j + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&W.tag[sl], jn + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  // tags only grow, so this wait ends whatever the interleaving (a slot
-  // overtaken by ticket j + 16 would need 14 tickets handed out while this
-  // wave sits between its LDS atomic and this load)
+  // tags only grow, and the slot keeps ticket j until this wave has read it
   while (__hip_atomic_load(&W.tag[j % R], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < j + 1)
     __builtin_amdgcn_s_sleep(1);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  return W.ring[j % R] * wpb + s;
+  const unsigned long long t = W.ring[j % R];
+  if (lane == 0) __hip_atomic_fetch_add(&W.rd[j % R], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return t * wpb + s;
 }
 
 // every thread of the workgroup, after its last wt_next: the last workgroup

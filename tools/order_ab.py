@@ -4,7 +4,9 @@
 3/4/5 = k_fixed_q with 1/4/16 workgroup-rounds per ticket; 0 = the per-length
 default) on the C1 / C4 / C64 shapes and the other multiples of 8, one process, interleaved
 rounds after a 500 ms settle, outputs asserted equal.  One JSON line per
-(shape, order)."""
+(shape, order).  c3 = C3 (32-byte keys, four seeds, k_fixed_lanes); f1 = the
+fused hash + positions kernel (k_fixed_pos), f1p = positions from resident
+hashes (k_positions), f4 = CRC32C of 16-byte keys (k_crc_fixed_ct)."""
 import json, os, sys, time
 import numpy as np
 import torch
@@ -13,7 +15,8 @@ import raikv_amd as kvh  # noqa: E402
 
 torch.cuda.set_device(0)
 shapes = [(16, 100_000_000), (32, 125_000_000), (64, 100_000_000), (8, 100_000_000), (24, 100_000_000),
-          (40, 100_000_000), (48, 100_000_000), (56, 100_000_000), ("c3", 50_000_000)]
+          (40, 100_000_000), (48, 100_000_000), (56, 100_000_000), ("c3", 50_000_000), ("f1", 100_000_000),
+          ("f1p", 100_000_000), ("f4", 100_000_000)]
 if len(sys.argv) > 1:
     shapes = [s for s in shapes if str(s[0]) in sys.argv[1].split(",")]
 from raikv_amd.workload import C3_SEEDS  # noqa: E402
@@ -22,14 +25,29 @@ VS = [int(x) for x in os.environ.get("ORDERS", "1,2").split(",")]
 NAMES = {0: "default", 1: "static", 2: "wave_tickets", 3: "tickets_r1", 4: "tickets_r4", 5: "tickets_r16"}
 g = torch.Generator(device="cuda")
 g.manual_seed(7)
+F1_GEOM = dict(map_size=64 << 30, hash_entry_size=64, hash_value_ratio=1.0, cuckoo_buckets=4, cuckoo_arity=4)
 for L, n in shapes:
-    c3 = L == "c3"  # C3: 32-byte keys, arity-4 multi-seed (k_fixed_lanes)
-    if c3:
-        L = 32
+    tag = L if isinstance(L, str) else None
+    L = 32 if tag == "c3" else 16 if tag else L
     keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
-    out = torch.empty((n, 4, 2) if c3 else (n, 2), dtype=torch.int64, device="cuda")
-    hash_ = (lambda: kvh.meow128_multiseed(keys, L, list(C3_SEEDS), out=out)) if c3 else \
-        (lambda: kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out))
+    if tag == "c3":
+        out = torch.empty((n, 4, 2), dtype=torch.int64, device="cuda")
+        hash_ = lambda: kvh.meow128_multiseed(keys, L, list(C3_SEEDS), out=out)
+    elif tag in ("f1", "f1p"):
+        geom = kvh.HtGeom.from_map(**F1_GEOM)
+        hashes = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+        out = torch.empty((n, geom.per_key), dtype=torch.int64, device="cuda")
+        if tag == "f1":
+            hash_ = lambda: kvh.meow128_fixed_positions(keys, L, kvh.STATIC_SEED, geom, hashes=hashes, out=out)
+        else:
+            kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=hashes, fixup=True)
+            hash_ = lambda: kvh.ht_positions(hashes, geom, out=out)
+    elif tag == "f4":
+        out = torch.empty((n,), dtype=torch.int32, device="cuda")
+        hash_ = lambda: kvh.crc_c_fixed(keys, L, 0, out=out)
+    else:
+        out = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+        hash_ = lambda: kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out)
     ref = None
     for v in VS:
         kvh.lib.kvh_set_tuning(24, v)
@@ -59,9 +77,8 @@ for L, n in shapes:
     kvh.lib.kvh_set_tuning(24, 0)
     for v in VS:
         ms = float(np.median(res[v]))
-        print(json.dumps({"key_len": L, "n": n, "arity": 4 if c3 else 1, "order": NAMES[v],
-                          "median_ms": ms,
-                          "min_ms": float(np.min(res[v])), "G_hash_s": n * (4 if c3 else 1) / ms / 1e6,
-                          "alg_TBps": n * (L + 16 * (4 if c3 else 1)) / ms / 1e9}), flush=True)
+        print(json.dumps({"shape": tag or f"L{L}", "key_len": L, "n": n, "order": NAMES[v], "median_ms": ms,
+                          "min_ms": float(np.min(res[v])), "G_units_s": n / ms / 1e6}), flush=True)
     del keys, out
+    hashes = None
     torch.cuda.empty_cache()
