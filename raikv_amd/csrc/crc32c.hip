@@ -342,10 +342,12 @@ __device__ __attribute__((noinline)) void crc_wide_window(const uint8_t* __restr
   }
 }
 
-template <int WIN, int NW, int SH = 0, int R = 32, int G = 0, int SUB = 1>
+// Q: windows taken in address order through wave tickets (tickets.hpp, knob 24)
+template <int WIN, int NW, int SH = 0, int R = 32, int G = 0, int SUB = 1, bool Q = false>
 __global__ void __launch_bounds__(NW * 64)
 k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
-                 const uint32_t* seeds, uint32_t seed, uint32_t* out) {  // seeds may alias out
+                 const uint32_t* seeds, uint32_t seed, uint32_t* out,
+                 unsigned long long* __restrict__ tk = nullptr) {  // seeds may alias out
   constexpr int M = WIN / 64;
   static_assert(WIN <= 256 * 4, "hist slice doubles as the CRC staging area");
   __shared__ uint32_t lds[R == 32 ? kWords : kWords / 2];
@@ -353,14 +355,17 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
   __shared__ uint32_t roff_s[NW][WIN];
   __shared__ uint16_t rlen_s[NW][WIN];
   __shared__ uint16_t ridx_s[NW][WIN];
+  __shared__ WaveTickets WT;
   fill_crc<R>(lds);
   __syncthreads();
+  if constexpr (Q) wt_init(WT, tk);
   const CrcLdsT<R> T(lds);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* hist = hist_s[wv];
   const uint64_t nwin = (n + WIN - 1) / WIN;
   const uint64_t kend = offs[n];  // the buffer holds every byte up to the last key's end
-  for (uint64_t w = (uint64_t)blockIdx.x * NW + wv; w < nwin; w += (uint64_t)gridDim.x * NW) {
+  for (uint64_t w = Q ? wt_next(WT, tk, NW) : (uint64_t)blockIdx.x * NW + wv; w < nwin;
+       w = Q ? wt_next(WT, tk, NW) : w + (uint64_t)gridDim.x * NW) {
     const uint64_t i0 = w * WIN;
     const uint32_t k = (uint32_t)(n - i0 < (uint64_t)WIN ? n - i0 : (uint64_t)WIN);
     const WinOffs<WIN> W = win_load<WIN>(offs, i0, k);
@@ -447,6 +452,7 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
     }
     wave_lds_sync();  // staging read before the next window's histogram
   }
+  if constexpr (Q) wt_done(tk);
 }
 
 }  // namespace
@@ -572,9 +578,17 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
   else if (v == 4)  // as 3, keys read as dwordx4 groups (crc_key_g)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 1>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
-  else if (v == 6)  // as 4, the next key's first two groups in flight
-    hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
-                       (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+  else if (v == 6) {  // as 4, the next key's first two groups in flight; windows in address order unless knob 24 = 1
+    if (knob(g_tune_order) != 1) {
+      unsigned long long* tk = nullptr;
+      if ((rc = stream_tickets((hipStream_t)stream, &tk))) return rc;
+      hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2, 1, true>), dim3(cus), dim3(1024), 0,
+                         (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, tk);
+    } else {
+      hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
+                         (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, nullptr);
+    }
+  }
   else if (v == 5)  // as 4, two sub-counters per length bucket in the window sort
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 1, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);

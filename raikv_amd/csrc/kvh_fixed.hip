@@ -375,13 +375,17 @@ __device__ __forceinline__ void meow_small(Blk (&D)[U][NC], uint32_t L, const Me
   }
 }
 
-template <int NC, int NT, int U>
+// Q: chunks in address order through wave tickets (tickets.hpp, knob 24)
+template <int NC, int NT, int U, bool Q = false>
 __global__ void __launch_bounds__(kBlock)
 k_fixed_rt(const uint8_t* __restrict__ keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2,
-           uint64_t* __restrict__ out, uint32_t flags) {
-  __shared__ uint32_t lds[LdsTab<NT>::kWords];
+           uint64_t* __restrict__ out, uint32_t flags, unsigned long long* __restrict__ tk = nullptr) {
+  struct Smem { uint32_t tab[LdsTab<NT>::kWords]; WaveTickets W; };  // tables first
+  __shared__ Smem sm;
+  uint32_t* lds = sm.tab;
   fill_tables<NT>(lds);
   __syncthreads();
+  if constexpr (Q) wt_init(sm.W, tk);
   const LdsTab<NT> T(lds);
   const MeowConst K = uniform(make_const(s1, s2, (uint64_t)L, T));
   const bool fix = (flags & KVH_FIXUP) != 0;
@@ -389,7 +393,8 @@ k_fixed_rt(const uint8_t* __restrict__ keys, uint64_t n, uint32_t L, uint64_t s1
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
   const uint64_t last = n - 1, total = n * (uint64_t)L;
-  for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
+  for (uint64_t b = Q ? wt_next(sm.W, tk, blockDim.x >> 6) * (64 * U) : wave * 64 * U; b < n;
+       b = Q ? wt_next(sm.W, tk, blockDim.x >> 6) * (64 * U) : b + step) {  // wave-uniform trip count
     const bool exact = (b + 64 * U) * (uint64_t)L + 32 > total;  // this chunk reaches the batch's end
     Blk D[U][NC];
 #pragma unroll
@@ -422,13 +427,22 @@ k_fixed_rt(const uint8_t* __restrict__ keys, uint64_t n, uint32_t L, uint64_t s1
       store_h<true>(out, j < last ? j : last, h[u], fix);
     }
   }
+  if constexpr (Q) wt_done(tk);
 }
 
 template <int NC, int NT, int U>
 int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2, uint64_t* out,
                     uint32_t flags, hipStream_t st, int cus) {
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
-  hipLaunchKernelGGL((k_fixed_rt<NC, NT, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, L, s1, s2, out, flags);
+  if (knob(g_tune_order) != 1) {  // chunk order (knob 24): wave tickets unless 1 = static
+    unsigned long long* tk = nullptr;
+    if (int rc = stream_tickets(st, &tk)) return rc;
+    hipLaunchKernelGGL((k_fixed_rt<NC, NT, U, true>), dim3(grid), dim3(kBlock), 0, st, keys, n, L, s1, s2, out,
+                       flags, tk);
+  } else {
+    hipLaunchKernelGGL((k_fixed_rt<NC, NT, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, L, s1, s2, out, flags,
+                       nullptr);
+  }
   return launch_done();
 }
 

@@ -102,7 +102,7 @@ def test_fixed_in_order_tickets(kvh, order):
 
 
 def _tickets_cases(kvh, rng):
-    for L in (16, 32, 64, 24, 8, 40):
+    for L in (16, 32, 64, 24, 8, 40, 48, 56):
         for n in (1, 63, 4095, 4097, 65536 * 3 + 5, 1_000_003):
             kb = rng.integers(0, 256, n * L, dtype=np.uint8)
             t = dev(kb)
@@ -134,6 +134,44 @@ def _tickets_cases(kvh, rng):
         kvh.meow128_fixed(t, 16, STATIC, out=o2, stream=s2)
     torch.cuda.synchronize()
     assert torch.equal(o1, want) and torch.equal(o2, want)
+
+
+@pytest.mark.parametrize("n", [1, 4097, 1_000_003])
+def test_order_knob_every_streaming_kernel(kvh, n):
+    """Every kernel that takes its chunks through wave tickets by default
+    (runtime-length k_fixed_rt, k_fixed_lanes (C3), the fused hash+positions
+    kernel, CRC32C of fixed and of variable-length keys) equals its
+    static-order form (knob 24 = 1) on the same input, twice in a row (the
+    counter reset)."""
+    from raikv_amd.workload import C3_SEEDS
+    rng = np.random.default_rng(n)
+    geom = kvh.HtGeom.from_map(map_size=1 << 30, hash_entry_size=64, hash_value_ratio=1.0, cuckoo_buckets=4,
+                               cuckoo_arity=4)
+    k16 = dev(rng.integers(0, 256, n * 16, dtype=np.uint8))
+    k32 = dev(rng.integers(0, 256, n * 32, dtype=np.uint8))
+    k20 = dev(rng.integers(0, 256, n * 20, dtype=np.uint8))
+    k50 = dev(rng.integers(0, 256, n * 50, dtype=np.uint8))
+    lens = rng.integers(0, 300, n).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    kv, dof = dev(rng.integers(0, 256, int(offs[-1]) + 1, dtype=np.uint8)), dev(offs.view(np.int64))
+    runs = {
+        "rt20": lambda: kvh.meow128_fixed(k20, 20, STATIC),
+        "rt50": lambda: kvh.meow128_fixed(k50, 50, STATIC),
+        "c3": lambda: kvh.meow128_multiseed(k32, 32, list(C3_SEEDS)),
+        "fused": lambda: torch.cat([t.view(torch.int64).reshape(n, -1) for t in
+                                    kvh.meow128_fixed_positions(k16, 16, STATIC, geom)], 1),
+        "crc16": lambda: kvh.crc_c_fixed(k16, 16, 7),
+        "crc_var": lambda: kvh.crc_c_var(kv, dof, 7),
+    }
+    for name, run in runs.items():
+        prev = kvh.lib.kvh_set_tuning(24, 1)
+        try:
+            want = run().cpu()
+        finally:
+            kvh.lib.kvh_set_tuning(24, prev)
+        for _ in range(2):
+            got = run().cpu()
+            assert torch.equal(got, want), f"{name} n={n}"
 
 
 def test_all_lengths_0_300_all_paths(kvh):

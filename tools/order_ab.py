@@ -6,7 +6,8 @@ default) on the C1 / C4 / C64 shapes and the other multiples of 8, one process, 
 rounds after a 500 ms settle, outputs asserted equal.  One JSON line per
 (shape, order).  c3 = C3 (32-byte keys, four seeds, k_fixed_lanes); f1 = the
 fused hash + positions kernel (k_fixed_pos), f1p = positions from resident
-hashes (k_positions), f4 = CRC32C of 16-byte keys (k_crc_fixed_ct)."""
+hashes (k_positions), f4 = CRC32C of 16-byte keys (k_crc_fixed_ct), f4v = CRC32C
+of the C2 zipf keys (k_crc_var_sorted); 20 / 33 / 50 B run k_fixed_rt."""
 import json, os, sys, time
 import numpy as np
 import torch
@@ -16,7 +17,8 @@ import raikv_amd as kvh  # noqa: E402
 torch.cuda.set_device(0)
 shapes = [(16, 100_000_000), (32, 125_000_000), (64, 100_000_000), (8, 100_000_000), (24, 100_000_000),
           (40, 100_000_000), (48, 100_000_000), (56, 100_000_000), ("c3", 50_000_000), ("f1", 100_000_000),
-          ("f1p", 100_000_000), ("f4", 100_000_000)]
+          ("f1p", 100_000_000), ("f4", 100_000_000), (20, 100_000_000), (33, 100_000_000), (50, 100_000_000),
+          ("f4v", 100_000_000)]
 if len(sys.argv) > 1:
     shapes = [s for s in shapes if str(s[0]) in sys.argv[1].split(",")]
 from raikv_amd.workload import C3_SEEDS  # noqa: E402
@@ -42,6 +44,13 @@ for L, n in shapes:
         else:
             kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=hashes, fixup=True)
             hash_ = lambda: kvh.ht_positions(hashes, geom, out=out)
+    elif tag == "f4v":
+        from raikv_amd.workload import zipf_lengths, offsets_from_lengths  # noqa: E402
+        offs_np = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=3))
+        keys = torch.randint(0, 256, (int(offs_np[-1]),), dtype=torch.uint8, device="cuda", generator=g)
+        offs = torch.from_numpy(offs_np.view(np.int64)).cuda()
+        out = torch.empty((n,), dtype=torch.int32, device="cuda")
+        hash_ = lambda: kvh.crc_c_var(keys, offs, 0, out=out)
     elif tag == "f4":
         out = torch.empty((n,), dtype=torch.int32, device="cuda")
         hash_ = lambda: kvh.crc_c_fixed(keys, L, 0, out=out)
