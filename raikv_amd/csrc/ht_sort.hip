@@ -598,19 +598,18 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
 // for its sorted positions and stores it coalesced.  The duplicate test takes
 // the successor's field from the same LDS round.  Runs of equal digit still
 // compare ties through global memory (rare, and those lines are L2-hot).
-// PF: the next bucket's lines are touched (one dword per 128-byte line) at
-// the start of this bucket's LDS phases, so its own loads later hit L2 /
-// MALL.  (The barriers do not wait for global accesses on gfx950 --
-// workgroup scope orders LDS only, s_waitcnt lgkmcnt -- so the output stores
-// already drain under the next bucket's phases.)
-template <uint32_t CAP, int D, int T = kBkT, bool PF = false>
+// (Its barriers do not wait for global accesses on gfx950 -- workgroup scope
+// orders LDS only, s_waitcnt lgkmcnt -- so a bucket's output stores already
+// drain under the next bucket's phases.  Touching the next bucket's lines at
+// the start of this one's LDS phases, so its loads would hit L2 / MALL, was
+// 4 % slower: profiles/r04/s12/.)
+template <uint32_t CAP, int D, int T = kBkT>
 __global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD (512 threads x 2 per CU spill: 87 VGPRs)
 k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
            uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
            uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
-           uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf, uint32_t* __restrict__ pf_sink = nullptr) {
+           uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
   static_assert(CAP % T == 0, "records per thread");
-  uint32_t pfacc = 0;
   constexpr uint32_t PER = CAP / T;
   constexpr uint32_t nd = 1u << D, per = nd / T;
   struct SortArrays {
@@ -648,20 +647,6 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
         f0[j] = __builtin_nontemporal_load(q);
         f1[j] = __builtin_nontemporal_load(q + 1);
         f2[j] = __builtin_nontemporal_load(q + 2);
-      }
-    }
-    uint32_t pfv[2] = {0u, 0u};
-    if constexpr (PF) {  // the next bucket's lines, one dword each (consumed after this bucket's field rounds)
-      const uint32_t bn = b + gridDim.x;
-      if (bn < nb) {
-        const uint32_t Rn = cnt[bn];
-        const uint8_t* pn = (const uint8_t*)(recs + start[bn]);
-        const uint32_t bytes = (Rn < CAP ? Rn : CAP) * (uint32_t)sizeof(R24);
-#pragma unroll
-        for (uint32_t q = 0; q < 2; q++) {
-          const uint32_t o = (tid + q * T) * 128u;
-          if (o < bytes) pfv[q] = *(const uint32_t*)(pn + o);
-        }
       }
     }
 #pragma unroll
@@ -763,10 +748,6 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       }
       __syncthreads();
     }
-    if constexpr (PF) pfacc ^= pfv[0] ^ pfv[1];
-  }
-  if constexpr (PF) {
-    if (pf_sink) pf_sink[blockIdx.x * T + tid] = pfacc;  // never set: keeps the prefetch loads
   }
   if (dedup && dups) {
     const uint32_t t = block_sum<T>(d_total, wsum);
@@ -1717,11 +1698,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       else if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 1)
         hipLaunchKernelGGL((k_bk_sortr<7168, 12>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
-                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf, nullptr);
-      else if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 3)
-        hipLaunchKernelGGL((k_bk_sortr<7168, 12, kBkT, true>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0,
-                           st, (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
-                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf, nullptr);
+                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
       else if (small_b)
         hipLaunchKernelGGL((k_bk_sort<8000, 12, R24>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
