@@ -270,11 +270,10 @@ int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t
   const bool a16 = ((uintptr_t)keys & 15) == 0;
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
   // chunk order (knob 24): wave tickets (in address order)
-  // by default where they measured faster (8-32 B: 5-11 %, 48 / 56 B: 3 / 6 %,
-  // profiles/r04/s10/order_ab.jsonl); the static order at 40 and 64 B (4 / 5 %
-  // slower with tickets)
+  // by default, at every length with the keys per lane re-swept under them
+  // (profiles/r04/s14/sweep.jsonl); knob 24 = 1: the static order
   int ord = knob(g_tune_order);
-  if (ord == 0) ord = (L <= 32 || L == 48 || L == 56) ? 2 : 1;
+  if (ord == 0) ord = 2;
   if (ord != 1) {
     unsigned long long* tk = nullptr;
     if (int rc = stream_tickets(st, &tk)) return rc;
@@ -455,11 +454,12 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
   if (int rc = 0; g_exp.fixed && g_exp.fixed(L, keys, n, s1, s2, out, flags, st, cus, knob(g_tune_nt), knob(g_tune_kpl), &rc))
     return rc;
   if constexpr (L == 16 || L == 32) {
-    // per-length defaults from tools/tune.py: Td0..Td3 in LDS
-    // (no rotations), 4 keys per lane at 16 B, 2 at 32 B
+    // per-length defaults: Td0..Td3 in LDS (no
+    // rotations), 4 keys per lane (32 B: 2 under the static order, 4 under
+    // wave tickets, 2.6 % apart: profiles/r04/s16/ab.jsonl)
     const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
     const int nt = tnt ? tnt : 4;
-    const int kpl = tkpl ? tkpl : (L == 16 ? 4 : 2);
+    const int kpl = tkpl ? tkpl : 4;
     switch (nt * 100 + kpl) {
       case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
       case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
@@ -471,12 +471,14 @@ int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, u
       case 208: return launch_k<L, 2, 8>(keys, n, s1, s2, out, flags, st, cus);
       default: break;  // a knob pair without an instance: this length's default
     }
-    return launch_k<L, 4, (L == 16 ? 4 : 2)>(keys, n, s1, s2, out, flags, st, cus);
+    return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
   } else {
-    // per-length defaults (NT, keys per lane) from tools/len_sweep.py over
-    // 100M keys (profiles/r03/len_sweep_*.jsonl): 24 B NT4/U4, 40-48 B
-    // NT4/U1, 56-64 B NT4/U2; 8 B (unmeasured) NT2/U4
-    constexpr int dnt = L == 8 ? 2 : 4, dkpl = L == 8 || L == 24 ? 4 : (L == 40 || L == 48) ? 1 : 2;
+    // per-length defaults (NT, keys per lane) under wave tickets, from the
+    // round-4 sweep over 100M keys (profiles/r04/s14/sweep.jsonl; the round-3
+    // static-order sweep had 40-48 B at U1 and 56-64 B at U2): 8 / 24 B
+    // U4, 40 / 48 B U3 (7 / 4 % over their previous defaults), 56 / 64 B U1
+    // (4 / 8 %); NT4 (8 B: 6 % over NT2, profiles/r04/s16/ab.jsonl)
+    constexpr int dnt = 4, dkpl = L == 8 || L == 24 ? 4 : (L == 40 || L == 48) ? 3 : 1;
     const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
     switch ((tnt ? tnt : dnt) * 100 + (tkpl ? tkpl : dkpl)) {
       case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
@@ -521,19 +523,20 @@ int launch_lanes_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t 
   const bool a16 = ((uintptr_t)keys & 15) == 0;
   if constexpr (L == 32) {
     // C3's length: Td0..Td3 in LDS (no rotates, one 16-wave workgroup per CU)
-    // and 2 keys per lane by default -- 118 vs 112 G hash/s for Td0/Td1 with
-    // two workgroups per CU (tools/tune.py, profiles/r02/c3_layout_ab.txt);
+    // -- 118 vs 112 G hash/s for Td0/Td1 with two workgroups per CU
+    // (tools/tune.py, profiles/r02/c3_layout_ab.txt) -- and 4 keys per lane by
+    // default under wave tickets (2.7 % over 2: profiles/r04/s16/ab.jsonl);
     // knobs 0 / 3 select the others
     const int nt = knob(g_tune_nt), kpl = knob(g_tune_kpl);
     if (a16) {
-      switch ((nt ? nt : 4) * 10 + (kpl ? kpl : 2)) {
+      switch ((nt ? nt : 4) * 10 + (kpl ? kpl : 4)) {
         case 22: break;
         case 21: return launch_lanes_v<L, 2, 1>(keys, n, s, arity, out, flags, st, cus);
         case 24: return launch_lanes_v<L, 2, 4>(keys, n, s, arity, out, flags, st, cus);
         case 41: return launch_lanes_v<L, 4, 1>(keys, n, s, arity, out, flags, st, cus);
         case 42: return launch_lanes_v<L, 4, 2>(keys, n, s, arity, out, flags, st, cus);
         case 44: return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);
-        default: return set_err(KVH_EINVAL);
+        default: return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);  // no instance: the default
       }
     }
   }

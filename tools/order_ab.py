@@ -15,15 +15,23 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import raikv_amd as kvh  # noqa: E402
 
 torch.cuda.set_device(0)
+for kv in filter(None, os.environ.get("KNOBS", "").split(",")):  # e.g. KNOBS=3=2 (keys per lane)
+    k, v = kv.split("=")
+    assert kvh.lib.kvh_set_tuning(int(k), int(v)) >= 0, kv
 shapes = [(16, 100_000_000), (32, 125_000_000), (64, 100_000_000), (8, 100_000_000), (24, 100_000_000),
           (40, 100_000_000), (48, 100_000_000), (56, 100_000_000), ("c3", 50_000_000), ("f1", 100_000_000),
           ("f1p", 100_000_000), ("f4", 100_000_000), (20, 100_000_000), (33, 100_000_000), (50, 100_000_000),
           ("f4v", 100_000_000)]
-if len(sys.argv) > 1:
-    shapes = [s for s in shapes if str(s[0]) in sys.argv[1].split(",")]
+if len(sys.argv) > 1:  # a comma list of shape names; any other key length runs 100M keys of it
+    known = {str(s[0]): s for s in shapes}
+    shapes = [known[t] if t in known else (int(t), 100_000_000) for t in sys.argv[1].split(",")]
 from raikv_amd.workload import C3_SEEDS  # noqa: E402
 st = torch.cuda.current_stream()
 VS = [int(x) for x in os.environ.get("ORDERS", "1,2").split(",")]
+KN = 24  # the knob the A/B alternates; VARY=K:v1,v2 alternates knob K instead of the chunk order
+if os.environ.get("VARY"):
+    KN, vals = os.environ["VARY"].split(":")
+    KN, VS = int(KN), [int(x) for x in vals.split(",")]
 NAMES = {0: "default", 1: "static", 2: "wave_tickets", 3: "tickets_r1", 4: "tickets_r4", 5: "tickets_r16"}
 g = torch.Generator(device="cuda")
 g.manual_seed(7)
@@ -59,7 +67,7 @@ for L, n in shapes:
         hash_ = lambda: kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out)
     ref = None
     for v in VS:
-        kvh.lib.kvh_set_tuning(24, v)
+        kvh.lib.kvh_set_tuning(KN, v)
         hash_()
         torch.cuda.synchronize()
         if ref is None:
@@ -72,9 +80,9 @@ for L, n in shapes:
         hash_()
         torch.cuda.synchronize()
     res = {v: [] for v in VS}
-    for r in range(6):
+    for r in range(int(os.environ.get("ROUNDS", "6"))):
         for v in VS:
-            kvh.lib.kvh_set_tuning(24, v)
+            kvh.lib.kvh_set_tuning(KN, v)
             hash_()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
             for a, b in ev:
@@ -83,10 +91,10 @@ for L, n in shapes:
                 b.record(st)
             torch.cuda.synchronize()
             res[v] += [a.elapsed_time(b) for a, b in ev]
-    kvh.lib.kvh_set_tuning(24, 0)
+    kvh.lib.kvh_set_tuning(KN, 0)
     for v in VS:
         ms = float(np.median(res[v]))
-        print(json.dumps({"shape": tag or f"L{L}", "key_len": L, "n": n, "order": NAMES[v], "median_ms": ms,
+        print(json.dumps({"shape": tag or f"L{L}", "knobs": os.environ.get("KNOBS", ""), "key_len": L, "n": n, "order": NAMES[v] if KN == 24 else f"knob{KN}={v}", "median_ms": ms,
                           "min_ms": float(np.min(res[v])), "G_units_s": n / ms / 1e6}), flush=True)
     del keys, out
     hashes = None
