@@ -602,7 +602,8 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
 // orders LDS only, s_waitcnt lgkmcnt -- so a bucket's output stores already
 // drain under the next bucket's phases.  Touching the next bucket's lines at
 // the start of this one's LDS phases, so its loads would hit L2 / MALL, was
-// 4 % slower: profiles/r04/s12/.)
+// 4 % slower: profiles/r04/s12/; so was taking the buckets in address
+// order from a ticket counter, 2 %: s19/.)
 template <uint32_t CAP, int D, int T = kBkT>
 __global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD (512 threads x 2 per CU spill: 87 VGPRs)
 k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
