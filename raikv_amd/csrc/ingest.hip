@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <type_traits>
 #include "kvh_internal.hpp"
+#include "tickets.hpp"
 #include "../../include/kvh.h"
 
 using namespace kvh;
@@ -649,11 +650,15 @@ __device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, co
   }
 }
 
-template <int NT, int NH, int PD = 2>
+// Q: chunks in address order through wave tickets (tickets.hpp; n < 2^32 - 1,
+// the queues then hold span indices themselves)
+template <int NT, int NH, int PD = 2, bool Q = false>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
-        const uint64_t* __restrict__ dcount = nullptr) {  // dcount: n = min(n, *dcount), read on the device
+        const uint64_t* __restrict__ dcount = nullptr,  // dcount: n = min(n, *dcount), read on the device
+        unsigned long long* __restrict__ tk = nullptr) {
+  static_assert(!Q || PD == 2, "the ticket form keeps two chunk bases");
   constexpr int NW = 1024 / 64;
   constexpr uint32_t CH = 64 * NH;  // spans per wave per iteration
   // medium spans stack up from 0, longer ones down from QCAP - 1; each holds
@@ -673,22 +678,30 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   __syncthreads();
   const LdsTab<NT> T(lds);
   for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) kfull[l] = make_const(s1, s2, l, T);
-  __syncthreads();
+  __shared__ WaveTickets WT;
+  if constexpr (Q) wt_init(WT, tk);  // ends with a barrier
+  else __syncthreads();
   if (dcount) {  // no barrier follows
     const uint64_t dn = *dcount;
     n = dn < n ? dn : n;
   }
-  if (n == 0) return;
+  if (n == 0) {  // grid-uniform
+    if constexpr (Q) wt_done(tk);
+    return;
+  }
   const bool fix = (flags & KVH_FIXUP) != 0;
   const uint32_t nul = (flags & KVH_NULTERM) ? 1u : 0u;
   const uint32_t lane = threadIdx.x & 63;
   uint32_t* q = queue[threadIdx.x >> 6];
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint64_t step = (uint64_t)gridDim.x * NW * CH;  // spans per grid iteration
+  // spans per grid iteration (static order); Q: the queues hold span indices
+  // (CH_Q = ~0: j = e / CH_Q * step + e % CH_Q = e)
+  const uint64_t step = (uint64_t)gridDim.x * NW * CH;
+  const uint32_t CHq = Q ? 0xffffffffu : CH;
   // The long-span queue is a stack: entry e = CH * (iteration) + 64 * half + lane
   // -> span wave*CH + (e / CH) * step + e % CH; full sets of 64 pop off the top.
   uint32_t qn = 0, ql = 0;  // wave-uniform: medium (16..31 hashed bytes) and long queue depths
-  const uint64_t qbase = wave * CH;
+  const uint64_t qbase = Q ? 0 : wave * CH;
   auto is_short = [nul](uint32_t D) { return D + nul - 1u < 15u; };
   // Pipeline, unrolled by PD so that no register is renamed while its load
   // is in flight: iteration c issues the offsets/lengths of chunk c+PD and the
@@ -699,7 +712,16 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   uint64_t mo[PD][NH];
   uint32_t mD[PD][NH];
   ShortRaw tr[2][NH];
-  const uint64_t b0 = qbase;
+  // Q: cb[u] = base of the chunk whose offsets sit in slot u
+  uint64_t cb[PD];
+  if constexpr (Q) {
+#pragma unroll
+    for (int d = 0; d < PD; d++) cb[d] = wt_next(WT, tk, NW) * CH;
+  } else {
+#pragma unroll
+    for (int d = 0; d < PD; d++) cb[d] = qbase + d * step;
+  }
+  const uint64_t b0 = cb[0];
 #pragma unroll
   for (int h = 0; h < NH; h++) {
     const uint64_t j0 = std::min<uint64_t>(b0 + 64 * h + lane, n - 1);
@@ -707,7 +729,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
     const uint32_t D0 = lens[j0];
 #pragma unroll
     for (int d = 1; d < PD; d++) {
-      const uint64_t jd = std::min<uint64_t>(b0 + d * step + 64 * h + lane, n - 1);
+      const uint64_t jd = std::min<uint64_t>(cb[d] + 64 * h + lane, n - 1);
       mo[d][h] = __builtin_nontemporal_load(offs + jd);  // read once: streaming
       mD[d][h] = __builtin_nontemporal_load(lens + jd);
     }
@@ -718,16 +740,18 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   auto body = [&](uint64_t b, auto uc) {
     constexpr int u = decltype(uc)::value;  // offset slot, a compile-time constant
     constexpr int un = (u + 1) % PD, x = u & 1;  // next chunk's offset slot; this chunk's text slot
+    const uint64_t bn = Q ? cb[un] : b + step;  // the next chunk
+    cb[u] = Q ? wt_next(WT, tk, NW) * CH : b + PD * step;  // the chunk PD on
 #pragma unroll
-    for (int h = 0; h < NH; h++) {  // offsets of chunk b + PD step into slot u (chunk b's, consumed)
-      const uint64_t jj = std::min<uint64_t>(b + PD * step + 64 * h + lane, n - 1);
+    for (int h = 0; h < NH; h++) {  // offsets of chunk cb[u] into slot u (chunk b's, consumed)
+      const uint64_t jj = std::min<uint64_t>(cb[u] + 64 * h + lane, n - 1);
       mo[u][h] = __builtin_nontemporal_load(offs + jj);
       mD[u][h] = __builtin_nontemporal_load(lens + jj);
     }
 #pragma unroll
-    for (int h = 0; h < NH; h++) {  // text of chunk b + step
+    for (int h = 0; h < NH; h++) {  // text of the next chunk
       const uint32_t D1 = mD[un][h];
-      tr[x ^ 1][h] = short_issue(buf + mo[un][h], D1, b + step + 64 * h + lane < n && D1 && is_short(D1));
+      tr[x ^ 1][h] = short_issue(buf + mo[un][h], D1, bn + 64 * h + lane < n && D1 && is_short(D1));
       tr[x ^ 1][h].D = D1;
     }
     bool valid[NH], shrt[NH];
@@ -762,7 +786,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
       const uint32_t H = tr[x][h].D + nul;
       const bool med = valid[h] && !shrt[h] && H - 16u < 16u, lng = valid[h] && !shrt[h] && !med;
       const uint64_t mm = __ballot(med), lm = __ballot(lng);
-      const uint32_t e = CH * it + 64 * h + lane;
+      const uint32_t e = Q ? (uint32_t)(b + 64 * h + lane) : CH * it + 64 * h + lane;
       if (mm) {
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
         if (med) q[qn + below] = e;
@@ -777,33 +801,45 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
     if (qn >= 64 || ql >= 64) {
       wave_lds_sync();
       while (qn >= 64) {
-        spans_medium<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CH, nul, fix, kfull, psel, T);
+        spans_medium<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CHq, nul, fix, kfull, psel, T);
         qn -= 64;
       }
       while (ql >= 64) {  // its newest 64 entries: q[QCAP - ql .. QCAP - ql + 64)
-        spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, 64, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
+        spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, 64, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T);
         ql -= 64;
       }
       wave_lds_sync();
     }
     it++;
   };
-  for (uint64_t b = b0; b < n; b += PD * step) {  // wave-uniform trip count
-    body(b, std::integral_constant<int, 0>{});
-    if (b + step >= n) break;
-    body(b + step, std::integral_constant<int, 1>{});
-    if constexpr (PD >= 4) {
-      if (b + 2 * step >= n) break;
-      body(b + 2 * step, std::integral_constant<int, 2 % PD>{});
-      if (b + 3 * step >= n) break;
-      body(b + 3 * step, std::integral_constant<int, 3 % PD>{});
+  if constexpr (Q) {  // a wave's tickets only grow: past the end once, past it for good
+    if (b0 < n) {
+      for (;;) {
+        body(cb[0], std::integral_constant<int, 0>{});
+        if (cb[1] >= n) break;
+        body(cb[1], std::integral_constant<int, 1>{});
+        if (cb[0] >= n) break;
+      }
+    }
+  } else {
+    for (uint64_t b = b0; b < n; b += PD * step) {  // wave-uniform trip count
+      body(b, std::integral_constant<int, 0>{});
+      if (b + step >= n) break;
+      body(b + step, std::integral_constant<int, 1>{});
+      if constexpr (PD >= 4) {
+        if (b + 2 * step >= n) break;
+        body(b + 2 * step, std::integral_constant<int, 2 % PD>{});
+        if (b + 3 * step >= n) break;
+        body(b + 3 * step, std::integral_constant<int, 3 % PD>{});
+      }
     }
   }
   if (qn || ql) {
     wave_lds_sync();
-    if (qn) spans_medium<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CH, nul, fix, kfull, psel, T);
-    if (ql) spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, ql, lane, qbase, step, CH, nul, fix, kfull, s1, s2, T);
+    if (qn) spans_medium<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CHq, nul, fix, kfull, psel, T);
+    if (ql) spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, ql, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T);
   }
+  if constexpr (Q) wt_done(tk);
 }
 
 
@@ -902,6 +938,25 @@ uint64_t tok_chunks(const void* text, size_t nbytes) {
 
 }  // namespace
 
+namespace {
+// k_spans<4, 2>, its chunks in address order through wave tickets unless
+// knob 24 = 1 (or the spans overflow the queues' u32 span indices)
+int launch_spans(const void* buf, const uint64_t* offs, const uint32_t* lens, uint64_t n, uint64_t seed1,
+                 uint64_t seed2, uint64_t* out, uint32_t flags, const uint64_t* dcount, uint32_t grid,
+                 hipStream_t st) {
+  if (knob(g_tune_order) != 1 && n < 0xffffffffull) {
+    unsigned long long* tk = nullptr;
+    if (int rc = stream_tickets(st, &tk)) return rc;
+    hipLaunchKernelGGL((k_spans<4, 2, 2, true>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens, n,
+                       seed1, seed2, out, flags, dcount, tk);
+  } else {
+    hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens, n, seed1,
+                       seed2, out, flags, dcount, nullptr);
+  }
+  return launch_done();
+}
+}  // namespace
+
 extern "C" {
 
 size_t kvh_tokenize_scratch_bytes(size_t nbytes) {
@@ -963,9 +1018,8 @@ int kvh_tokenize_hash(const void* text, size_t nbytes, uint32_t max_token, uint6
   if (rc) return rc;
   // the span hash takes its count from the device: no host round trip
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((cap + 1023) / 1024, (uint64_t)cus));
-  hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)text,
-                     tok_offs, tok_lens, (uint64_t)cap, seed1, seed2, out, flags, (const uint64_t*)count);
-  return launch_done();
+  return launch_spans(text, tok_offs, tok_lens, cap, seed1, seed2, out, flags, (const uint64_t*)count, grid,
+                      (hipStream_t)stream);
 }
 
 size_t kvh_frag_offsets_scratch_bytes(size_t nbytes) {
@@ -1041,8 +1095,7 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
   const int sk = g_tune_spans.load(std::memory_order_relaxed);
   if (sk == 2)
-    hipLaunchKernelGGL((k_spans<4, 2>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
-                       lens, (uint64_t)n, seed1, seed2, out, flags);
+    return launch_spans(buf, offs, lens, n, seed1, seed2, out, flags, nullptr, grid, (hipStream_t)stream);
   else if (sk == 1)
     hipLaunchKernelGGL((k_spans<4, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
                        lens, (uint64_t)n, seed1, seed2, out, flags);

@@ -140,9 +140,9 @@ def _tickets_cases(kvh, rng):
 def test_order_knob_every_streaming_kernel(kvh, n):
     """Every kernel that takes its chunks through wave tickets by default
     (runtime-length k_fixed_rt, k_fixed_lanes (C3), the fused hash+positions
-    kernel, CRC32C of fixed and of variable-length keys) equals its
-    static-order form (knob 24 = 1) on the same input, twice in a row (the
-    counter reset)."""
+    kernel, CRC32C of fixed and of variable-length keys, the span hash alone
+    and behind the tokenizer) equals its static-order form (knob 24 = 1) on
+    the same input, twice in a row (the counter reset)."""
     from raikv_amd.workload import C3_SEEDS
     rng = np.random.default_rng(n)
     geom = kvh.HtGeom.from_map(map_size=1 << 30, hash_entry_size=64, hash_value_ratio=1.0, cuckoo_buckets=4,
@@ -154,6 +154,9 @@ def test_order_knob_every_streaming_kernel(kvh, n):
     lens = rng.integers(0, 300, n).astype(np.uint64)
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
     kv, dof = dev(rng.integers(0, 256, int(offs[-1]) + 1, dtype=np.uint8)), dev(offs.view(np.int64))
+    dlen = dev(np.minimum(lens, 40).astype(np.int32))  # spans of 0-40 bytes at the var keys' offsets
+    tb = rng.choice(np.frombuffer(b"abcdefgh \n\t", dtype=np.uint8), size=max(16, n * 4))
+    text = dev(tb)
     runs = {
         "rt20": lambda: kvh.meow128_fixed(k20, 20, STATIC),
         "rt50": lambda: kvh.meow128_fixed(k50, 50, STATIC),
@@ -162,6 +165,9 @@ def test_order_knob_every_streaming_kernel(kvh, n):
                                     kvh.meow128_fixed_positions(k16, 16, STATIC, geom)], 1),
         "crc16": lambda: kvh.crc_c_fixed(k16, 16, 7),
         "crc_var": lambda: kvh.crc_c_var(kv, dof, 7),
+        # spans with a long / medium / short mix (k_spans' three paths and queues)
+        "spans": lambda: kvh.meow128_spans(kv, dof[:-1], dlen, STATIC),
+        "tokenize_hash": lambda: kvh.tokenize_hash(text, STATIC)[2],
     }
     for name, run in runs.items():
         prev = kvh.lib.kvh_set_tuning(24, 1)

@@ -21,7 +21,7 @@ for kv in filter(None, os.environ.get("KNOBS", "").split(",")):  # e.g. KNOBS=3=
 shapes = [(16, 100_000_000), (32, 125_000_000), (64, 100_000_000), (8, 100_000_000), (24, 100_000_000),
           (40, 100_000_000), (48, 100_000_000), (56, 100_000_000), ("c3", 50_000_000), ("f1", 100_000_000),
           ("f1p", 100_000_000), ("f4", 100_000_000), (20, 100_000_000), (33, 100_000_000), (50, 100_000_000),
-          ("f4v", 100_000_000)]
+          ("f4v", 100_000_000), ("f3", 1 << 30)]
 if len(sys.argv) > 1:  # a comma list of shape names; any other key length runs 100M keys of it
     known = {str(s[0]): s for s in shapes}
     shapes = [known[t] if t in known else (int(t), 100_000_000) for t in sys.argv[1].split(",")]
@@ -52,6 +52,13 @@ for L, n in shapes:
         else:
             kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=hashes, fixup=True)
             hash_ = lambda: kvh.ht_positions(hashes, geom, out=out)
+    elif tag == "f3":  # 1 GiB text -> tokens -> NUL-terminated span hashes (one kvh_tokenize_hash call)
+        del keys
+        r = torch.randint(0, 8, (n,), dtype=torch.uint8, device="cuda", generator=g)
+        keys = torch.where(r == 0, 32, torch.where(r == 1, 10, 97 + r)).to(torch.uint8)
+        del r
+        out = None  # the call allocates; its hashes are what the A/B compares
+        hash_ = lambda: kvh.tokenize_hash(keys, kvh.STATIC_SEED)[2]
     elif tag == "f4v":
         from raikv_amd.workload import zipf_lengths, offsets_from_lengths  # noqa: E402
         offs_np = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=3))
@@ -68,12 +75,13 @@ for L, n in shapes:
     ref = None
     for v in VS:
         kvh.lib.kvh_set_tuning(KN, v)
-        hash_()
+        got = hash_()
+        got = out if out is not None else got
         torch.cuda.synchronize()
         if ref is None:
-            ref = out.clone()
+            ref = got.clone()
         else:
-            assert torch.equal(ref, out), f"order {v} differs at L={L}"
+            assert torch.equal(ref, got), f"order {v} differs at L={L}"
     del ref
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:
