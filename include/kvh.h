@@ -457,11 +457,14 @@ int         kvh_device_synchronize(void);
  *   0 = tables per LDS (0 per-length default, 2 or 4),
  *   1 = workgroups per CU multiplier (1-8), 2 = force the generic kernel (0/1),
  *   3 = keys per lane per step in the fixed-length kernel (0 default, 1, 2, 4, 8),
- *   7 = variable-length kernel (23 default: per-wave windows sorted by 16-byte
- *       length class, keys read as dwordx4 groups, one straight-line variant
- *       per chunk shape, 16 waves; 24 / 25 the same at 12 waves, 25 with the
- *       next block's groups in flight; 13 the round-2 sorted-window kernel;
- *       7 sorted by exact length; 0 lane per key in input order),
+ *   7 = variable-length kernel (46 default: per-wave windows sorted by
+ *       16-byte length class, keys read as dwordx4 groups, one straight-line
+ *       variant per chunk shape, 16 waves, windows taken in address order
+ *       through wave tickets; 23 the same with a static window order; 24 / 25
+ *       23 at 12 waves, 25 with the next block's groups in flight; 44 / 47
+ *       23 / 46 with four tables at 16 copies; 45 23 with clamped group loads;
+ *       48 46 at 12 waves; 13 the round-2 sorted-window kernel; 7 sorted by
+ *       exact length; 0 lane per key in input order),
  *   8 = multi-seed kernel (1 lanes per key, 0 one lane per key),
  *  14 = variable-length CRC32C kernel (6 default: length-sorted windows, 16
  *       waves on 16-copy tables, keys read as dwordx4 groups, the next key's
@@ -479,6 +482,13 @@ int         kvh_device_synchronize(void);
  *       take the zero-copy tiny path (default 16384; 0 off),
  *  22 = ht_sort bucket sort (0 two workgroups per CU when the buckets are
  *       small enough; 1 always one per CU),
+ *  23 = ht_sort two-pass bucket sort (1 default: records read once into
+ *       registers, k_bk_sortr; 0 k_bk_sort; 2 k_bk_sortr2),
+ *  24 = chunk order of the streaming kernels (0 default: every fixed-length,
+ *       runtime-length, multi-seed, fused-positions, CRC32C and span kernel
+ *       takes its chunks in address order through per-stream wave tickets;
+ *       1 the static per-wave order everywhere; 2 wave tickets, 3 / 4 / 5
+ *       workgroup tickets of 1 / 4 / 16 rounds for the fixed-length kernel),
  *   3 also takes 3 for the 40-64-byte fixed-length kernels.
  * Returns the previous value or KVH_EINVAL.  (Research kernels and ablation
  * builds whose outputs are not hashes exist only in the experiments build,
