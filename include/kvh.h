@@ -482,8 +482,11 @@ int         kvh_device_synchronize(void);
  *       take the zero-copy tiny path (default 16384; 0 off),
  *  22 = ht_sort bucket sort (0 two workgroups per CU when the buckets are
  *       small enough; 1 always one per CU),
- *  23 = ht_sort two-pass bucket sort (1 default: records read once into
- *       registers, k_bk_sortr; 0 k_bk_sort; 2 k_bk_sortr2),
+ *  23 = ht_sort two-pass bucket sort (3 default: buckets of <= 3K records,
+ *       up to 15 bucket bits with an 8-bit second pass, each bucket's
+ *       records read once into registers by one of two 512-thread
+ *       workgroups per CU; 1 the same at 6K-record buckets and one
+ *       1024-thread workgroup per CU; 0 k_bk_sort; 2 k_bk_sortr2),
  *  24 = chunk order of the streaming kernels (0 default: every fixed-length,
  *       runtime-length, multi-seed, fused-positions, CRC32C and span kernel
  *       takes its chunks in address order through per-stream wave tickets;

@@ -1184,30 +1184,38 @@ constexpr int kTwT = 512;                      // threads per workgroup
 constexpr int kTwW = kTwT / 64;                // waves
 constexpr int kTwPer = (int)(kTwTile / kTwT);  // elements per thread
 constexpr int kTwD = 128;                      // digit values (<= 7 bits)
+constexpr int kTwD8 = 256;                     // pass 2 of the 15-bit split (knob 23 = 3): 8 bits
+constexpr int kTwMaxB = 15;                    // bucket bits of the two-pass path
 
-struct TwShared {
-  R24 stage[kTwTile];                  // the tile in digit order
-  uint16_t cnt[kTwPer][kTwW][kTwD];    // per (round, wave, digit) counts -> offsets in the digit
-  uint16_t bkt[kTwTile];               // the full bucket id of each staged record
-  uint8_t dig[kTwTile];                // its digit
-  uint32_t lstart[kTwD], gofs[kTwD], wtot[2];
+template <uint32_t ND>
+struct TwSh {
+  R24 stage[kTwTile];                // the tile in digit order
+  uint16_t cnt[kTwPer][kTwW][ND];    // per (round, wave, digit) counts -> offsets in the digit
+  uint16_t bkt[kTwTile];             // the full bucket id of each staged record
+  uint8_t dig[kTwTile];              // its digit
+  uint32_t lstart[ND], gofs[ND], wtot[ND / 64];
 };
+using TwShared = TwSh<kTwD>;
 
 // Stable rank of the tile's elements by digit (element k*kTwT + tid holds
 // dg[k], valid v[k]): pos[k] = its position in the digit-sorted tile;
-// S.lstart[d] = digit d's first position.  Ends with a barrier.
-__device__ __forceinline__ void tw_rank(const uint32_t (&dg)[kTwPer], const bool (&v)[kTwPer], TwShared& S,
+// S.lstart[d] = digit d's first position.  Ends with a barrier.  ND = 128
+// or 256 digit values.
+template <uint32_t ND = kTwD>
+__device__ __forceinline__ void tw_rank(const uint32_t (&dg)[kTwPer], const bool (&v)[kTwPer], TwSh<ND>& S,
                                         uint32_t (&pos)[kTwPer]) {
+  constexpr int DB = ND == 256 ? 8 : 7;
+  static_assert(ND == 128 || ND == 256, "digit values");
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint16_t* c = &S.cnt[0][0][0];
-  for (uint32_t i = tid; i < (uint32_t)(kTwPer * kTwW * kTwD); i += kTwT) c[i] = 0;
+  for (uint32_t i = tid; i < (uint32_t)(kTwPer * kTwW * ND); i += kTwT) c[i] = 0;
   __syncthreads();
   uint32_t below[kTwPer];
 #pragma unroll
   for (int k = 0; k < kTwPer; k++) {
     uint64_t eq = __ballot(v[k]);
 #pragma unroll
-    for (int bit = 0; bit < 7; bit++) {
+    for (int bit = 0; bit < DB; bit++) {
       const uint64_t B = __ballot((dg[k] >> bit) & 1u);
       eq &= ((dg[k] >> bit) & 1u) ? B : ~B;
     }
@@ -1215,7 +1223,7 @@ __device__ __forceinline__ void tw_rank(const uint32_t (&dg)[kTwPer], const bool
     if (v[k] && below[k] == 0) S.cnt[k][w][dg[k]] = (uint16_t)__popcll(eq);
   }
   __syncthreads();
-  if (tid < (uint32_t)kTwD) {  // per digit: running offsets over (round, wave), then the digit starts
+  if (tid < ND) {  // per digit: running offsets over (round, wave), then the digit starts
     uint32_t run = 0;
 #pragma unroll
     for (int k = 0; k < kTwPer; k++)
@@ -1235,7 +1243,11 @@ __device__ __forceinline__ void tw_rank(const uint32_t (&dg)[kTwPer], const bool
     S.lstart[tid] = inc - run;  // within this wave's 64 digits
   }
   __syncthreads();
-  if (tid >= 64 && tid < (uint32_t)kTwD) S.lstart[tid] += S.wtot[0];
+  if (tid >= 64 && tid < ND) {
+    uint32_t add = 0;
+    for (uint32_t q = 0; q < w; q++) add += S.wtot[q];
+    S.lstart[tid] += add;
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kTwPer; k++)
@@ -1343,30 +1355,33 @@ __device__ __forceinline__ bool tw_tile2(uint32_t j, const uint32_t* __restrict_
   return true;
 }
 
+template <uint32_t ND = kTwD>
 __global__ void __launch_bounds__(kTwT)
 k_tw_hist2(const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs, const uint32_t* __restrict__ cnt1,
            const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2, uint32_t* __restrict__ H2) {
-  __shared__ uint32_t hist[kTwD];
+  __shared__ uint32_t hist[ND];
   const uint32_t tid = threadIdx.x, nb2 = 1u << B2;
   uint32_t d1, p0, p1;
   if (!tw_tile2(blockIdx.x, tbs, nb1, cnt1, start1, &d1, &p0, &p1)) return;  // workgroup-uniform
-  if (tid < (uint32_t)kTwD) hist[tid] = 0;
+  if (tid < ND) hist[tid] = 0;
   __syncthreads();
   for (uint32_t p = p0 + tid; p < p1; p += kTwT) atomicAdd(&hist[bA[p] & (nb2 - 1)], 1u);
   __syncthreads();
   if (tid < nb2) H2[(uint64_t)blockIdx.x * nb2 + tid] = hist[tid];
 }
 
-// Exclusive scan, in place, of the columns c < ncols (<= 128) of rows
-// [r0, r1) of a row-major table with `ncols` words per row, by one
-// 1024-thread workgroup: 8 groups of 128 threads, group g scans a
-// contiguous eighth of the rows (the 128 threads of a group read one row's
+// Exclusive scan, in place, of the columns c < ncols (<= NC = 128 or 256)
+// of rows [r0, r1) of a row-major table with `ncols` words per row, by one
+// 1024-thread workgroup: 1024 / NC groups of NC threads, group g scans a
+// contiguous share of the rows (the NC threads of a group read one row's
 // words together: coalesced), group sums combined in LDS.  *total[c] gets
 // the column sum when total != nullptr.
+template <uint32_t NC = kTwD>
 __device__ __forceinline__ void tw_colscan(uint32_t* __restrict__ Tb, uint32_t r0, uint32_t r1, uint32_t ncols,
-                                           uint32_t* __restrict__ total, uint32_t (&part)[8][kTwD]) {
-  const uint32_t c = threadIdx.x & (kTwD - 1), grp = threadIdx.x >> 7;
-  const uint32_t rows = r1 - r0, per = (rows + 7) / 8;
+                                           uint32_t* __restrict__ total, uint32_t (&part)[1024 / NC][NC]) {
+  constexpr uint32_t NG = 1024 / NC;
+  const uint32_t c = threadIdx.x & (NC - 1), grp = threadIdx.x / NC;
+  const uint32_t rows = r1 - r0, per = (rows + NG - 1) / NG;
   const uint32_t a = r0 + min(rows, grp * per), b = r0 + min(rows, (grp + 1) * per);
   uint32_t sum = 0;
   if (c < ncols) {
@@ -1387,7 +1402,7 @@ __device__ __forceinline__ void tw_colscan(uint32_t* __restrict__ Tb, uint32_t r
   if (c < ncols) {
     if (grp == 0 && total) {
       uint32_t t = 0;
-      for (uint32_t g = 0; g < 8; g++) t += part[g][c];
+      for (uint32_t g = 0; g < NG; g++) t += part[g][c];
       total[c] = t;
     }
     uint32_t r = a;
@@ -1415,11 +1430,12 @@ k_tw_scan1(uint32_t* __restrict__ S, uint32_t nch, uint32_t nb1, uint32_t* __res
 
 // pass 2, one workgroup per top digit d1: H2 over d1's tiles -> running
 // offsets within each bucket (d1, d2); cnt[(d1, d2)] = the bucket's size
+template <uint32_t ND = kTwD>
 __global__ void __launch_bounds__(1024)
 k_tw_scan2(uint32_t* __restrict__ H2, const uint32_t* __restrict__ tbs, uint32_t B2, uint32_t* __restrict__ cnt) {
-  __shared__ uint32_t part[8][kTwD];
+  __shared__ uint32_t part[1024 / ND][ND];
   const uint32_t d1 = blockIdx.x;
-  tw_colscan(H2, tbs[d1], tbs[d1 + 1], 1u << B2, cnt + (d1 << B2), part);
+  tw_colscan<ND>(H2, tbs[d1], tbs[d1 + 1], 1u << B2, cnt + (d1 << B2), part);
 }
 
 // start[b] = start1[d1] + the sizes of d1's earlier buckets
@@ -1448,13 +1464,13 @@ k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start
 // from the position without loading (2.17 GB, 0.90 ms: the floor), 4 stores
 // non-temporally (5.06 GB), 6 = 5 with non-temporal loads.  Only 0, 3, 5, 6
 // give the product's output; 1, 2, 4 are attribution probes.
-template <int MODE>
+template <int MODE, uint32_t ND = kTwD>
 __global__ void __launch_bounds__(kTwT)
 k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
               const uint32_t* __restrict__ cnt1, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
               const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, R24* __restrict__ rec,
               R24* __restrict__ dummy) {
-  __shared__ TwShared S;
+  __shared__ TwSh<ND> S;
   const uint32_t tid = threadIdx.x, nb2 = 1u << B2, j = xcd_tile(blockIdx.x, gridDim.x);
   uint32_t d1, p0, p1;
   if (!tw_tile2(j, tbs, nb1, cnt1, start1, &d1, &p0, &p1)) return;  // workgroup-uniform
@@ -1502,7 +1518,7 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
     }
   }
   if (tid < nb2) S.gofs[tid] = start[(d1 << B2) | tid] + H2[(uint64_t)j * nb2 + tid];
-  tw_rank(dg, v, S, pos);
+  tw_rank<ND>(dg, v, S, pos);
   if constexpr (MODE == 5 || MODE == 6) {
 #pragma unroll
     for (int k = 0; k < kTwPer; k++)
@@ -1578,8 +1594,8 @@ int sort_layout(size_t n, SortLayout* L) {
   L->tw_H1 = o; o += al256(4 * ntiles * kTwD);
   L->tw_S1 = o; o += al256(4 * nch * kTwD);
   L->tw_small = o; o += al256(4 * (3 * kTwD + 2));  // cnt1, start1, tbs
-  L->tw_H2 = o; o += al256(4 * (ntiles + kTwD) * kTwD);
-  L->tw_bk = o; o += al256(4 * (3 * (1u << kBkMaxB) + 1));  // cnt, start, ovf, novf
+  L->tw_H2 = o; o += al256(4 * (ntiles + kTwD8) * kTwD8);  // pass-2 counts, up to 8-bit digits
+  L->tw_bk = o; o += al256(4 * (3 * (1u << kTwMaxB) + 1));   // cnt, start, ovf, novf
   L->total = std::max(radix_total, o);
   return 0;
 }
@@ -1639,14 +1655,20 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
     // LDS capacity); larger batches take the radix path below
     const double reach = (double)geom->ht_size / std::ldexp(1.0, (int)std::min<uint32_t>(sb, 64));
     auto mean_of = [&](uint32_t B) { return (double)n / (reach * std::ldexp(1.0, (int)B)); };
+    // knob 23 = 3: half-size buckets (mean <= 3072, up to 15 bits: pass 2 of
+    // 8 bits) for the bucket sort at two 512-thread workgroups per CU
+    const int b3 = g_tune_sort_b3.load(std::memory_order_relaxed);
+    const bool half = b3 == 3 && engine != 2;
     uint32_t B = 0;
-    while (B < (uint32_t)kBkMaxB && mean_of(B) > 6144.0) B++;
+    while (B < (uint32_t)(half ? kTwMaxB : kBkMaxB) && mean_of(B) > (half ? 3072.0 : 6144.0)) B++;
     // buckets then hold ~mean +- sqrt(mean): the two-per-CU bucket sort (capacity
     // 8000) when the mean leaves a wide margin (knob 22 = 1 forces the 12288 one)
-    const bool small_b = mean_of(B) <= 6400.0 && g_tune_sort_cap.load(std::memory_order_relaxed) == 0;
+    const bool small_b = mean_of(B) <= (half ? 3200.0 : 6400.0) && g_tune_sort_cap.load(std::memory_order_relaxed) == 0;
     if (mean_of(B) <= 9000.0 && engine != 2 && B >= 2) {
-      // two passes of <= 7 bits, tile-stable LDS-staged scatters
-      const uint32_t B2 = B / 2, B1 = B - B2, nb1 = 1u << B1, nb = 1u << B;
+      // two passes of <= 7 bits (the 15-bit split: 7 + 8), tile-stable LDS-staged scatters
+      const uint32_t B2 = half ? std::min<uint32_t>(8, B - B / 2) : B / 2, B1 = B - B2, nb1 = 1u << B1,
+                     nb = 1u << B;
+      const bool d8 = B2 == 8;
       const uint32_t ntiles = (uint32_t)((n + kTwTile - 1) / kTwTile);
       const uint32_t nch = (ntiles + kBkChunk - 1) / kBkChunk;
       R24* recA = (R24*)(s + L.tw_recA);
@@ -1680,23 +1702,39 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       hipLaunchKernelGGL(k_tw_tiles, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt1, nb1, tbs);
       if ((rc = launch_done())) return rc;
       const uint32_t ntB = ntiles + nb1;  // an upper bound: the tiles past tbs[nb1] return at once
-      hipLaunchKernelGGL(k_tw_hist2, dim3(ntB), dim3(kTwT), 0, st, (const uint16_t*)bA, (const uint32_t*)tbs,
-                         (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2, H2);
+      if (d8)
+        hipLaunchKernelGGL(k_tw_hist2<kTwD8>, dim3(ntB), dim3(kTwT), 0, st, (const uint16_t*)bA, (const uint32_t*)tbs,
+                           (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2, H2);
+      else
+        hipLaunchKernelGGL(k_tw_hist2<kTwD>, dim3(ntB), dim3(kTwT), 0, st, (const uint16_t*)bA, (const uint32_t*)tbs,
+                           (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2, H2);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_tw_scan2, dim3(nb1), dim3(1024), 0, st, H2, (const uint32_t*)tbs, B2, cnt);
+      if (d8)
+        hipLaunchKernelGGL(k_tw_scan2<kTwD8>, dim3(nb1), dim3(1024), 0, st, H2, (const uint32_t*)tbs, B2, cnt);
+      else
+        hipLaunchKernelGGL(k_tw_scan2<kTwD>, dim3(nb1), dim3(1024), 0, st, H2, (const uint32_t*)tbs, B2, cnt);
       if ((rc = launch_done())) return rc;
       hipLaunchKernelGGL(k_tw_start2, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
                          nb1, B2, start);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_tw_scatter2<3>, dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA, (const uint16_t*)bA,
-                         (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2,
-                         (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
+      if (d8)
+        hipLaunchKernelGGL((k_tw_scatter2<3, kTwD8>), dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA,
+                           (const uint16_t*)bA, (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1,
+                           nb1, B2, (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
+      else
+        hipLaunchKernelGGL((k_tw_scatter2<3, kTwD>), dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA,
+                           (const uint16_t*)bA, (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1,
+                           nb1, B2, (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
       if ((rc = launch_done())) return rc;
-      if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 2)
+      if (small_b && half)  // half-size buckets: two 512-thread workgroups per CU
+        hipLaunchKernelGGL((k_bk_sortr<3584, 11, 512>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(512), 0,
+                           st, (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
+                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      else if (small_b && b3 == 2)
         hipLaunchKernelGGL((k_bk_sortr2<7168, 11>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0,
                            st, (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                            items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
-      else if (small_b && g_tune_sort_b3.load(std::memory_order_relaxed) == 1)
+      else if (small_b && b3 == 1)
         hipLaunchKernelGGL((k_bk_sortr<7168, 12>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                            items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
@@ -1827,7 +1865,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
 
 }  // namespace
 
-namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; std::atomic<int> g_tune_sort_b3{1}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; std::atomic<int> g_tune_sort_b3{3}; } }
 
 extern "C" {
 

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round-4 session 23: half-size buckets (knob 23 = 3: 15 bits, 8-bit second pass, 2 x 512-thread bucket sorts per CU):
+# sort tests, f2 A/B (1 vs 3), kernel trace of the A/B.
+set -o pipefail
+O=${1:-gpurun_out/r4s23}
+cd ${GRAFT_REPO_ROOT:-.}; mkdir -p $O; export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_sort.py > $O/gpu_tests.txt 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/gpu_tests.txt; tail -2 $O/gpu_tests.txt; [ $rc -ne 0 ] && exit $rc
+TUNE_KNOB=23 timeout -k 10 300 python3 tools/tune_sort.py 1,3 > $O/f2_half_ab.jsonl 2> $O/f2_half_ab.log || exit 1
+cat $O/f2_half_ab.jsonl
+TUNE_KNOB=23 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 tools/tune_sort.py 1,3 > $O/trace.log 2>&1 || exit 1
+python3 - $O <<'PY'
+import csv, glob, sys
+rows = []
+for f in glob.glob(sys.argv[1] + "/trace/**/*kernel_trace.csv", recursive=True):
+    rows += list(csv.DictReader(open(f)))
+by = {}
+for r in rows:
+    if "k_bk_sort" in r["Kernel_Name"] or "k_tw_" in r["Kernel_Name"]:
+        by.setdefault(r["Kernel_Name"][:60], []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+for k, v in by.items():
+    print(k, len(v), "avg ms", sum(v) / len(v) / 1e6, "min ms", min(v) / 1e6)
+PY
