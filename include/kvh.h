@@ -463,7 +463,8 @@ int         kvh_device_synchronize(void);
  *       through wave tickets; 23 the same with a static window order; 24 / 25
  *       23 at 12 waves, 25 with the next block's groups in flight; 44 / 47
  *       23 / 46 with four tables at 16 copies; 45 23 with clamped group loads;
- *       48 46 at 12 waves; 13 the round-2 sorted-window kernel; 7 sorted by
+ *       48 46 at 12 waves; 49 / 50 46 / 48 with the next block's groups in
+ *       flight; 13 the round-2 sorted-window kernel; 7 sorted by
  *       exact length; 0 lane per key in input order),
  *   8 = multi-seed kernel (1 lanes per key, 0 one lane per key),
  *  14 = variable-length CRC32C kernel (6 default: length-sorted windows, 16

@@ -1021,7 +1021,7 @@ int kvh_set_tuning(int k, int value) {
     case 2: return set(g_tune_generic, value ? 1 : 0);
     case 3: if (value < 0 || value > 8 || value == 5 || value == 6 || value == 7) return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) && (value < 44 || value > 48) &&
+    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) && (value < 44 || value > 50) &&
                 !(g_exp.var_knob && g_exp.var_knob(value)))
               return KVH_EINVAL;
             return set(g_tune_var, value);

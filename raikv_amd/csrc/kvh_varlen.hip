@@ -454,11 +454,19 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       return launch_done();
     }
     case 47:    // round-4 A/B: 46 with four tables at 16 copies (LdsTab<5>)
-    case 48: {  // round-4 A/B: 46 with 12 waves per workgroup
+    case 48:    // round-4 A/B: 46 with 12 waves per workgroup
+    case 49:    // round-4 A/B: 46 with the next block's groups in flight
+    case 50: {  // round-4 A/B: 25 (12 waves, next block's groups in flight) in address order
       unsigned long long* tk = nullptr;
       if (int rc = stream_tickets(st, &tk)) return rc;
       if (var == 47)
         hipLaunchKernelGGL((k_var9<5, 16, 256, false, true, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
+                           (uint64_t)n, seed1, seed2, out, flags, tk);
+      else if (var == 49)
+        hipLaunchKernelGGL((k_var9<2, 16, 256, true, true, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
+                           (uint64_t)n, seed1, seed2, out, flags, tk);
+      else if (var == 50)
+        hipLaunchKernelGGL((k_var9<2, 12, 192, true, true, false, true>), dim3(grid), dim3(768), 0, st, kp, offsets,
                            (uint64_t)n, seed1, seed2, out, flags, tk);
       else
         hipLaunchKernelGGL((k_var9<2, 12, 192, false, true, false, true>), dim3(grid), dim3(768), 0, st, kp, offsets,

@@ -431,7 +431,7 @@ def test_cpp_hash_test_program(kvh):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("variant", [0, 7, 13, 23, 24, 25, 44, 45, 46, 47, 48])
+@pytest.mark.parametrize("variant", [0, 7, 13, 23, 24, 25, 44, 45, 46, 47, 48, 49, 50])
 def test_var_kernel_variants_vs_oracle(kvh, variant):
     """The variable-length kernels (kvh_set_tuning(7, v): 0 unsorted, 7
     length-sorted windows, 13 windows sorted by 16-byte length class) against
