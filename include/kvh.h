@@ -488,6 +488,8 @@ int         kvh_device_synchronize(void);
  *       records read once into registers by one of two 512-thread
  *       workgroups per CU; 1 the same at 6K-record buckets and one
  *       1024-thread workgroup per CU; 0 k_bk_sort; 2 k_bk_sortr2),
+ *  25 = counting-sort bits of the knob-23 = 3 bucket sort (0 default = 11,
+ *       10, 12),
  *  24 = chunk order of the streaming kernels (0 default: every fixed-length,
  *       runtime-length, multi-seed, fused-positions, CRC32C and span kernel
  *       takes its chunks in address order through per-stream wave tickets;

@@ -1726,10 +1726,16 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
                            (const uint16_t*)bA, (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1,
                            nb1, B2, (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
       if ((rc = launch_done())) return rc;
-      if (small_b && half)  // half-size buckets: two 512-thread workgroups per CU
-        hipLaunchKernelGGL((k_bk_sortr<3584, 11, 512>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(512), 0,
-                           st, (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
-                           items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+      if (small_b && half) {  // half-size buckets: two 512-thread workgroups per CU
+        const uint32_t hg = std::min<uint32_t>(nb, 2u * (uint32_t)cus);
+        const int hd = g_tune_sort_hd.load(std::memory_order_relaxed);  // knob 25: counting-sort bits
+#define KVH_BKH(Dv)                                                                                                \
+  hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512>), dim3(hg), dim3(512), 0, st, (const R24*)recB, (const uint32_t*)cnt, \
+                     (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,                        \
+                     (unsigned long long*)dup_count, novf, ovf)
+        if (hd == 10) KVH_BKH(10); else if (hd == 12) KVH_BKH(12); else KVH_BKH(11);
+#undef KVH_BKH
+      }
       else if (small_b && b3 == 2)
         hipLaunchKernelGGL((k_bk_sortr2<7168, 11>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0,
                            st, (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
@@ -1865,7 +1871,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
 
 }  // namespace
 
-namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; std::atomic<int> g_tune_sort_b3{3}; } }
+namespace kvh { namespace rt { std::atomic<int> g_tune_sort_bits{0}; std::atomic<int> g_tune_sort_engine{0}; std::atomic<int> g_tune_sort_cap{0}; std::atomic<int> g_tune_sort_b3{3}; std::atomic<int> g_tune_sort_hd{0}; } }
 
 extern "C" {
 

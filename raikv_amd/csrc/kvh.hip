@@ -1037,6 +1037,7 @@ int kvh_set_tuning(int k, int value) {
     case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_cap, value);
     case 23: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_sort_b3, value);
     case 24: if (value < 0 || value > 5) return KVH_EINVAL; return set(g_tune_order, value);
+    case 25: if (value != 0 && value != 10 && value != 11 && value != 12) return KVH_EINVAL; return set(g_tune_sort_hd, value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }
