@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 session 26: f1 (fused hash + positions) tables x keys per lane under wave tickets
-# (interleaved rounds, outputs asserted equal within each run).
+# (interleaved rounds, outputs asserted equal within each run).  Ran against a temporary
+# knob 0 / 3 path in launch_fused (ht_pos.hip), removed after it measured no gain.
 set -o pipefail
 O=${1:-gpurun_out/r4s26}
 cd ${GRAFT_REPO_ROOT:-.}; mkdir -p $O; export TMPDIR=/tmp
