@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-4 session 12: k_bk_sortr with the next bucket prefetched (knob 23 = 3):
 # sort tests, f2 A/B (1 vs 3), kernel trace of the A/B.
+# (Knob 23 = 3 named that temporary variant then; it was removed after the A/B, and 23 = 3 now
+# selects the half-size buckets of session 23.)
 set -o pipefail
 O=${1:-gpurun_out/r4s12}
 cd ${GRAFT_REPO_ROOT:-.}; mkdir -p $O; export TMPDIR=/tmp

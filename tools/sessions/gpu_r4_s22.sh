@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 session 22: tokenizer chunk per wave 16 / 32 / 64 KiB (knob 19 = 1 / 2 / 3):
 # ingest tests, f3 A/B under a kernel trace.
+# (Ran against a temporary knob 19 = 2 / 3 path, removed after the A/B.)
 set -o pipefail
 O=${1:-gpurun_out/r4s22}
 cd ${GRAFT_REPO_ROOT:-.}; mkdir -p $O; export TMPDIR=/tmp
