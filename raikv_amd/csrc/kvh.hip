@@ -181,6 +181,12 @@ int stream_tickets(hipStream_t st, unsigned long long** tk) {
     if (sp.first == st) { *tk = sp.second; return 0; }
   constexpr size_t kPairs = 256;
   if (P.used == P.chunks.size() * kPairs) {
+    // a new chunk needs hipMalloc + hipMemset, which a stream being captured
+    // into a graph cannot take: make one call on the stream before capturing
+    // 
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return set_err(KVH_EINVAL);
     unsigned long long* c = nullptr;
     if ((e = hipMalloc((void**)&c, kPairs * 2 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
     if ((e = hipMemset(c, 0, kPairs * 2 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
