@@ -13,7 +13,9 @@ HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/
             raikv_amd/csrc/bs_meow.hpp raikv_amd/csrc/kvh_var.hpp raikv_amd/csrc/tickets.hpp include/kvh.h include/raikv_amd/key_hash.hpp
 
 CPP_TESTS := tests/cpp/hash_test_gpu tests/cpp/bs_host_test tests/cpp/e2e_host tests/cpp/host_latency tests/cpp/paths_gpu \
-             tools/copy_peak tools/fetch_calib tools/scatter2_probe tools/stream_forms tools/scatter2_real
+             tests/cpp/kv_compat_crc tests/cpp/streams_gpu \
+             tools/copy_peak tools/fetch_calib tools/scatter2_probe tools/stream_forms tools/scatter2_real \
+             tools/pin_reuse_probe
 
 KV_LIB   := raikv_amd/libkvh_kv.so
 
@@ -37,14 +39,33 @@ $(KV_LIB): raikv_amd/csrc/kv_compat.cpp raikv_amd/csrc/kv_compat.map include/kvh
 # kvh_set_tuning values (raikv_amd/csrc/kvh_internal.hpp: rt::g_exp).  Used by
 # tools/*.py through KVH_LIB=tools/libkvh_exp.so; never loaded by the tests
 # of the product path.
+# The product sources are compiled again with -DKVH_EXPERIMENTS, which keeps
+# the variants that lost their A/B (knob 7 = 7, 13, 24, 25, 44, 45, 47-50;
+# knob 14 = 1-5; knob 23 = 1, 2; knob 24 = 3-5) selectable there.
 EXP_LIB  := tools/libkvh_exp.so
 EXP_SRCS := tools/exp/kvh_exp.hip
 EXP_OBJS := $(EXP_SRCS:.hip=.o)
+EXP_POBJS := $(patsubst raikv_amd/csrc/%.hip,tools/exp/obj/%.o,$(SRCS))
 tools/exp/%.o: tools/exp/%.hip tools/exp/meow_exp.hpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) $(INC) -c -o $@ $<
-$(EXP_LIB): $(OBJS) $(EXP_OBJS) raikv_amd/csrc/kvh.map
-	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(OBJS) $(EXP_OBJS)
+tools/exp/obj/%.o: raikv_amd/csrc/%.hip $(HDRS)
+	@mkdir -p tools/exp/obj
+	$(HIPCC) $(HIPFLAGS) -DKVH_EXPERIMENTS $(INC) -c -o $@ $<
+$(EXP_LIB): $(EXP_POBJS) $(EXP_OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(EXP_POBJS) $(EXP_OBJS)
 experiments: $(EXP_LIB)
+
+# PROBE (not the product): the product sources with the round-4 unordered
+# ticket fetches (tickets.hpp, KVH_TICKETS_UNORDERED), to show once that the
+# poisoned-output test catches the chunks they drop
+UNO_LIB  := tools/libkvh_unordered.so
+UNO_OBJS := $(patsubst raikv_amd/csrc/%.hip,tools/uno/%.o,$(SRCS))
+tools/uno/%.o: raikv_amd/csrc/%.hip $(HDRS)
+	@mkdir -p tools/uno
+	$(HIPCC) $(HIPFLAGS) -DKVH_TICKETS_UNORDERED $(INC) -c -o $@ $<
+$(UNO_LIB): $(UNO_OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(UNO_OBJS)
+unordered: $(UNO_LIB)
 
 oracle:
 	$(MAKE) -C oracle
@@ -68,12 +89,30 @@ tests/cpp/e2e_host: tests/cpp/e2e_host.cpp $(LIB) include/kvh.h
 	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
 
+# a C program linking only libkvh_kv.so: the CRC32C symbols of key_hash.h:8-20
+tests/cpp/kv_compat_crc: tests/cpp/kv_compat_crc.c $(KV_LIB) include/kvh_kv.h
+	gcc -O2 -std=c11 $(INC) -o $@ $< -L raikv_amd -lkvh_kv -Wl,-rpath,'$$ORIGIN/../../raikv_amd'
+
+# ticket state per stream: hipStreamPerThread from several host threads, and
+# launches captured into a graph and replayed on other streams
+tests/cpp/streams_gpu: tests/cpp/streams_gpu.cpp $(LIB) include/kvh.h oracle
+	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L raikv_amd -lkvh -L oracle -loracle -L/opt/rocm/lib -lamdhip64 -lpthread \
+	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,'$$ORIGIN/../../oracle' -Wl,-rpath,/opt/rocm/lib
+
 # per-call latency of the host pipelines at raikv's batch sizes, beside the
 # reference CPU path (dlopen'ed from oracle/_ref at run time, test-only)
 tests/cpp/host_latency: tests/cpp/host_latency.cpp $(LIB) include/kvh.h
 	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
 	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 -ldl \
 	    -Wl,-rpath,'$$ORIGIN/../../raikv_amd' -Wl,-rpath,/opt/rocm/lib
+
+# probe: host range registered, unregistered, unmapped and mapped again at the
+# same address, then a pageable H2D copy
+tools/pin_reuse_probe: tools/pin_reuse_probe.cpp $(LIB) include/kvh.h
+	g++ -O2 -std=c++17 $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L raikv_amd -lkvh -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../raikv_amd' -Wl,-rpath,/opt/rocm/lib
 
 # measurement: the box's achievable streaming rate for bench.py's roofline
 tools/copy_peak: tools/copy_peak.hip
@@ -92,10 +131,10 @@ tests/cpp/bs_host_test: tests/cpp/bs_host_test.cpp raikv_amd/csrc/bs_aes.hpp rai
 	g++ -O2 -std=c++17 -o $@ $< -Loracle -loracle -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 clean:
-	rm -f $(LIB) $(KV_LIB) $(OBJS) $(CPP_TESTS) $(EXP_LIB) $(EXP_OBJS)
+	rm -f $(LIB) $(KV_LIB) $(OBJS) $(CPP_TESTS) $(EXP_LIB) $(EXP_OBJS) $(EXP_POBJS) $(UNO_LIB) $(UNO_OBJS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle cpptests clean experiments
+.PHONY: all oracle cpptests clean experiments unordered
 
 # f2: the real k_tw_scatter2 under ablations: ht_sort.hip
 # compiled into the probe, the product's other objects linked

@@ -635,6 +635,15 @@ def main():
         par = timed_parity(args.config, cfg, seed, T, args.parity_keys, rank) if args.parity_keys > 0 else None
     except Exception as e:  # reported, never hidden: a failed check is not a pass
         par = {"checked": 0, "mismatches": None, "error": repr(e)[:300]}
+    # every output word of the path, on the device: the timed output equals a
+    # relaunch into poisoned buffers, in the default chunk order and in the
+    # static one (a skipped chunk would keep the previous
+    # launch's correct values and pass the sample above)
+    if par is not None:
+        try:
+            par["full_compare"] = full_compare(kvh, cfg, T, run, out)
+        except Exception as e:  # reported, never hidden
+            par["full_compare"] = {"ok": False, "error": repr(e)[:300]}
     del T
     per_rank = kdist.gather({"rank": rank, "kernel_ms": kern_ms, "keys": n, "parity": par}, world)
 
@@ -682,6 +691,8 @@ def main():
                                         else sum(p["mismatches"] for p in pr)),
                          "against": pr[0].get("against", pr[0].get("error")),
                          "sample": f"{args.parity_keys} random keys + first + last of each rank's timed output",
+                         "full_compare": all((p.get("full_compare") or {}).get("ok") is True for p in pr),
+                         "full_compare_detail": pr[0].get("full_compare"),
                          **({"errors": [p["error"] for p in pr if "error" in p]} if any("error" in p for p in pr)
                             else {})}
     if world > 1:
@@ -796,6 +807,51 @@ def timed_parity(name, cfg, seed, T, k: int, rank: int) -> dict:
         r = bp.meow_fixed(T["keys"].view(n, L)[ti].cpu().numpy(), L, u64(T["out"][ti]), seeds)
     r["seconds"] = round(time.perf_counter() - t0, 2)
     return r
+
+
+POISON = 0xA5
+
+
+def full_compare(kvh, cfg, T, run, out) -> dict:
+    """After the timed region: clone the output of the last timed launch,
+    fill every output buffer with 0xA5 bytes, launch once more (default chunk
+    order), compare the WHOLE output on the device with the clone and count
+    words still holding the sentinel; then the same under the static chunk
+    order (knob 24 = 1).  Every key's output must be rewritten, identically,
+    by both orders (src/key_hash.c:1413-1429: every key has a hash)."""
+    import torch
+    if cfg.get("ingest"):
+        k = int(T["t_cnt"].item())
+        outs = [T["t_offs"][:k], T["t_lens"][:k], T["t_out"][:k]]
+    elif cfg.get("sort"):
+        outs = [T["s_ho"], T["s_io"]]
+    elif cfg.get("crc"):
+        outs = [T["crc_out"]]
+    elif cfg.get("positions"):
+        outs = [T["pos"]] + ([T["hashes"]] if cfg["positions"] == "fused" else [])
+    else:
+        outs = [out]
+    timed = [t.clone() for t in outs]
+    word = int.from_bytes(bytes([POISON]) * 8, "little", signed=True)
+    res = {"words": int(sum(t.numel() for t in outs)), "against": "the timed output, whole, on the device"}
+    for name, order in (("default_order", None), ("static_order", 1)):
+        prev = kvh.lib.kvh_set_tuning(24, order) if order is not None else None
+        try:
+            for t in outs:
+                t.view(torch.uint8).fill_(POISON)
+            run(out)
+            torch.cuda.synchronize()
+        finally:
+            if prev is not None:
+                kvh.lib.kvh_set_tuning(24, prev)
+        same = all(torch.equal(a, b) for a, b in zip(outs, timed))
+        left = sum(int((t.view(torch.int64) == word).sum()) for t in outs
+                   if t.dtype == torch.int64 and t.is_contiguous())
+        res[name] = {"equal": bool(same), "sentinel_words": left}
+    for t, c in zip(outs, timed):  # leave the timed output in place
+        t.copy_(c)
+    res["ok"] = all(res[k]["equal"] and res[k]["sentinel_words"] == 0 for k in ("default_order", "static_order"))
+    return res
 
 
 def copy_peak(alg_bytes):

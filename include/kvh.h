@@ -451,27 +451,32 @@ const char *kvh_strerror(int err);
 const char *kvh_version(void);
 /* synchronise the current device (host wall-clock timing helpers) */
 int         kvh_device_synchronize(void);
+/* Streams.  The in-order streaming kernels (fixed and variable length,
+ * multi-seed, fused positions, CRC32C, span hashing) take their chunks in
+ * address order through ticket words kept per (device, stream): made on a
+ * stream's first call (synchronous hipMalloc / hipMemset, once per 256
+ * streams), reset by each launch's last workgroup, so launches on one
+ * stream need nothing else.  hipStreamPerThread gets words per calling
+ * thread.  A call on a stream that is being captured into a graph launches
+ * the static-order form of its kernel (no shared words: the graph may be
+ * replayed on any stream, and concurrently).  kvh_stream_release
+ * synchronises `stream` and hands its words back; call it before destroying
+ * a stream that called this library (not needed for the null stream or
+ * hipStreamPerThread).  0 or a negative error. */
+int         kvh_stream_release(void *stream);
 /* Tuning knobs: each selects among kernels that return the same hashes, or
  * sizes the host pipeline.  Process-wide; atomic (a call already running
  * keeps the value it read).
- *   0 = tables per LDS (0 per-length default, 2 or 4),
  *   1 = workgroups per CU multiplier (1-8), 2 = force the generic kernel (0/1),
- *   3 = keys per lane per step in the fixed-length kernel (0 default, 1, 2, 4, 8),
  *   7 = variable-length kernel (46 default: per-wave windows sorted by
  *       16-byte length class, keys read as dwordx4 groups, one straight-line
- *       variant per chunk shape, 16 waves, windows taken in address order
- *       through wave tickets; 23 the same with a static window order; 24 / 25
- *       23 at 12 waves, 25 with the next block's groups in flight; 44 / 47
- *       23 / 46 with four tables at 16 copies; 45 23 with clamped group loads;
- *       48 46 at 12 waves; 49 / 50 46 / 48 with the next block's groups in
- *       flight; 13 the round-2 sorted-window kernel; 7 sorted by
- *       exact length; 0 lane per key in input order),
+ *       variant per chunk shape, windows taken in address order through wave
+ *       tickets; 23 the same in the static window order; 0 lane per key in
+ *       input order),
  *   8 = multi-seed kernel (1 lanes per key, 0 one lane per key),
  *  14 = variable-length CRC32C kernel (6 default: length-sorted windows, 16
  *       waves on 16-copy tables, keys read as dwordx4 groups, the next key's
- *       first groups in flight; 4 without that; 5 with split histogram
- *       counters; 3 byte-aligned pieces; 1 10 waves on 32-copy tables; 2 8
- *       waves; 0 input order),
+ *       first groups in flight; 0 input order),
  *  15 / 16 = host pipeline chunk MiB / slots, 17 = ht_sort radix key bits
  *       (0 auto; nonzero also selects the radix engine),
  *  18 = span-hash kernel (2 / 1 short spans in place + per-wave medium and
@@ -486,19 +491,23 @@ int         kvh_device_synchronize(void);
  *  23 = ht_sort two-pass bucket sort (3 default: buckets of <= 3K records,
  *       up to 15 bucket bits with an 8-bit second pass, each bucket's
  *       records read once into registers by one of two 512-thread
- *       workgroups per CU; 1 the same at 6K-record buckets and one
- *       1024-thread workgroup per CU; 0 k_bk_sort; 2 k_bk_sortr2),
+ *       workgroups per CU; 0 k_bk_sort),
+ *  24 = chunk order of the streaming kernels (0 default and 2: every
+ *       fixed-length, runtime-length, multi-seed, fused-positions,
+ *       variable-length, CRC32C and span kernel takes its chunks in address
+ *       order through per-stream wave tickets; 1 the static per-wave order
+ *       everywhere),
  *  25 = counting-sort bits of the knob-23 = 3 bucket sort (0 default = 11,
  *       10, 12),
- *  24 = chunk order of the streaming kernels (0 default: every fixed-length,
- *       runtime-length, multi-seed, fused-positions, CRC32C and span kernel
- *       takes its chunks in address order through per-stream wave tickets;
- *       1 the static per-wave order everywhere; 2 wave tickets, 3 / 4 / 5
- *       workgroup tickets of 1 / 4 / 16 rounds for the fixed-length kernel),
- *   3 also takes 3 for the 40-64-byte fixed-length kernels.
- * Returns the previous value or KVH_EINVAL.  (Research kernels and ablation
- * builds whose outputs are not hashes exist only in the experiments build,
- * tools/libkvh_exp.so, never in libkvh.so.) */
+ *  26 = TEST ONLY: the first takers of every other wave ticket sleep
+ *       value x ~4 us before fetching the next one (0 default, up to 65535);
+ *       slows the in-order kernels, never changes their output.
+ * Returns the previous value or KVH_EINVAL.  The kernels that lost their A/B
+ * (knobs 0 and 3: tables per LDS and keys per lane other than the per-length
+ * defaults; knob 7 = 7, 13, 24, 25, 44, 45, 47-50; knob 14 = 1-5; knob 23 =
+ * 1, 2; knob 24 = 3-5) and the ablation builds whose outputs are not hashes
+ * exist only in the experiments build, tools/libkvh_exp.so, never in
+ * libkvh.so, which rejects those values. */
 int         kvh_set_tuning(int knob, int value);
 
 #ifdef __cplusplus

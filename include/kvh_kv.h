@@ -1,11 +1,12 @@
 /*
- * kvh_kv.h -- the kv_* Meow symbols that libkvh_kv.so exports, for a raikv
- * build that links it in place of src/key_hash.c's Meow family.  The
- * prototypes and types are the ones raikv's include/raikv/key_hash.h:59-130
- * declares (same names, argument meaning, x[] layouts and struct layouts), so
+ * kvh_kv.h -- the kv_* symbols that libkvh_kv.so exports, for a raikv
+ * build that links it in place of src/key_hash.c's Meow and CRC32C families.
+ * The prototypes and types are the ones raikv's include/raikv/key_hash.h:8-20
+ * (CRC32C) and :59-130 (Meow) declare (same names, argument meaning, x[] layouts and struct layouts), so
  * raikv's call sites (key_ctx.cpp:103, cli.cpp:846/1031, ctest.c:82, ...)
- * compile and link unchanged; only the Meow functions are provided (HMAC-Meow
- * is a different function, out of scope).  Each call is one GPU round trip
+ * compile and link unchanged; only the Meow and CRC32C functions are
+ * provided (HMAC-Meow is a different function, out of scope; kv_djb is an
+ * inline function of key_hash.h itself).  Each call is one GPU round trip
  * (include/kvh.h, the drop-ins' latency note): link compatibility, not a
  * per-key hot path.  A GPU error aborts the process (the reference functions
  * cannot fail and have no error return).
@@ -36,6 +37,17 @@ typedef struct {
 } meow_vec_t;
 #endif
 
+/* CRC32C (key_hash.h:8-20; key_hash.c:27-179) */
+uint32_t kv_hash_uint(uint32_t i);
+uint32_t kv_hash_uint2(uint32_t r, uint32_t i);
+uint32_t kv_crc_c(const void *p, size_t sz, uint32_t seed);
+void kv_crc_c_2_diff(const void *p, size_t sz, uint32_t *seed, const void *p2, size_t sz2, uint32_t *seed2);
+void kv_crc_c_4_diff(const void *p, size_t sz, uint32_t *seed, const void *p2, size_t sz2, uint32_t *seed2,
+                     const void *p3, size_t sz3, uint32_t *seed3, const void *p4, size_t sz4, uint32_t *seed4);
+void kv_crc_c_array(const void **p, size_t *psz, uint32_t *seed, size_t count);
+void kv_crc_c_key_array(const void *p, size_t *psz, uint32_t *seed, size_t count);
+
+/* Meow (key_hash.h:59-130) */
 uint64_t kv_hash_meow64(const void *p, size_t sz, uint64_t seed);
 void kv_hash_meow128(const void *p, size_t sz, uint64_t *h1, uint64_t *h2);
 void kv_hash_meow128_vec(const meow_vec_t *vec, size_t vec_sz, uint64_t *h1, uint64_t *h2);

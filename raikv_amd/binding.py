@@ -153,8 +153,41 @@ def check(rc: int, what: str = "kvh") -> None:
         raise KvhError(f"{what} failed: {rc} ({msg.decode() if msg else '?'})")
 
 
+# Test hook: with poisoning on, every output this module
+# allocates -- device tensors and host arrays -- is filled with 0xA5 bytes
+# before the call, so an element the kernel never wrote shows up as a
+# mismatch instead of as whatever the caching allocator left there.  Off by
+# default (the product allocates outputs uninitialised); tests/conftest.py
+# turns it on for the GPU suite, or KVH_POISON_OUTPUTS=1.
+_POISON = os.environ.get("KVH_POISON_OUTPUTS", "") == "1"
+POISON_BYTE = 0xA5
+
+
+def set_poison_outputs(on: bool) -> bool:
+    """Turn output poisoning on or off; returns the previous setting."""
+    global _POISON
+    prev, _POISON = _POISON, bool(on)
+    return prev
+
+
+def _empty(shape, dtype, device):
+    t = torch.empty(shape, dtype=dtype, device=device)
+    if _POISON and t.numel():
+        t.view(torch.uint8).fill_(POISON_BYTE)  # on the current stream; _stream_ptr orders a caller's stream after it
+    return t
+
+
+def _np_empty(shape, dtype=np.uint64):
+    a = np.empty(shape, dtype=dtype)
+    if _POISON:
+        a.view(np.uint8).fill(POISON_BYTE)
+    return a
+
+
 def _stream_ptr(stream) -> Optional[int]:
     if stream is not None:
+        if _POISON and torch is not None and hasattr(stream, "wait_stream"):
+            stream.wait_stream(torch.cuda.current_stream())  # the poison fill first
         return int(getattr(stream, "cuda_stream", stream))
     if torch is not None and torch.cuda.is_available():
         return int(torch.cuda.current_stream().cuda_stream)
@@ -194,7 +227,7 @@ def _dev_ptr(t) -> int:
 
 
 def _new_out(shape, like):
-    return torch.empty(shape, dtype=torch.int64, device=like.device)
+    return _empty(shape, torch.int64, like.device)
 
 
 # --------------------------------------------------------------- batches
@@ -219,7 +252,7 @@ def ht_positions(hashes, geom: "HtGeom", out=None, pos32: bool = False, stream=N
     n = hashes.numel() // 2
     a = geom.per_key
     if out is None:
-        out = torch.empty((n, a), dtype=torch.int32 if pos32 else torch.int64, device=hashes.device)
+        out = _empty((n, a), torch.int32 if pos32 else torch.int64, hashes.device)
     check(lib.kvh_ht_positions(_dev_ptr(hashes) if n else None, n, C.byref(geom), _dev_ptr(out) if n else None,
                                KVH_POS32 if pos32 else 0, _stream_ptr(stream)), "kvh_ht_positions")
     return out
@@ -234,7 +267,7 @@ def meow128_fixed_positions(keys, key_len: int, seed: Tuple[int, int], geom: "Ht
     if hashes is None and keep_hashes:
         hashes = _new_out((n, 2), keys)
     if out is None:
-        out = torch.empty((n, a), dtype=torch.int32 if pos32 else torch.int64, device=keys.device)
+        out = _empty((n, a), torch.int32 if pos32 else torch.int64, keys.device)
     check(lib.kvh_meow128_fixed_positions(_dev_ptr(keys) if n else None, key_len, n, U64(seed[0] & (2**64 - 1)),
                                           U64(seed[1] & (2**64 - 1)), C.byref(geom),
                                           _dev_ptr(hashes) if (hashes is not None and n) else None,
@@ -262,7 +295,7 @@ class HtSorter:
         if out is None:
             out = _new_out((n, 2), hashes)
         if items_out is None:
-            items_out = torch.empty((n,), dtype=torch.int64, device=hashes.device)
+            items_out = _empty((n,), torch.int64, hashes.device)
         check(lib.kvh_ht_sort(_dev_ptr(hashes) if n else None, _dev_ptr(items) if items is not None else None, n,
                               C.byref(self.geom), _dev_ptr(out) if n else None, _dev_ptr(items_out) if n else None,
                               _dev_ptr(self.dups), KVH_DEDUP if dedup else 0, _dev_ptr(self.scratch),
@@ -278,8 +311,8 @@ def tokenize(text, max_token: int = 256, cap: Optional[int] = None, stream=None)
     scratch = torch.empty((max(1, lib.kvh_tokenize_scratch_bytes(n) // 8),), dtype=torch.int64, device=text.device)
     if cap is None:
         cap = n // 2 + 1
-    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=text.device)
-    lens = torch.empty((max(cap, 1),), dtype=torch.int32, device=text.device)
+    offs = _empty((max(cap, 1),), torch.int64, text.device)
+    lens = _empty((max(cap, 1),), torch.int32, text.device)
     _after_current(stream)
     check(lib.kvh_tokenize(_dev_ptr(text) if n else None, n, max_token, _dev_ptr(offs), _dev_ptr(lens), cap,
                            _dev_ptr(cnt), _dev_ptr(scratch), scratch.numel() * 8, _stream_ptr(stream)), "kvh_tokenize")
@@ -297,9 +330,9 @@ def tokenize_hash(text, seed: Tuple[int, int], max_token: int = 256, cap: Option
     scratch = torch.empty((max(1, lib.kvh_tokenize_scratch_bytes(n) // 8),), dtype=torch.int64, device=text.device)
     if cap is None:
         cap = n // 2 + 1
-    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=text.device)
-    lens = torch.empty((max(cap, 1),), dtype=torch.int32, device=text.device)
-    out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=text.device)
+    offs = _empty((max(cap, 1),), torch.int64, text.device)
+    lens = _empty((max(cap, 1),), torch.int32, text.device)
+    out = _empty((max(cap, 1), 2), torch.int64, text.device)
     _after_current(stream)
     check(lib.kvh_tokenize_hash(_dev_ptr(text) if n else None, n, max_token, U64(seed[0] & (2**64 - 1)),
                                 U64(seed[1] & (2**64 - 1)),
@@ -333,7 +366,7 @@ def frag_offsets(buf, cap: Optional[int] = None, stream=None):
                           device=buf.device)
     if cap is None:
         cap = n // 2 + 1
-    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=buf.device)
+    offs = _empty((max(cap, 1),), torch.int64, buf.device)
     _after_current(stream)
     check(lib.kvh_frag_offsets(_dev_ptr(buf) if n else None, n, _dev_ptr(offs), cap, _dev_ptr(cnt), _dev_ptr(scratch),
                                scratch.numel() * 8, _stream_ptr(stream)), "kvh_frag_offsets")
@@ -349,8 +382,8 @@ def frags_hash(buf, seed: Tuple[int, int], cap: Optional[int] = None, fixup: boo
                           device=buf.device)
     if cap is None:
         cap = n // 2 + 1
-    offs = torch.empty((max(cap, 1),), dtype=torch.int64, device=buf.device)
-    out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=buf.device)
+    offs = _empty((max(cap, 1),), torch.int64, buf.device)
+    out = _empty((max(cap, 1), 2), torch.int64, buf.device)
     _after_current(stream)
     check(lib.kvh_frags_hash(_dev_ptr(buf) if n else None, n, U64(seed[0] & (2**64 - 1)), U64(seed[1] & (2**64 - 1)),
                              KVH_FIXUP if fixup else 0, _dev_ptr(offs), _dev_ptr(out), cap, _dev_ptr(cnt),
@@ -375,7 +408,7 @@ def crc_c_fixed(keys, key_len: int, seed: int = 0, seeds=None, out=None, stream=
     patterns in an int32 device tensor [n]; seeds: optional int32 [n]."""
     n = keys.numel() // key_len if key_len else 0
     if out is None:
-        out = torch.empty((n,), dtype=torch.int32, device=keys.device)
+        out = _empty((n,), torch.int32, keys.device)
     check(lib.kvh_crc_c_fixed(_dev_ptr(keys) if keys.numel() else None, key_len, n,
                               _dev_ptr(seeds) if seeds is not None else None, seed & 0xFFFFFFFF,
                               _dev_ptr(out) if n else None, _stream_ptr(stream)), "kvh_crc_c_fixed")
@@ -386,7 +419,7 @@ def crc_c_var(keys, offsets, seed: int = 0, seeds=None, out=None, stream=None):
     """kv_crc_c over n variable-length keys (u64 offsets [n+1])."""
     n = offsets.numel() - 1
     if out is None:
-        out = torch.empty((n,), dtype=torch.int32, device=offsets.device)
+        out = _empty((n,), torch.int32, offsets.device)
     check(lib.kvh_crc_c_var(_dev_ptr(keys) if keys.numel() else _dev_ptr(offsets), _dev_ptr(offsets), n,
                             _dev_ptr(seeds) if seeds is not None else None, seed & 0xFFFFFFFF,
                             _dev_ptr(out) if n else None, _stream_ptr(stream)), "kvh_crc_c_var")
@@ -445,7 +478,7 @@ def meow128_fixed_host(keys: np.ndarray, key_len: int, seed: Tuple[int, int],
     """Host keys -> host hashes through the chunked H2D/kernel/D2H pipeline."""
     n = keys.size // key_len
     if out is None:
-        out = np.empty((n, 2), dtype=np.uint64)
+        out = _np_empty((n, 2))
     check(lib.kvh_meow128_fixed_host(keys.ctypes.data, key_len, n, U64(seed[0]), U64(seed[1]),
                                      out.ctypes.data, KVH_FIXUP if fixup else 0),
           "kvh_meow128_fixed_host")
@@ -459,7 +492,7 @@ def meow128_var_host(keys: np.ndarray, offsets: np.ndarray, seed: Tuple[int, int
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = offsets.size - 1
     if out is None:
-        out = np.empty((n, 2), dtype=np.uint64)
+        out = _np_empty((n, 2))
     kb = keys if keys.size else np.zeros(1, np.uint8)
     check(lib.kvh_meow128_var_host(kb.ctypes.data, offsets.ctypes.data, n, U64(seed[0]), U64(seed[1]),
                                    out.ctypes.data, KVH_FIXUP if fixup else 0), "kvh_meow128_var_host")
@@ -478,12 +511,12 @@ def meow128_host_multi(keys: np.ndarray, seed: Tuple[int, int], devices: Sequenc
     if offsets is not None:
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         n = offsets.size - 1
-        out = np.empty((n, 2), dtype=np.uint64) if out is None else out
+        out = _np_empty((n, 2)) if out is None else out
         check(lib.kvh_meow128_var_host_multi(kb.ctypes.data, offsets.ctypes.data, n, U64(seed[0]), U64(seed[1]),
                                              out.ctypes.data, fl, dv, len(devices)), "kvh_meow128_var_host_multi")
     else:
         n = keys.size // key_len
-        out = np.empty((n, 2), dtype=np.uint64) if out is None else out
+        out = _np_empty((n, 2)) if out is None else out
         check(lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, key_len, n, U64(seed[0]), U64(seed[1]),
                                                out.ctypes.data, fl, dv, len(devices)),
               "kvh_meow128_fixed_host_multi")
@@ -572,7 +605,7 @@ class KeyFragment:
         sv = (U64 * 2)(seed & (2**64 - 1), seed2 & (2**64 - 1))
         raws = [f._raw() for f in frags]
         arr = (P * max(1, len(raws)))(*[C.cast(r, P) for r in raws])
-        out = np.empty((len(frags), 2), dtype=np.uint64)
+        out = _np_empty((len(frags), 2))
         check(lib.kvh_hash_key_frags(sv, arr, len(frags), out.ctypes.data), "kvh_hash_key_frags")
         return out
 

@@ -538,9 +538,9 @@ int kvh_crc_c_fixed(const void* keys, uint32_t key_len, size_t n, const uint32_t
   const uint8_t* k = (const uint8_t*)keys;
   // chunk order (knob 24): wave tickets (in address order) unless 1 = static
   unsigned long long* tk = nullptr;
-  const bool q = knob(g_tune_order) != 1;
-  if (q)
+  if (knob(g_tune_order) != 1)
     if ((rc = stream_tickets(st, &tk))) return rc;
+  const bool q = tk != nullptr;  // no words for a captured launch: the static order
   switch (key_len) {
 #define KVH_CRC_L(Lv, Uv)                                                                                   \
   case Lv:                                                                                                  \
@@ -569,7 +569,19 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
   const int v = g_tune_crc_var.load(std::memory_order_relaxed);
-  if (v == 1)
+  if (v == 6) {  // windows in address order unless knob 24 = 1 (or a captured launch)
+    unsigned long long* tk = nullptr;
+    if (knob(g_tune_order) != 1)
+      if ((rc = stream_tickets((hipStream_t)stream, &tk))) return rc;
+    if (tk)
+      hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2, 1, true>), dim3(cus), dim3(1024), 0,
+                         (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, tk);
+    else
+      hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
+                         (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, nullptr);
+  }
+#ifdef KVH_EXPERIMENTS  // the variants that lost their A/B (round 3): experiments build only
+  else if (v == 1)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 10>), dim3(cus), dim3(640), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 3)  // tables with 16 copies (64 KiB): 16 waves per CU
@@ -578,23 +590,13 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
   else if (v == 4)  // as 3, keys read as dwordx4 groups (crc_key_g)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 1>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
-  else if (v == 6) {  // as 4, the next key's first two groups in flight; windows in address order unless knob 24 = 1
-    if (knob(g_tune_order) != 1) {
-      unsigned long long* tk = nullptr;
-      if ((rc = stream_tickets((hipStream_t)stream, &tk))) return rc;
-      hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2, 1, true>), dim3(cus), dim3(1024), 0,
-                         (hipStream_t)stream, (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, tk);
-    } else {
-      hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
-                         (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, nullptr);
-    }
-  }
   else if (v == 5)  // as 4, two sub-counters per length bucket in the window sort
     hipLaunchKernelGGL((k_crc_var_sorted<256, 16, 0, 16, 1, 2>), dim3(cus), dim3(1024), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
   else if (v == 2)
     hipLaunchKernelGGL((k_crc_var_sorted<256, 8>), dim3(cus), dim3(512), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);
+#endif
   else
     hipLaunchKernelGGL(k_crc_var, dim3(grid_crc(n, cus)), dim3(kBlock), 0, (hipStream_t)stream,
                        (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out);

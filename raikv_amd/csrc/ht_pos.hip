@@ -277,9 +277,9 @@ int launch_fused(const uint8_t* k, uint64_t n, uint64_t s1, uint64_t s2, HtGeom 
   const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t)cus * 2));
   // chunk order (knob 24): wave tickets (in address order) unless 1 = static
   unsigned long long* tk = nullptr;
-  const bool q = knob(g_tune_order) != 1;
-  if (q)
+  if (knob(g_tune_order) != 1)
     if (int rc = stream_tickets(st, &tk)) return rc;
+  const bool q = tk != nullptr;  // no words for a captured launch: the static order
 #define KVH_FP(Wt, Qv) hipLaunchKernelGGL((k_fixed_pos<L, NT, A, P32, Wt, U, Qv>), dim3((uint32_t)grid), \
                                           dim3(kFusedBlock), 0, st, k, n, s1, s2, g, out, pos, tk)
   if (narrow(g)) {

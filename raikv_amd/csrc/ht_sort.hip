@@ -1736,6 +1736,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
         if (hd == 10) KVH_BKH(10); else if (hd == 12) KVH_BKH(12); else KVH_BKH(11);
 #undef KVH_BKH
       }
+#ifdef KVH_EXPERIMENTS  // knob 23 = 1 / 2 lost their A/B (round 4): experiments build only
       else if (small_b && b3 == 2)
         hipLaunchKernelGGL((k_bk_sortr2<7168, 11>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0,
                            st, (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
@@ -1744,6 +1745,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
         hipLaunchKernelGGL((k_bk_sortr<7168, 12>), dim3(std::min<uint32_t>(nb, (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,
                            items_out, dedup ? 1u : 0u, (unsigned long long*)dup_count, novf, ovf);
+#endif
       else if (small_b)
         hipLaunchKernelGGL((k_bk_sort<8000, 12, R24>), dim3(std::min<uint32_t>(nb, 2u * (uint32_t)cus)), dim3(kBkT), 0, st,
                            (const R24*)recB, (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out,

@@ -944,9 +944,10 @@ namespace {
 int launch_spans(const void* buf, const uint64_t* offs, const uint32_t* lens, uint64_t n, uint64_t seed1,
                  uint64_t seed2, uint64_t* out, uint32_t flags, const uint64_t* dcount, uint32_t grid,
                  hipStream_t st) {
-  if (knob(g_tune_order) != 1 && n < 0xffffffffull) {
-    unsigned long long* tk = nullptr;
+  unsigned long long* tk = nullptr;
+  if (knob(g_tune_order) != 1 && n < 0xffffffffull)
     if (int rc = stream_tickets(st, &tk)) return rc;
+  if (tk) {  // (no words for a captured launch: the static order)
     hipLaunchKernelGGL((k_spans<4, 2, 2, true>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens, n,
                        seed1, seed2, out, flags, dcount, tk);
   } else {

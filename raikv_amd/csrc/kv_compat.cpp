@@ -1,8 +1,8 @@
-// kv_compat.cpp -- link-compatible kv_* Meow symbols over the C-ABI
-// (libkvh_kv.so).  A raikv build that drops src/key_hash.c's Meow family and
-// links this library instead keeps every call site of
-// include/raikv/key_hash.h:59-130 unchanged: same names, same argument
-// meaning, same x[] layouts, void returns.  Each call runs on the current
+// kv_compat.cpp -- link-compatible kv_* symbols over the C-ABI
+// (libkvh_kv.so).  A raikv build that drops src/key_hash.c's Meow and CRC32C
+// families and links this library instead keeps every call site of
+// include/raikv/key_hash.h:8-20 and :59-130 unchanged: same names, same
+// argument meaning, same x[] / seed[] layouts, void returns.  Each call runs on the current
 // GPU through libkvh.so's host drop-ins (one device round trip per call: the
 // latency trap include/kvh.h documents above them -- this library is for
 // link compatibility and tests; batches belong on kvh_meow128_*_host /
@@ -91,6 +91,42 @@ void kv_hash_meow128_2_diff_length(const void* p, size_t sz, const void* p2, siz
 void kv_hash_meow128_4_diff_length(const void* p, size_t sz, const void* p2, size_t sz2, const void* p3,
                                    size_t s3, const void* p4, size_t s4, uint64_t* x) {
   must(kvh_hash_meow128_4_diff_length(p, sz, p2, sz2, p3, s3, p4, s4, x), "kv_hash_meow128_4_diff_length");
+}
+
+// CRC32C family (key_hash.h:8-20, key_hash.c:27-179): the kvh_crc_c drop-ins
+uint32_t kv_hash_uint(uint32_t i) {
+  const uint32_t h = kvh_hash_uint(i);
+  must(kvh_last_error(), "kv_hash_uint");
+  return h;
+}
+
+uint32_t kv_hash_uint2(uint32_t r, uint32_t i) {
+  const uint32_t h = kvh_hash_uint2(r, i);
+  must(kvh_last_error(), "kv_hash_uint2");
+  return h;
+}
+
+uint32_t kv_crc_c(const void* p, size_t sz, uint32_t seed) {
+  const uint32_t h = kvh_crc_c(p, sz, seed);
+  must(kvh_last_error(), "kv_crc_c");
+  return h;
+}
+
+void kv_crc_c_2_diff(const void* p, size_t sz, uint32_t* seed, const void* p2, size_t sz2, uint32_t* seed2) {
+  must(kvh_crc_c_2_diff(p, sz, seed, p2, sz2, seed2), "kv_crc_c_2_diff");
+}
+
+void kv_crc_c_4_diff(const void* p, size_t sz, uint32_t* seed, const void* p2, size_t sz2, uint32_t* seed2,
+                     const void* p3, size_t sz3, uint32_t* seed3, const void* p4, size_t sz4, uint32_t* seed4) {
+  must(kvh_crc_c_4_diff(p, sz, seed, p2, sz2, seed2, p3, sz3, seed3, p4, sz4, seed4), "kv_crc_c_4_diff");
+}
+
+void kv_crc_c_array(const void** p, size_t* psz, uint32_t* seed, size_t count) {
+  must(kvh_crc_c_array(p, psz, seed, count), "kv_crc_c_array");
+}
+
+void kv_crc_c_key_array(const void* p, size_t* psz, uint32_t* seed, size_t count) {
+  must(kvh_crc_c_key_array(p, psz, seed, count), "kv_crc_c_key_array");
 }
 
 }  // extern "C"

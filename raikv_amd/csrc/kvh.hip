@@ -158,45 +158,117 @@ int device_cus(int* cus) {
   return 0;
 }
 
-// Ticket counters for the in-order streaming kernels (k_fixed_q): two
-// words per (device, stream), zero between launches -- the kernel's last
-// workgroup puts them back to zero as it exits, so no memset precedes a
-// launch and graph capture sees one kernel.  Launches on one stream are
-// serialised, so a stream's pair is never used by two kernels at once.
+// Ticket words for the in-order streaming kernels (tickets.hpp): four u64
+// per (device, stream), zero between launches -- the kernel's last
+// workgroup puts the counters back to zero as it exits, so no memset precedes
+// a launch.  Launches on one stream are serialised, so a stream's words are
+// never used by two kernels at once.  Two kinds of handle do not name one
+// serialised queue, and are resolved here:
+//  - hipStreamPerThread is one handle value for a different stream on every
+//    host thread: its words are kept per (calling thread, device);
+//  - a launch captured into a graph may be replayed on any stream, and
+//    several replays may run at once: a captured launch takes the static
+//    chunk order (*tk = nullptr; the launchers then run the static form).
+// Lookups are one map search under the device's own lock.  kvh_stream_release
+// hands a stream's words back (before the stream is destroyed).  Word 2 holds
+// the test-only fetch delay of knob 26, written when the words are made.
+constexpr int kTkDev = 64;
+constexpr size_t kTkQuads = 256;  // words made 256 x 4 at a time
 struct TicketPool {
-  std::vector<unsigned long long*> chunks;  // 256 pairs each
-  std::vector<std::pair<hipStream_t, unsigned long long*>> by_stream;
+  std::mutex mu;
+  std::vector<unsigned long long*> chunks;
+  std::vector<std::pair<unsigned long long*, uint32_t>> spare;  // released (zero counters) and their delay word
+  std::map<std::pair<uintptr_t, uint32_t>, unsigned long long*> by_stream;  // (stream, delay) -> words
   size_t used = 0;
 };
-std::vector<TicketPool> g_tickets;
+TicketPool g_tickets[kTkDev];
+std::atomic<int> g_tune_tkdbg{0};  // knob 26: test-only ticket fetch delay (tickets.hpp word 2)
+
+// four zeroed words of device `dev` with word 2 = dbg; caller holds P.mu
+int new_words(TicketPool& P, uint32_t dbg, unsigned long long** out) {
+  hipError_t e;
+  unsigned long long* p = nullptr;
+  uint32_t had = 0;
+  if (!P.spare.empty()) {
+    p = P.spare.back().first;
+    had = P.spare.back().second;
+    P.spare.pop_back();
+  } else {
+    if (P.used == P.chunks.size() * kTkQuads) {
+      unsigned long long* c = nullptr;
+      if ((e = hipMalloc((void**)&c, kTkQuads * 4 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
+      if ((e = hipMemset(c, 0, kTkQuads * 4 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_err(e);
+      P.chunks.push_back(c);
+    }
+    p = P.chunks[P.used / kTkQuads] + 4 * (P.used % kTkQuads);
+    P.used++;
+  }
+  if (had != dbg) {
+    const unsigned long long w = dbg;
+    if ((e = hipMemcpy(p + 2, &w, sizeof w, hipMemcpyHostToDevice)) != hipSuccess) return hip_err(e);
+  }
+  *out = p;
+  return 0;
+}
+
+struct PerThreadWords {  // hipStreamPerThread's words of this thread, per device (kept for the process)
+  unsigned long long* p[kTkDev] = {};
+  uint32_t dbg[kTkDev] = {};
+};
+thread_local PerThreadWords t_pts;
 
 int stream_tickets(hipStream_t st, unsigned long long** tk) {
+  *tk = nullptr;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return hip_err(e);
-  std::lock_guard<std::mutex> g(g_mu);
-  if ((int)g_tickets.size() <= dev) g_tickets.resize(dev + 1);
-  TicketPool& P = g_tickets[dev];
-  for (auto& sp : P.by_stream)
-    if (sp.first == st) { *tk = sp.second; return 0; }
-  constexpr size_t kPairs = 256;
-  if (P.used == P.chunks.size() * kPairs) {
-    // a new chunk needs hipMalloc + hipMemset, which a stream being captured
-    // into a graph cannot take: make one call on the stream before capturing
-    // 
+  if (dev < 0 || dev >= kTkDev) return set_err(KVH_EINVAL);
+  if (st != nullptr && st != hipStreamLegacy) {  // the legacy null stream is never captured
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (st && hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
-      return set_err(KVH_EINVAL);
-    unsigned long long* c = nullptr;
-    if ((e = hipMalloc((void**)&c, kPairs * 2 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
-    if ((e = hipMemset(c, 0, kPairs * 2 * sizeof(unsigned long long))) != hipSuccess) return hip_err(e);
-    P.chunks.push_back(c);
+    if ((e = hipStreamIsCapturing(st, &cs)) != hipSuccess) return hip_err(e);
+    if (cs != hipStreamCaptureStatusNone) return 0;  // captured: the static order
   }
-  unsigned long long* p = P.chunks[P.used / kPairs] + 2 * (P.used % kPairs);
-  P.used++;
-  P.by_stream.emplace_back(st, p);
+  const uint32_t dbg = (uint32_t)g_tune_tkdbg.load(std::memory_order_relaxed);
+  TicketPool& P = g_tickets[dev];
+  if (st == hipStreamPerThread) {
+    if (t_pts.p[dev] && t_pts.dbg[dev] == dbg) { *tk = t_pts.p[dev]; return 0; }
+    std::lock_guard<std::mutex> g(P.mu);
+    unsigned long long* p = nullptr;
+    if (int rc = new_words(P, dbg, &p)) return rc;
+    t_pts.p[dev] = p;  // a previous thread-local set (another delay: tests only) stays allocated
+    t_pts.dbg[dev] = dbg;
+    *tk = p;
+    return 0;
+  }
+  std::lock_guard<std::mutex> g(P.mu);
+  const auto key = std::make_pair((uintptr_t)st, dbg);
+  auto it = P.by_stream.find(key);
+  if (it != P.by_stream.end()) { *tk = it->second; return 0; }
+  unsigned long long* p = nullptr;
+  if (int rc = new_words(P, dbg, &p)) return rc;
+  P.by_stream.emplace(key, p);
   *tk = p;
   return 0;
+}
+
+int stream_release(hipStream_t st) {
+  if (st == nullptr || st == hipStreamLegacy || st == hipStreamPerThread) return set_err(0);
+  hipError_t e = hipStreamSynchronize(st);  // every launch that holds the words has finished
+  if (e != hipSuccess) return hip_err(e);
+  for (int d = 0; d < kTkDev; d++) {
+    TicketPool& P = g_tickets[d];
+    std::lock_guard<std::mutex> g(P.mu);
+    for (auto it = P.by_stream.begin(); it != P.by_stream.end();) {
+      if (it->first.first == (uintptr_t)st) {
+        P.spare.emplace_back(it->second, it->first.second);
+        it = P.by_stream.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  return set_err(0);
 }
 
 int launch_done() {
@@ -1011,6 +1083,8 @@ const char* kvh_strerror(int err) {
 
 const char* kvh_version(void) { return KVH_VERSION; }
 
+int kvh_stream_release(void* stream) { return stream_release((hipStream_t)stream); }
+
 int kvh_device_synchronize(void) {
   hipError_t e = hipDeviceSynchronize();
   return e == hipSuccess ? set_err(0) : hip_err(e);
@@ -1019,20 +1093,26 @@ int kvh_device_synchronize(void) {
 // Every knob selects among kernels whose outputs are the same hashes (or
 // sizes the host pipeline); the ablation and research knobs exist only in
 // the experiments build.  Atomic exchange: safe against concurrent calls.
+#ifdef KVH_EXPERIMENTS
+constexpr bool kExperiments = true;   // tools/libkvh_exp.so: the product sources with the losing variants
+#else
+constexpr bool kExperiments = false;
+#endif
 int kvh_set_tuning(int k, int value) {
   auto set = [](Knob& g, int v) { return g.exchange(v, std::memory_order_relaxed); };
   switch (k) {
-    case 0: if (value != 0 && value != 2 && value != 4) return KVH_EINVAL; return set(g_tune_nt, value);
+    case 0: if (value != 0 && !(kExperiments && (value == 2 || value == 4))) return KVH_EINVAL; return set(g_tune_nt, value);
     case 1: if (value < 1 || value > 8) return KVH_EINVAL; return set(g_tune_wgmul, value);
     case 2: return set(g_tune_generic, value ? 1 : 0);
-    case 3: if (value < 0 || value > 8 || value == 5 || value == 6 || value == 7) return KVH_EINVAL;
+    case 3: if (value != 0 && !(kExperiments && value > 0 && value <= 8 && value != 5 && value != 6 && value != 7))
+              return KVH_EINVAL;
             return set(g_tune_kpl, value);
-    case 7: if (value != 0 && value != 7 && value != 13 && (value < 23 || value > 25) && (value < 44 || value > 50) &&
-                !(g_exp.var_knob && g_exp.var_knob(value)))
+    case 7: if (value != 0 && value != 23 && value != 46 && !(g_exp.var_knob && g_exp.var_knob(value)))
               return KVH_EINVAL;
             return set(g_tune_var, value);
     case 8: return set(g_tune_ms_lanes, value ? 1 : 0);
-    case 14: if (value < 0 || value > 6) return KVH_EINVAL; return set(g_tune_crc_var, value);
+    case 14: if (value != 0 && value != 6 && !(kExperiments && value > 0 && value < 6)) return KVH_EINVAL;
+             return set(g_tune_crc_var, value);
     case 15: if (value < 1 || value > 1024) return KVH_EINVAL; return set(g_tune_pipe_mib, value);
     case 16: if (value < 2 || value > 16) return KVH_EINVAL; return set(g_tune_pipe_slots, value);
     case 17: if (value < 0 || value > 64) return KVH_EINVAL; return set(g_tune_sort_bits, value);
@@ -1041,9 +1121,11 @@ int kvh_set_tuning(int k, int value) {
     case 20: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_engine, value);
     case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
     case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_cap, value);
-    case 23: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_sort_b3, value);
-    case 24: if (value < 0 || value > 5) return KVH_EINVAL; return set(g_tune_order, value);
+    case 23: if (value != 0 && value != 3 && !(kExperiments && (value == 1 || value == 2))) return KVH_EINVAL;
+             return set(g_tune_sort_b3, value);
+    case 24: if (value < 0 || value > (kExperiments ? 5 : 2)) return KVH_EINVAL; return set(g_tune_order, value);
     case 25: if (value != 0 && value != 10 && value != 11 && value != 12) return KVH_EINVAL; return set(g_tune_sort_hd, value);
+    case 26: if (value < 0 || value > 0xffff) return KVH_EINVAL; return g_tune_tkdbg.exchange(value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }

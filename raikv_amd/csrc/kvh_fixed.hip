@@ -69,6 +69,7 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
   }
 }
 
+#ifdef KVH_EXPERIMENTS  // lost its A/B to k_fixed_qw (round 4): experiments build only
 // k_fixed with the chunks taken IN ADDRESS ORDER (round 4, knob 24 = 3/4/5;
 // k_fixed_qw below is the default form).  A workgroup-iteration (16 waves x 64U keys) is one ticket from a
 // per-stream counter (stream_tickets), the next ticket fetched one iteration
@@ -131,6 +132,8 @@ k_fixed_q(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2
     }
   }
 }
+
+#endif  // KVH_EXPERIMENTS
 
 // k_fixed_qw: the same in-order tickets without the per-ticket barrier
 // (tickets.hpp: each wave takes chunks one at a time through an LDS counter
@@ -271,24 +274,30 @@ int launch_k(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
   // chunk order (knob 24): wave tickets (in address order)
   // by default, at every length with the keys per lane re-swept under them
-  // (profiles/r04/s14/sweep.jsonl); knob 24 = 1: the static order
-  int ord = knob(g_tune_order);
-  if (ord == 0) ord = 2;
-  if (ord != 1) {
+  // (profiles/r04/s14/sweep.jsonl); knob 24 = 1, and a launch captured into a
+  // graph (stream_tickets gives no words), the static order
+  if (knob(g_tune_order) != 1) {
     unsigned long long* tk = nullptr;
     if (int rc = stream_tickets(st, &tk)) return rc;
+#ifdef KVH_EXPERIMENTS
+    const int ord = knob(g_tune_order);
 #define KVH_Q(A, R) hipLaunchKernelGGL((k_fixed_q<L, NT, A, U, R>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, \
                                        out, flags, tk)
-    if (ord == 2) {
+    if (tk && ord >= 3) {
+      if (a16) { if (ord == 3) KVH_Q(true, 1); else if (ord == 4) KVH_Q(true, 4); else KVH_Q(true, 16); }
+      else { if (ord == 3) KVH_Q(false, 1); else if (ord == 4) KVH_Q(false, 4); else KVH_Q(false, 16); }
+      return launch_done();
+    }
+#undef KVH_Q
+#endif
+    if (tk) {
       if (a16)
         hipLaunchKernelGGL((k_fixed_qw<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags, tk);
       else
         hipLaunchKernelGGL((k_fixed_qw<L, NT, false, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags,
                            tk);
-    } else if (a16) { if (ord == 3) KVH_Q(true, 1); else if (ord == 4) KVH_Q(true, 4); else KVH_Q(true, 16); }
-    else { if (ord == 3) KVH_Q(false, 1); else if (ord == 4) KVH_Q(false, 4); else KVH_Q(false, 16); }
-#undef KVH_Q
-    return launch_done();
+      return launch_done();
+    }
   }
   if (a16)
     hipLaunchKernelGGL((k_fixed<L, NT, true, U>), dim3(grid), dim3(kBlock), 0, st, keys, n, s1, s2, out, flags);
@@ -433,9 +442,10 @@ template <int NC, int NT, int U>
 int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, uint64_t s2, uint64_t* out,
                     uint32_t flags, hipStream_t st, int cus) {
   const uint32_t grid = grid_for(n, cus, NT == 4 ? 1 : 2);
-  if (knob(g_tune_order) != 1) {  // chunk order (knob 24): wave tickets unless 1 = static
-    unsigned long long* tk = nullptr;
+  unsigned long long* tk = nullptr;
+  if (knob(g_tune_order) != 1)  // chunk order (knob 24): wave tickets unless 1 = static (or captured)
     if (int rc = stream_tickets(st, &tk)) return rc;
+  if (tk) {
     hipLaunchKernelGGL((k_fixed_rt<NC, NT, U, true>), dim3(grid), dim3(kBlock), 0, st, keys, n, L, s1, s2, out,
                        flags, tk);
   } else {
@@ -445,61 +455,49 @@ int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, ui
   return launch_done();
 }
 
-// Default (NT, U) per length from tools/tune.py and tools/len_sweep.py
-// sweeps; knobs 0 and 3 select the others (a pair with no instance at this
-// length runs the length's default).
+// Default (NT, U) per length, from the round-4 sweeps under wave tickets
+// over 100M keys (profiles/r04/s14/sweep.jsonl, s16/ab.jsonl): Td0..Td3 in LDS
+// (NT4: no rotations; 8 B 6 % over NT2) everywhere; keys per lane 4 at 8, 16,
+// 24 and 32 B (32 B: 2.6 % over 2), 3 at 40 / 48 B (7 / 4 % over the round-3
+// defaults), 1 at 56 / 64 B (4 / 8 %).  The other (NT, U) instances are the
+// sweep's losers and compile only into the experiments build, where knobs 0
+// and 3 select them (a pair with no instance runs the default).
+template <int L>
+struct FixedDefault {
+  static constexpr int NT = 4;
+  static constexpr int U = (L == 40 || L == 48) ? 3 : (L >= 56 ? 1 : 4);
+};
+
 template <int L>
 int launch_fixed_nt(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out,
                     uint32_t flags, hipStream_t st, int cus) {
   if (int rc = 0; g_exp.fixed && g_exp.fixed(L, keys, n, s1, s2, out, flags, st, cus, knob(g_tune_nt), knob(g_tune_kpl), &rc))
     return rc;
-  if constexpr (L == 16 || L == 32) {
-    // per-length defaults: Td0..Td3 in LDS (no
-    // rotations), 4 keys per lane (32 B: 2 under the static order, 4 under
-    // wave tickets, 2.6 % apart: profiles/r04/s16/ab.jsonl)
-    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
-    const int nt = tnt ? tnt : 4;
-    const int kpl = tkpl ? tkpl : 4;
-    switch (nt * 100 + kpl) {
-      case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 408: return launch_k<L, 4, 8>(keys, n, s1, s2, out, flags, st, cus);
-      case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 208: return launch_k<L, 2, 8>(keys, n, s1, s2, out, flags, st, cus);
-      default: break;  // a knob pair without an instance: this length's default
-    }
-    return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
-  } else {
-    // per-length defaults (NT, keys per lane) under wave tickets, from the
-    // round-4 sweep over 100M keys (profiles/r04/s14/sweep.jsonl; the round-3
-    // static-order sweep had 40-48 B at U1 and 56-64 B at U2): 8 / 24 B
-    // U4, 40 / 48 B U3 (7 / 4 % over their previous defaults), 56 / 64 B U1
-    // (4 / 8 %); NT4 (8 B: 6 % over NT2, profiles/r04/s16/ab.jsonl)
-    constexpr int dnt = 4, dkpl = L == 8 || L == 24 ? 4 : (L == 40 || L == 48) ? 3 : 1;
-    const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
-    switch ((tnt ? tnt : dnt) * 100 + (tkpl ? tkpl : dkpl)) {
-      case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
-      case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
-      case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
-      case 403: if constexpr (L >= 40) return launch_k<L, 4, 3>(keys, n, s1, s2, out, flags, st, cus); break;
-      case 203: if constexpr (L >= 40) return launch_k<L, 2, 3>(keys, n, s1, s2, out, flags, st, cus); break;
-      default: break;
-    }
-    return launch_k<L, dnt, dkpl>(keys, n, s1, s2, out, flags, st, cus);  // no instance: the default
+  constexpr int dnt = FixedDefault<L>::NT, dkpl = FixedDefault<L>::U;
+#ifdef KVH_EXPERIMENTS
+  const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
+  switch ((tnt ? tnt : dnt) * 100 + (tkpl ? tkpl : dkpl)) {
+    case 401: return launch_k<L, 4, 1>(keys, n, s1, s2, out, flags, st, cus);
+    case 402: return launch_k<L, 4, 2>(keys, n, s1, s2, out, flags, st, cus);
+    case 404: return launch_k<L, 4, 4>(keys, n, s1, s2, out, flags, st, cus);
+    case 201: return launch_k<L, 2, 1>(keys, n, s1, s2, out, flags, st, cus);
+    case 202: return launch_k<L, 2, 2>(keys, n, s1, s2, out, flags, st, cus);
+    case 204: return launch_k<L, 2, 4>(keys, n, s1, s2, out, flags, st, cus);
+    case 408: if constexpr (L == 16 || L == 32) return launch_k<L, 4, 8>(keys, n, s1, s2, out, flags, st, cus); break;
+    case 208: if constexpr (L == 16 || L == 32) return launch_k<L, 2, 8>(keys, n, s1, s2, out, flags, st, cus); break;
+    case 403: if constexpr (L >= 40) return launch_k<L, 4, 3>(keys, n, s1, s2, out, flags, st, cus); break;
+    case 203: if constexpr (L >= 40) return launch_k<L, 2, 3>(keys, n, s1, s2, out, flags, st, cus); break;
+    default: break;  // a knob pair without an instance: this length's default
   }
+#endif
+  return launch_k<L, dnt, dkpl>(keys, n, s1, s2, out, flags, st, cus);
 }
 
 template <int L, int NT, int U>
 int launch_lanes_v(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t arity, uint64_t* out,
                    uint32_t flags, hipStream_t st, int cus) {
   const uint32_t grid = grid_for(n * arity, cus, NT == 4 ? 1 : 2);
-  // chunk order (knob 24): 0 / 2 wave tickets (the default), 1 static
+  // chunk order (knob 24): 0 / 2 wave tickets (the default), 1 static (and captured launches)
   const int ord = knob(g_tune_order);
   unsigned long long* tk = nullptr;
   if (ord != 1)
@@ -508,7 +506,7 @@ int launch_lanes_v(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t 
   hipLaunchKernelGGL((k_fixed_lanes<L, NT, true, U, LAv, Qv>), dim3(grid), dim3(kBlock), 0, st, keys, n, out, flags, \
                      s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7], s[8], s[9], s[10], s[11], s[12], s[13],   \
                      s[14], s[15], tk)
-  if (ord != 1) {
+  if (tk) {
     if (arity == 2) KVH_LANES_V(2, true); else if (arity == 4) KVH_LANES_V(4, true); else KVH_LANES_V(8, true);
   } else {
     if (arity == 2) KVH_LANES_V(2, false); else if (arity == 4) KVH_LANES_V(4, false); else KVH_LANES_V(8, false);
@@ -524,20 +522,21 @@ int launch_lanes_L(const uint8_t* keys, uint64_t n, const uint64_t* s, uint32_t 
   if constexpr (L == 32) {
     // C3's length: Td0..Td3 in LDS (no rotates, one 16-wave workgroup per CU)
     // -- 118 vs 112 G hash/s for Td0/Td1 with two workgroups per CU
-    // (tools/tune.py, profiles/r02/c3_layout_ab.txt) -- and 4 keys per lane by
-    // default under wave tickets (2.7 % over 2: profiles/r04/s16/ab.jsonl);
-    // knobs 0 / 3 select the others
-    const int nt = knob(g_tune_nt), kpl = knob(g_tune_kpl);
+    // (tools/tune.py, profiles/r02/c3_layout_ab.txt) -- and 4 keys per lane
+    // under wave tickets (2.7 % over 2: profiles/r04/s16/ab.jsonl); the other
+    // pairs in the experiments build (knobs 0 / 3)
     if (a16) {
+#ifdef KVH_EXPERIMENTS
+      const int nt = knob(g_tune_nt), kpl = knob(g_tune_kpl);
       switch ((nt ? nt : 4) * 10 + (kpl ? kpl : 4)) {
-        case 22: break;
         case 21: return launch_lanes_v<L, 2, 1>(keys, n, s, arity, out, flags, st, cus);
         case 24: return launch_lanes_v<L, 2, 4>(keys, n, s, arity, out, flags, st, cus);
         case 41: return launch_lanes_v<L, 4, 1>(keys, n, s, arity, out, flags, st, cus);
         case 42: return launch_lanes_v<L, 4, 2>(keys, n, s, arity, out, flags, st, cus);
-        case 44: return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);
-        default: return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);  // no instance: the default
+        default: break;
       }
+#endif
+      return launch_lanes_v<L, 4, 4>(keys, n, s, arity, out, flags, st, cus);
     }
   }
   const uint32_t grid = grid_for(n * arity, cus, 2);
@@ -592,17 +591,28 @@ int fixed_dispatch(const uint8_t* k, uint32_t key_len, uint64_t n, uint64_t seed
     }
   }
   if (!knob(g_tune_generic) && key_len >= 1 && key_len < 64) {  // any other length below one block
+    // NT4, 4 keys per lane for one 16-byte chunk, 2 above (the experiments
+    // build has the other pairs behind knobs 0 / 3)
+    const int nc = (int)(key_len + 15) / 16;
+#ifdef KVH_EXPERIMENTS
     const int tnt = knob(g_tune_nt), tkpl = knob(g_tune_kpl);
-    const int nc = (int)(key_len + 15) / 16, nt = tnt ? tnt : 4, kpl = tkpl ? tkpl : (nc == 1 ? 4 : 2);
+    const int nt = tnt ? tnt : 4, kpl = tkpl ? tkpl : (nc == 1 ? 4 : 2);
     switch (nc * 1000 + nt * 10 + kpl) {
 #define KVH_RT(NCv, NTv, Uv) \
   case NCv * 1000 + NTv * 10 + Uv: return launch_fixed_rt<NCv, NTv, Uv>(k, n, key_len, seed1, seed2, out, flags, st, cus);
-      KVH_RT(1, 4, 4) KVH_RT(1, 4, 2) KVH_RT(1, 4, 8) KVH_RT(1, 2, 4) KVH_RT(1, 2, 8)
-      KVH_RT(2, 4, 2) KVH_RT(2, 4, 4) KVH_RT(2, 2, 2) KVH_RT(2, 2, 4)
-      KVH_RT(3, 4, 2) KVH_RT(3, 4, 4) KVH_RT(3, 2, 2) KVH_RT(3, 2, 4)
-      KVH_RT(4, 4, 2) KVH_RT(4, 4, 4) KVH_RT(4, 2, 2) KVH_RT(4, 2, 4)
+      KVH_RT(1, 4, 2) KVH_RT(1, 4, 8) KVH_RT(1, 2, 4) KVH_RT(1, 2, 8)
+      KVH_RT(2, 4, 4) KVH_RT(2, 2, 2) KVH_RT(2, 2, 4)
+      KVH_RT(3, 4, 4) KVH_RT(3, 2, 2) KVH_RT(3, 2, 4)
+      KVH_RT(4, 4, 4) KVH_RT(4, 2, 2) KVH_RT(4, 2, 4)
 #undef KVH_RT
-      default: break;  // a knob pair without an instance: the generic kernel
+      default: break;  // a knob pair without an instance: the default
+    }
+#endif
+    switch (nc) {
+      case 1: return launch_fixed_rt<1, 4, 4>(k, n, key_len, seed1, seed2, out, flags, st, cus);
+      case 2: return launch_fixed_rt<2, 4, 2>(k, n, key_len, seed1, seed2, out, flags, st, cus);
+      case 3: return launch_fixed_rt<3, 4, 2>(k, n, key_len, seed1, seed2, out, flags, st, cus);
+      default: return launch_fixed_rt<4, 4, 2>(k, n, key_len, seed1, seed2, out, flags, st, cus);
     }
   }
   uint64_t s[16] = {seed1, seed2};

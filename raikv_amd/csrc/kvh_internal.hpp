@@ -194,8 +194,12 @@ int hip_err(hipError_t e);
 int device_cus(int* cus);
 // hipGetLastError after a launch -> 0 or the recorded error
 int launch_done();
-// the (device, stream)'s ticket counter pair for the in-order streaming kernels (kvh.hip)
+// the (device, stream)'s ticket words for the in-order streaming kernels (kvh.hip, tickets.hpp);
+// *tk = nullptr (and 0 returned) for a stream being captured into a graph: the caller then launches the
+// static-order form of its kernel
 int stream_tickets(hipStream_t st, unsigned long long** tk);
+// kvh_stream_release: synchronise `st` and hand its ticket words back
+int stream_release(hipStream_t st);
 // variable-length CRC32C kernel: 3 = length-sorted windows on 16-copy tables (default), 1 = on 32-copy
 // tables, 0 = lane per key in input order
 // (tuning knobs are atomics: kvh_set_tuning may run concurrently with launches)

@@ -5,7 +5,7 @@
 //   k_var9<NT,NW,KF,PF>   per-wave 256-key windows sorted by 16-byte length
 //                         class, keys read as dwordx4 groups, one
 //                         straight-line variant per chunk (the C2 default)
-//   k_var6<NT,WIN,NW,SH>  the round-2 sorted-window kernel (knob 7 = 13, 7)
+//   k_var6<NT,WIN,NW,SH>  the round-2 sorted-window kernel (knob 7 = 13, 7: experiments build only)
 //   k_generic<VAR,NT>     any length: fixed stride or u64 offsets, one lane per key
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -426,16 +426,28 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       uint64_t s[16] = {seed1, seed2};
       return generic_launch(true, kp, offsets, 0, n, s, 1, out, flags, st, cus);
     }
+    case 46: {  // the default: windows in address order (wave tickets), unless knob 24 = 1 or a captured launch
+      unsigned long long* tk = nullptr;
+      if (knob(g_tune_order) != 1)
+        if (int rc = stream_tickets(st, &tk)) return rc;
+      if (tk) {
+        hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
+                           (uint64_t)n, seed1, seed2, out, flags, tk);
+        return launch_done();
+      }
+    }
+      [[fallthrough]];
+    case 23:  // the static window order
+      hipLaunchKernelGGL((k_var9<2, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
+                         out, flags);
+      return launch_done();
+#ifdef KVH_EXPERIMENTS  // the variants that lost their A/B (rounds 2-4): experiments build only
     case 13:
       hipLaunchKernelGGL((k_var6<2, 256, kBlock / 64, 4>), dim3(grid), dim3(kBlock), 0, st, kp, offsets,
                          (uint64_t)n, seed1, seed2, out, flags);
       return launch_done();
     case 7:
       hipLaunchKernelGGL((k_var6<2, 256>), dim3(grid), dim3(kBlock), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
-                         out, flags);
-      return launch_done();
-    case 23:
-      hipLaunchKernelGGL((k_var9<2, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
       return launch_done();
     case 24:
@@ -446,19 +458,13 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       hipLaunchKernelGGL((k_var9<2, 12, 192, true>), dim3(grid), dim3(768), 0, st, kp, offsets, (uint64_t)n, seed1,
                          seed2, out, flags);
       return launch_done();
-    case 46: {  // round-4 A/B: windows in address order (wave tickets)
-      unsigned long long* tk = nullptr;
-      if (int rc = stream_tickets(st, &tk)) return rc;
-      hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
-                         (uint64_t)n, seed1, seed2, out, flags, tk);
-      return launch_done();
-    }
     case 47:    // round-4 A/B: 46 with four tables at 16 copies (LdsTab<5>)
     case 48:    // round-4 A/B: 46 with 12 waves per workgroup
     case 49:    // round-4 A/B: 46 with the next block's groups in flight
     case 50: {  // round-4 A/B: 25 (12 waves, next block's groups in flight) in address order
       unsigned long long* tk = nullptr;
       if (int rc = stream_tickets(st, &tk)) return rc;
+      if (!tk) return set_err(KVH_EINVAL);
       if (var == 47)
         hipLaunchKernelGGL((k_var9<5, 16, 256, false, true, false, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
                            (uint64_t)n, seed1, seed2, out, flags, tk);
@@ -481,6 +487,7 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       hipLaunchKernelGGL((k_var9<5, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);
       return launch_done();
+#endif
     default:
       break;
   }

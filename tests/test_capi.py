@@ -50,11 +50,21 @@ def test_product_library_exports_only_the_header():
     import raikv_amd
     lib = raikv_amd.lib
     for knob, val in ((5, 1), (5, 2), (5, 3), (6, 2), (9, 1), (10, 1), (11, 200), (12, 4), (13, 2), (7, 2),
-                      (7, 3), (7, 6), (7, 9), (7, 12), (7, 40), (7, 41), (7, 42), (7, 43), (18, 3), (18, 4), (22, 2)):
+                      (7, 3), (7, 6), (7, 9), (7, 12), (7, 40), (7, 41), (7, 42), (7, 43), (18, 3), (18, 4), (22, 2),
+                      (26, -1), (26, 1 << 16)):
         assert lib.kvh_set_tuning(knob, val) == -22, (knob, val)
+    # the variants that lost their A/B compile only into the experiments build
+    # (VERDICT r4 item 7): tables per LDS and keys per lane other than the
+    # per-length defaults, knob 7 = 7, 13, 24, 25, 44, 45, 47-50, knob 14 =
+    # 1-5, knob 23 = 1, 2, knob 24 = 3-5
+    for knob, vals in ((0, (2, 4)), (3, (1, 2, 3, 4, 8)), (7, (7, 13, 24, 25, 44, 45, 47, 48, 49, 50)),
+                       (14, (1, 2, 3, 4, 5)), (23, (1, 2)), (24, (3, 4, 5))):
+        for val in vals:
+            assert lib.kvh_set_tuning(knob, val) == -22, (knob, val)
     # product knobs still switch (and return the previous value)
-    prev = lib.kvh_set_tuning(7, 7)
-    assert prev == 46 and lib.kvh_set_tuning(7, prev) == 7
+    for knob, val, dflt in ((7, 23, 46), (7, 0, 46), (14, 0, 6), (23, 0, 3), (24, 1, 0), (24, 2, 0), (26, 6, 0)):
+        prev = lib.kvh_set_tuning(knob, val)
+        assert prev == dflt and lib.kvh_set_tuning(knob, prev) == val, (knob, val)
 
 
 def test_cpp_host_mirror_compiles():
@@ -69,7 +79,7 @@ def test_cpp_host_mirror_compiles():
 
 
 def test_kv_compat_library_exports_the_meow_family():
-    """libkvh_kv.so (link compatibility with include/raikv/key_hash.h:59-130)
+    """libkvh_kv.so (link compatibility with include/raikv/key_hash.h:8-20 and :59-130)
     exports exactly the kv_* names include/kvh_kv.h declares, and links
     libkvh.so (it hashes on the GPU through the C-ABI)."""
     lib = os.path.join(ROOT, "raikv_amd", "libkvh_kv.so")
@@ -78,6 +88,19 @@ def test_kv_compat_library_exports_the_meow_family():
     want = set(re.findall(r"\b(kv_[a-z0-9_]+)\s*\(", src))
     out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
     got = set(l.split()[-1] for l in out.splitlines() if " T " in l)
-    assert got == want and len(want) == 15, sorted(got ^ want)
+    assert got == want and len(want) == 22, sorted(got ^ want)
     deps = subprocess.run(["ldd", lib], capture_output=True, text=True).stdout
     assert "libkvh.so" in deps
+
+
+def test_kv_compat_c_program_needs_only_libkvh_kv():
+    """The C test program of the CRC32C family (tests/cpp/kv_compat_crc.c)
+    names only libkvh_kv.so among the engine's libraries: a raikv build that
+    drops src/key_hash.c links exactly that."""
+    exe = os.path.join(ROOT, "tests", "cpp", "kv_compat_crc")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "tests/cpp/kv_compat_crc"], check=True)
+    dyn = subprocess.run(["readelf", "-d", exe], capture_output=True, text=True, check=True).stdout
+    needed = [l.split("[")[1].rstrip("]") for l in dyn.splitlines() if "(NEEDED)" in l]
+    assert "libkvh_kv.so" in needed and "libkvh.so" not in needed and not any("amdhip" in x for x in needed), needed
+

@@ -4,6 +4,7 @@ kvh_crc_c_var and the host drop-ins vs the reference's own outputs
 """
 import ctypes as C
 import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -11,7 +12,7 @@ import pytest
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-from oracle_lib import GOLDEN, load_oracle, orc_crc_fixed, orc_crc_var  # noqa: E402
+from oracle_lib import GOLDEN, ROOT, load_oracle, orc_crc_fixed, orc_crc_var  # noqa: E402
 
 G = np.load(os.path.join(GOLDEN, "crc32c.npz"))
 ORC = load_oracle()
@@ -131,7 +132,7 @@ def test_full_size_var_property(kvh):
     assert c == s
 
 
-@pytest.mark.parametrize("kernel", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("kernel", [0, 6])
 @pytest.mark.parametrize("n", [1, 255, 257, 2561])
 def test_var_kernels_vs_oracle(kvh, kernel, n):
     """Both variable-length kernels (input order; length-sorted windows, knob
@@ -153,3 +154,35 @@ def test_var_kernels_vs_oracle(kvh, kernel, n):
         np.testing.assert_array_equal(got, orc_crc_var(ORC, flat, offs, seeds))
     finally:
         kvh.lib.kvh_set_tuning(14, prev)
+
+
+def test_kv_compat_c_program_links_only_libkvh_kv(kvh, tmp_path):
+    """a C program that includes only include/kvh_kv.h and
+    links only libkvh_kv.so calls every CRC32C symbol of
+    include/raikv/key_hash.h:8-20 (kv_crc_c over every length 0..300 under
+    three seeds, kv_crc_c_array / _2_diff / _4_diff over 3000 variable-length
+    keys with per-key seeds, kv_crc_c_key_array over prefixes, kv_hash_uint /
+    kv_hash_uint2) against the reference's own outputs (crc32c.npz)."""
+    import struct
+    exe = os.path.join(ROOT, "tests", "cpp", "kv_compat_crc")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "tests/cpp/kv_compat_crc"], check=True)
+    lk, ls, lo = G["len_keys"], G["len_seeds"], G["len_out"]
+    parts = [struct.pack("<III", lk.shape[0], lk.shape[1], ls.shape[0]), lk.astype(np.uint8).tobytes(),
+             ls.astype("<u4").tobytes(), lo.astype("<u4").tobytes()]
+    vo, vk = G["var_offsets"].astype("<u8"), G["var_keys"].astype(np.uint8)
+    parts += [struct.pack("<I", len(vo) - 1), vo.tobytes(), G["var_seeds"].astype("<u4").tobytes(),
+              G["var_out"].astype("<u4").tobytes(), struct.pack("<Q", vk.size), vk.tobytes()]
+    pb = G["prefix_buf"].astype(np.uint8)
+    parts += [struct.pack("<II", len(G["prefix_lens"]), pb.size), pb.tobytes(),
+              G["prefix_lens"].astype("<u4").tobytes(), G["prefix_seeds"].astype("<u4").tobytes(),
+              G["prefix_out"].astype("<u4").tobytes()]
+    parts += [struct.pack("<I", len(G["uint_in"])), G["uint_in"].astype("<u4").tobytes(),
+              G["uint_out"].astype("<u4").tobytes(), G["uint2_out"].astype("<u4").tobytes()]
+    f = tmp_path / "crc_cases.bin"
+    f.write_bytes(b"".join(parts))
+    r = subprocess.run([exe, str(f)], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "bad 0" in r.stdout
+

@@ -206,7 +206,7 @@ def test_var_windows_spanning_4gib(kvh):
     doff = dev_u64(offs)
     sd = torch.tensor(np.array(STATIC, dtype=np.uint64).view(np.int64), device="cuda").repeat(n, 1)
     lit = kvh.meow128_var_seeded(keys, doff, sd)
-    for variant in (13, 7, 0, 23):
+    for variant in (46, 0, 23):
         prev = kvh.lib.kvh_set_tuning(7, variant)
         try:
             got = kvh.meow128_var(keys, doff, STATIC)
@@ -231,13 +231,13 @@ def test_crc_windows_spanning_4gib(kvh):
     keys = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device="cuda", generator=g)
     doff = dev_u64(offs)
     res = {}
-    for variant in (0, 1, 2, 3, 4, 5, 6):
+    for variant in (0, 6):
         prev = kvh.lib.kvh_set_tuning(14, variant)
         try:
             res[variant] = kvh.crc_c_var(keys, doff, 0x1234)
         finally:
             kvh.lib.kvh_set_tuning(14, prev)
-    for v in (1, 2, 3, 4, 5, 6):
+    for v in (6,):
         assert torch.equal(res[v], res[0]), f"crc variant {v}"
     c = res[0].cpu().numpy().view(np.uint32)
     for i in list(range(0, 10, 3)) + [10, 250, 309] + list(range(310, n, 97)):

@@ -80,7 +80,6 @@ def test_var_host_pipeline(kvh, mib, slots):
         np.testing.assert_array_equal(ho, dev_hash_var(kvh, keys, offs, STATIC, fixup=True))
         # a caller's own buffer page-locked in place (raikv's shm segment)
         reg = np.empty(keys.size + 4096, dtype=np.uint8)
-        _REGISTERED_KEEP.append(reg)
         view = reg[:keys.size]
         view[:] = keys
         assert kvh.lib.kvh_host_register(view.ctypes.data, view.nbytes) == 0
@@ -136,15 +135,6 @@ def test_multi_device_rejects_bad_device_lists(kvh):
     assert kvh.lib.kvh_meow128_fixed_host_multi(kb.ctypes.data, 16, 100, 0, 0, out.ctypes.data, 0, neg, 1) == -22
 
 
-# Host buffers that were registered with the runtime (kvh_host_register) are
-# kept alive for the whole process, never returned to the allocator: a later
-# numpy array mmapped at the same address then cannot meet a stale runtime
-# mapping of the old pages in its own pageable H2D copy (two GPU sessions of
-# round 4 saw an illegal address in such a copy in a later test file after
-# these tests).
-_REGISTERED_KEEP = []
-
-
 def test_partially_registered_buffers_take_the_bounce_path(kvh):
     """a buffer page-locked only in part (its first pages
     registered, the rest pageable) must not be DMA'd past the registered
@@ -165,7 +155,6 @@ def test_partially_registered_buffers_take_the_bounce_path(kvh):
     out_raw = np.empty(n * 16 + 2 * page, dtype=np.uint8)
     ostart = (-out_raw.ctypes.data) % page
     out = out_raw[ostart:ostart + n * 16].view(np.uint64).reshape(n, 2)
-    _REGISTERED_KEEP.extend([bufs["keys"][0], bufs["offs"][0], out_raw])
     regs = [bufs["keys"][1], bufs["offs"][1], out]
     for r in regs:  # the first 2 pages only
         assert kvh.lib.kvh_host_register(r.ctypes.data, 2 * page) == 0
@@ -201,7 +190,6 @@ def test_two_registrations_with_a_pageable_gap_bounce(kvh):
     out_raw = np.empty(n * 16 + 4 * page, dtype=np.uint8)
     ostart = (-out_raw.ctypes.data) % page
     out = out_raw[ostart:ostart + n * 16].view(np.uint64).reshape(n, 2)
-    _REGISTERED_KEEP.extend([raw, out_raw])
     regs = []
     for a in (kv, out.reshape(-1).view(np.uint8)):
         base = a.ctypes.data

@@ -34,19 +34,18 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
 
 
-ENGINES = [(0, 0, 0), (0, 0, 1), (0, 0, 2), (0, 0, 3), (0, 2, None), (0, 1, None), (33, 0, None)]
-ENGINE_IDS = ["bucketed2", "bucketed2_sortr", "bucketed2_sortr2", "bucketed2_half", "bucketed1", "radix_u32",
-              "radix_u64"]
+ENGINES = [(0, 0, 0), (0, 0, 3), (0, 2, None), (0, 1, None), (33, 0, None)]
+ENGINE_IDS = ["bucketed2", "bucketed2_half", "bucketed1", "radix_u32", "radix_u64"]
 
 
 class _engine:
     """knob 20 = 0 two-pass bucketed (the default), 2 one-pass bucketed, 1
     radix; knob 17 = 33 forces the radix engine on u64 keys over slot + 33 h1
     bits (0: u32 keys when the prefix fits 31 bits); knob 23 picks the
-    two-pass path's bucket sort (0 k_bk_sort, 1 the register-resident
-    k_bk_sortr, 2 k_bk_sortr2, 3 -- the default -- half-size buckets: up to
-    15 bucket bits, the second pass on 8-bit digits, k_bk_sortr at two
-    512-thread workgroups per CU)."""
+    two-pass path's bucket sort (0 k_bk_sort, 3 -- the default -- half-size
+    buckets: up to 15 bucket bits, the second pass on 8-bit digits, the
+    register-resident k_bk_sortr at two 512-thread workgroups per CU; 1 / 2
+    only in the experiments build)."""
 
     def __init__(self, kvh, sort_bits, engine, b3=None):
         self.kvh, self.v, self.b3 = kvh, (sort_bits, engine), b3
@@ -191,15 +190,15 @@ def test_engines_agree(kvh, n, map_size):
         res["cap"] = (oh.clone(), oi.clone(), int(srt.dups.item()))
     finally:
         kvh.lib.kvh_set_tuning(22, prev)
-    # the other bucket sorts (knob 23 = 0, 1, 2; 3 is the default above)
-    for b3 in (0, 1, 2):
+    # the other bucket sort of the product (knob 23 = 0; 3 is the default above)
+    for b3 in (0,):
         prev = kvh.lib.kvh_set_tuning(23, b3)
         try:
             oh, oi = srt.sort(h, items=items, dedup=True)
             res[f"sortr{b3}"] = (oh.clone(), oi.clone(), int(srt.dups.item()))
         finally:
             kvh.lib.kvh_set_tuning(23, prev)
-    for e in (2, 1, "cap", "sortr0", "sortr1", "sortr2"):
+    for e in (2, 1, "cap", "sortr0"):
         assert torch.equal(res[0][0], res[e][0]) and torch.equal(res[0][1], res[e][1]) and res[0][2] == res[e][2], e
     if n <= 65537:
         og = orc_geom(ORC, map_size, 64, 1.0, 4, 4)
@@ -342,8 +341,8 @@ def test_full_size_properties(kvh):
     uniq = torch.unique(h, dim=0).shape[0]
     _, _ = srt.sort(h, dedup=True)
     assert int(srt.dups.item()) == n - uniq
-    # knob 23 = 1 at this size (the default 3 runs 15 bucket bits with an 8-bit second pass): word for word
-    prev = kvh.lib.kvh_set_tuning(23, 1)
+    # knob 23 = 0 at this size (the default 3 runs 15 bucket bits with an 8-bit second pass): word for word
+    prev = kvh.lib.kvh_set_tuning(23, 0)
     try:
         oh3, oi3 = srt.sort(h, dedup=False)
         assert torch.equal(oh3, oh) and torch.equal(oi3, oi)
