@@ -6,7 +6,8 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wno-pass-failed
 INC      := -Iinclude
 
 LIB      := raikv_amd/libkvh.so
-SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/kvh_fixed.hip raikv_amd/csrc/kvh_varlen.hip raikv_amd/csrc/ht_pos.hip raikv_amd/csrc/crc32c.hip raikv_amd/csrc/ingest.hip raikv_amd/csrc/ht_sort.hip
+SRCS     := raikv_amd/csrc/kvh.hip raikv_amd/csrc/kvh_fixed.hip raikv_amd/csrc/kvh_varlen.hip raikv_amd/csrc/ht_pos.hip raikv_amd/csrc/crc32c.hip raikv_amd/csrc/ingest.hip raikv_amd/csrc/ht_sort.hip \
+            raikv_amd/csrc/ht_refsort.hip
 OBJS     := $(SRCS:.hip=.o)
 HDRS     := raikv_amd/csrc/meow_dev.hpp raikv_amd/csrc/aes_tables.hpp raikv_amd/csrc/kvh_internal.hpp \
             raikv_amd/csrc/ht_pos.hpp raikv_amd/csrc/bs_prelude.hpp raikv_amd/csrc/bs_aes.hpp \

@@ -309,6 +309,7 @@ int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
  * sort_*.npz).  Not a bit-identical drop-in for kv_ht_radix_sort.
  * ------------------------------------------------------------------- */
 #define KVH_DEDUP     0x8u  /* zero h1 of an element equal (h1,h2) to its successor, count it */
+#define KVH_REF_ORDER 0x10u /* kvh_ht_sort: the reference's exact element order, n <= 65536 */
 
 /* layout of kv_ht_sort_t (include/raikv/radix_sort.h:8-11) */
 typedef struct {

@@ -18,6 +18,8 @@ from .binding import (  # noqa: F401
     frags_hash,
     HtSorter,
     KVH_DEDUP,
+    KVH_REF_ORDER,
+    set_poison_outputs,
     meow128_spans,
     meow128_frags,
     KVH_NULTERM,
@@ -49,5 +51,5 @@ __all__ = [
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "meow128_var_host", "meow128_host_multi", "shard_bounds", "host_empty", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
     "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
-    "tokenize", "tokenize_hash", "frag_offsets", "frags_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP",
+    "tokenize", "tokenize_hash", "frag_offsets", "frags_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "KVH_DEDUP", "KVH_REF_ORDER", "set_poison_outputs",
 ]

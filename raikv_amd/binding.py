@@ -23,6 +23,7 @@ KVH_FIXUP = 0x1
 KVH_POS32 = 0x2
 KVH_NULTERM = 0x4
 KVH_DEDUP = 0x8
+KVH_REF_ORDER = 0x10
 KVH_MAX_ARITY = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -136,6 +137,7 @@ def _load():
         "kvh_version": (C.c_char_p, []),
         "kvh_device_synchronize": (I, []),
         "kvh_set_tuning": (I, [I, I]),
+        "kvh_stream_release": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -288,7 +290,11 @@ class HtSorter:
         self.scratch = torch.empty((nb + 7) // 8, dtype=torch.int64, device=device)
         self.dups = torch.zeros((1,), dtype=torch.int64, device=device)
 
-    def sort(self, hashes, items=None, dedup: bool = False, out=None, items_out=None, stream=None):
+    def sort(self, hashes, items=None, dedup: bool = False, out=None, items_out=None, stream=None,
+             ref_order: bool = False):
+        """ref_order: the reference's exact element order (KVH_REF_ORDER,
+        kv_ht_radix_sort step for step; n <= 65536); else the engine's total
+        order (the same slot order, ties by (h1 << 1, h1, h2))."""
         n = hashes.numel() // 2
         if n > self.cap:
             raise KvhError(f"batch {n} > sorter capacity {self.cap}")
@@ -298,7 +304,8 @@ class HtSorter:
             items_out = _empty((n,), torch.int64, hashes.device)
         check(lib.kvh_ht_sort(_dev_ptr(hashes) if n else None, _dev_ptr(items) if items is not None else None, n,
                               C.byref(self.geom), _dev_ptr(out) if n else None, _dev_ptr(items_out) if n else None,
-                              _dev_ptr(self.dups), KVH_DEDUP if dedup else 0, _dev_ptr(self.scratch),
+                              _dev_ptr(self.dups), (KVH_DEDUP if dedup else 0) | (KVH_REF_ORDER if ref_order else 0),
+                              _dev_ptr(self.scratch),
                               self.scratch.numel() * 8, _stream_ptr(stream)), "kvh_ht_sort")
         return out, items_out
 

@@ -1618,6 +1618,8 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   }
   if (n == 0) return set_err(0);
   if (n >= (1ull << 32) || !hashes || !h_out || !scratch) return set_err(KVH_EINVAL);
+  if (flags & KVH_REF_ORDER)  // the reference's exact element order, n <= 64K (ht_refsort.hip)
+    return refsort_launch(hashes, items, n, geom, h_out, items_out, dup_count, dedup, scratch, scratch_bytes, st);
   SortLayout L;
   int rc = sort_layout(n, &L);
   if (rc) return rc;
@@ -1880,7 +1882,7 @@ extern "C" {
 size_t kvh_ht_sort_scratch_bytes(size_t n) {
   SortLayout L;
   if (sort_layout(n, &L) != 0) return 0;
-  return L.total;
+  return n <= 65536 ? std::max(L.total, refsort_scratch_bytes(n)) : L.total;  // either order
 }
 
 int kvh_ht_sort(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh_ht_geom_t* geom,
@@ -1912,8 +1914,9 @@ int kvh_ht_radix_sort(kvh_ht_sort_t* ar, uint32_t ar_size, const kvh_ht_geom_t* 
   do {
     if ((e = hipMemcpy(d + off_h, hv.data(), 16 * n, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_err(e); break; }
     if ((e = hipMemcpy(d + off_i, iv.data(), 8 * n, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_err(e); break; }
+    // up to 64K elements (ctest's batches) in the reference's exact order
     rc = sort_impl((const uint64_t*)(d + off_h), (const uint64_t*)(d + off_i), n, geom, (uint64_t*)(d + off_ho),
-                   (uint64_t*)(d + off_io), nullptr, 0, d + off_s, sb, (hipStream_t)0);
+                   (uint64_t*)(d + off_io), nullptr, n <= 65536 ? KVH_REF_ORDER : 0u, d + off_s, sb, (hipStream_t)0);
     if (rc) break;
     if ((e = hipMemcpy(hv.data(), d + off_ho, 16 * n, hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_err(e); break; }
     if ((e = hipMemcpy(iv.data(), d + off_io, 8 * n, hipMemcpyDeviceToHost)) != hipSuccess) { rc = hip_err(e); break; }

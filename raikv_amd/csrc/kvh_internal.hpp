@@ -7,6 +7,7 @@
 #include <stdint.h>
 #include <atomic>
 #include "meow_dev.hpp"
+#include "../../include/kvh.h"
 
 namespace kvh {
 
@@ -200,6 +201,11 @@ int launch_done();
 int stream_tickets(hipStream_t st, unsigned long long** tk);
 // kvh_stream_release: synchronise `st` and hand its ticket words back
 int stream_release(hipStream_t st);
+// kv_ht_radix_sort's exact order on the device, n <= 64K (ht_refsort.hip)
+size_t refsort_scratch_bytes(size_t n);
+int refsort_launch(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh_ht_geom_t* geom,
+                   uint64_t* h_out, uint64_t* items_out, uint64_t* dup_count, bool dedup, void* scratch,
+                   size_t scratch_bytes, hipStream_t st);
 // variable-length CRC32C kernel: 3 = length-sorted windows on 16-copy tables (default), 1 = on 32-copy
 // tables, 0 = lane per key in input order
 // (tuning knobs are atomics: kvh_set_tuning may run concurrently with launches)

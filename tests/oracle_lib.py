@@ -139,7 +139,48 @@ def load_ref_ht():
     lib.ref_cuckoo_bench.restype = C.c_double
     lib.ref_ht_sort_bench.argtypes = [U64, U64, U64, C.c_uint32, P, SZ, P]
     lib.ref_ht_sort_bench.restype = C.c_double
+    lib.ref_ht_sort.argtypes = [U64, C.c_uint32, C.c_float, C.c_uint16, C.c_uint8, P, SZ, P, P, P]
+    lib.ref_ht_sort.restype = C.c_int
     return lib
+
+
+def ref_ht_sort(lib, map_size, hashes):
+    """The compiled reference's kv_ht_radix_sort + ctest marking
+    (oracle/ref_cuckoo.cpp ref_ht_sort) on a 64-byte-entry 4x4 table of
+    map_size bytes -> (hashes, items, dup_count)."""
+    h = np.ascontiguousarray(hashes, dtype=np.uint64).reshape(-1, 2)
+    n = len(h)
+    oh = np.zeros((n, 2), np.uint64)
+    oi = np.zeros(n, np.uint64)
+    d = np.zeros(1, np.uint64)
+    assert lib.ref_ht_sort(map_size, 64, 1.0, 4, 4, h.ctypes.data, n, oh.ctypes.data, oi.ctypes.data,
+                           d.ctypes.data) == 0
+    return oh, oi, int(d[0])
+
+
+def ref_order_cases(seed=0):
+    """Inputs for the exact-order sort (KVH_REF_ORDER): table geometries whose
+    slot bit counts (1 + floor(log2 ht_size): 10, 17, 20, 25, 26) reach every
+    step of RadixSort::sort -- 8-bit passes, 2-5-bit last passes, the 1-bit
+    Hoare pass (17, 25) -- and batches with duplicates, a hot slot (one node
+    of equal slots, re-pushed down to no bits), slots clustered in one
+    top-level bucket, and sizes around the 32-element tail and 2048-element
+    wave thresholds."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for ms in (497152, 5 << 20, 64 << 20, 1200 << 20, 4 << 30):
+        for n in (2, 3, 4, 5, 31, 32, 33, 100, 2048, 2049, 5000, 16384):
+            h = rng.integers(0, 2**64, (n, 2), dtype=np.uint64)
+            kind = rng.integers(0, 4)
+            if kind == 1 and n > 8:  # exact duplicates
+                src = rng.integers(0, n, n // 8)
+                h[rng.integers(0, n, n // 8)] = h[src]
+            elif kind == 2 and n > 8:  # a hot h1 (one slot), distinct h2
+                h[rng.integers(0, n, n // 3), 0] = h[0, 0]
+            elif kind == 3:  # h1 clustered: few distinct high slot bits
+                h[:, 0] = (h[:, 0] & np.uint64(0xffff)) | (h[0, 0] & ~np.uint64(0xffff))
+            out.append((ms, h))
+    return out
 
 
 # ------------------------------------------------------------ CRC32C (§8 f4)
@@ -237,6 +278,24 @@ def np_ht_sort(geom, hashes: np.ndarray, items=None, dedup=False):
         oh[:-1, 0][eq] = 0
         dups = int(eq.sum())
     return oh, oi, dups
+
+
+def orc_ht_radix_sort_ref(lib, geom, hashes: np.ndarray, items=None, dedup=False):
+    """oracle/sort_oracle.c: kv_ht_radix_sort's exact element order
+    (radix_sort.h:89-298 via radix_sort.cpp:31-41) + ctest.c:96-104's marking.
+    Returns (hashes, items, dup_count)."""
+    lib.orc_ht_radix_sort_ref.argtypes = [C.POINTER(OrcGeom), P, C.c_uint32]
+    lib.orc_ht_radix_sort_ref.restype = None
+    lib.orc_ht_mark_dups.argtypes = [P, C.c_uint32]
+    lib.orc_ht_mark_dups.restype = U64
+    h = np.ascontiguousarray(hashes, dtype=np.uint64).reshape(-1, 2)
+    n = len(h)
+    el = np.empty((n, 3), dtype=np.uint64)
+    el[:, :2] = h
+    el[:, 2] = np.arange(n, dtype=np.uint64) if items is None else np.asarray(items, dtype=np.uint64)
+    lib.orc_ht_radix_sort_ref(C.byref(geom), el.ctypes.data, n)
+    d = int(lib.orc_ht_mark_dups(el.ctypes.data, n)) if dedup else 0
+    return el[:, :2].copy(), el[:, 2].copy(), d
 
 
 def sort_fixtures():

@@ -11,7 +11,8 @@ import pytest
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-from oracle_lib import load_oracle, np_ht_mod, np_ht_sort, orc_geom, sort_fixtures  # noqa: E402
+from oracle_lib import (load_oracle, np_ht_mod, np_ht_sort, orc_geom, orc_ht_radix_sort_ref,  # noqa: E402
+                        ref_order_cases, sort_fixtures)
 
 FIX = sort_fixtures()
 ORC = load_oracle()
@@ -88,19 +89,100 @@ def _sort_golden(kvh, f):
     np.testing.assert_array_equal(host(oi), np_ht_sort(og, h, items=items)[1])
 
 
-def test_radix_sort_drop_in(kvh):
+class SortT(C.Structure):  # kv_ht_sort_t (radix_sort.h:8-11)
+    _fields_ = [("key", C.c_uint64), ("key2", C.c_uint64), ("item", C.c_void_p)]
+
+
+@pytest.mark.parametrize("f", FIX, ids=[f["name"] for f in FIX])
+def test_radix_sort_drop_in_is_the_reference_order(kvh, f):
+    """kvh_ht_radix_sort (the kv_ht_radix_sort drop-in, radix_sort.h:19-20)
+    sorts a kv_ht_sort_t array in place in the reference's EXACT order for
+    batches of <= 64K (ctest's): the fixture's element order word for word,
+    items (pointers) carried."""
+    g = kvh.HtGeom.from_map(f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    h = f["hashes"]
+    ar = (SortT * len(h))(*[SortT(int(a), int(b), i + 1) for i, (a, b) in enumerate(h)])
+    assert kvh.lib.kvh_ht_radix_sort(ar, len(h), C.byref(g)) == 0
+    got = np.array([x.item for x in ar], dtype=np.uint64) - np.uint64(1)
+    np.testing.assert_array_equal(got, f["out_items"])
+    keys = np.array([[x.key, x.key2] for x in ar], dtype=np.uint64)
+    np.testing.assert_array_equal(keys, h[f["out_items"].astype(np.int64)])
+
+
+def test_radix_sort_drop_in_above_64k(kvh):
+    """Above 64K elements the drop-in takes the engine's total order (same
+    slot order; ties by (h1 << 1, h1, h2))."""
     f = FIX[0]
     g = kvh.HtGeom.from_map(f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
     og = orc_geom(ORC, f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
-    h = f["hashes"][:3000]
-
-    class SortT(C.Structure):
-        _fields_ = [("key", C.c_uint64), ("key2", C.c_uint64), ("item", C.c_void_p)]
-    ar = (SortT * len(h))(*[SortT(int(a), int(b), i + 1) for i, (a, b) in enumerate(h)])
+    rng = np.random.default_rng(3)
+    h = rng.integers(0, 2 ** 64, size=(65537, 2), dtype=np.uint64)
+    ar = (SortT * len(h))()
+    arr = np.frombuffer(ar, dtype=np.uint64).reshape(-1, 3)
+    arr[:, :2] = h
+    arr[:, 2] = np.arange(1, len(h) + 1, dtype=np.uint64)
     assert kvh.lib.kvh_ht_radix_sort(ar, len(h), C.byref(g)) == 0
     wh, wi, _ = np_ht_sort(og, h, items=np.arange(1, len(h) + 1, dtype=np.uint64))
-    np.testing.assert_array_equal(np.array([[x.key, x.key2] for x in ar], dtype=np.uint64), wh)
-    np.testing.assert_array_equal(np.array([x.item for x in ar], dtype=np.uint64), wi)
+    np.testing.assert_array_equal(arr[:, :2], wh)
+    np.testing.assert_array_equal(arr[:, 2], wi)
+
+
+@pytest.mark.parametrize("f", FIX, ids=[f["name"] for f in FIX])
+def test_ref_order_fixtures_word_for_word(kvh, f):
+    """kvh_ht_sort with KVH_REF_ORDER reproduces the
+    reference's kv_ht_radix_sort + ctest marking on its own fixtures word for
+    word: element order (ties included), zeroed duplicates, and the count
+    (99 on the 600-slot table, 992 and 1000 on the others)."""
+    g = kvh.HtGeom.from_map(f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    h = f["hashes"]
+    srt = kvh.HtSorter(g, len(h))
+    oh, oi = srt.sort(dev(h), dedup=True, ref_order=True)
+    np.testing.assert_array_equal(host(oi), f["out_items"])
+    np.testing.assert_array_equal(host(oh), f["out_hashes"])
+    assert int(srt.dups.item()) == f["dups"]
+    # a 16K slice (ctest's batch, ctest.c:34) against the pinned restatement
+    og = orc_geom(ORC, f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    part = h[:16384]
+    oh, oi = srt.sort(dev(part), dedup=True, ref_order=True)
+    wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, part, dedup=True)
+    np.testing.assert_array_equal(host(oi), wi)
+    np.testing.assert_array_equal(host(oh), wh)
+    assert int(srt.dups.item()) == wd
+
+
+def test_ref_order_every_step_vs_oracle(kvh):
+    """KVH_REF_ORDER against the pinned restatement (oracle/sort_oracle.c) on
+    batches that reach every step of RadixSort::sort: 8-bit and short last
+    passes, the 1-bit pass (17- and 25-bit slot counts), tails of 2-31,
+    nodes around the 2048-element wave threshold, duplicates, a hot slot,
+    clustered slots; plus 65536 elements, items carried."""
+    cases = ref_order_cases(seed=7)
+    rng = np.random.default_rng(8)
+    cases.append((64 << 20, rng.integers(0, 2 ** 64, size=(65536, 2), dtype=np.uint64)))
+    sorters = {}
+    for ms, h in cases:
+        if ms not in sorters:
+            sorters[ms] = (kvh.HtSorter(kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4), 65536),
+                           orc_geom(ORC, ms, 64, 1.0, 4, 4))
+        srt, og = sorters[ms]
+        items = rng.integers(0, 2 ** 63, len(h), dtype=np.uint64)
+        oh, oi = srt.sort(dev(h), items=dev(items), dedup=True, ref_order=True)
+        wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, h, items=items, dedup=True)
+        np.testing.assert_array_equal(host(oi), wi, err_msg=f"map {ms} n {len(h)}")
+        np.testing.assert_array_equal(host(oh), wh, err_msg=f"map {ms} n {len(h)}")
+        assert int(srt.dups.item()) == wd
+
+
+def test_ref_order_bounds(kvh):
+    g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
+    srt = kvh.HtSorter(g, 65537)
+    h = dev(np.ones((65537, 2), dtype=np.uint64))
+    with pytest.raises(kvh.KvhError):
+        srt.sort(h, ref_order=True)
+    # 0 and 1 elements: nothing to order
+    for n in (0, 1):
+        oh, oi = srt.sort(dev(np.full((n, 2), 5, dtype=np.uint64)), dedup=True, ref_order=True)
+        assert oh.shape[0] == n and int(srt.dups.item()) == 0
 
 
 def test_edges(kvh):

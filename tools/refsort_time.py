@@ -1,0 +1,45 @@
+"""Timing of the exact-order sort (KVH_REF_ORDER, ht_refsort.hip) at ctest's
+batch sizes, beside the reference's own kv_ht_radix_sort on one host core
+(oracle/_ref ref_ht_sort_bench, the checker library; 64 GiB-map geometry as
+bench.py's f2).  One JSON line per batch size: device ms per call (HIP events
+around 50 calls on the current stream), the reference's ms per call, and the
+default (total-order) engine's ms for comparison."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import raikv_amd as kvh  # noqa: E402
+from oracle_lib import load_ref_ht  # noqa: E402  (checker / CPU baseline only)
+
+ref = load_ref_ht()
+geom = kvh.HtGeom.from_map(map_size=64 << 30, hash_entry_size=64, hash_value_ratio=1.0, cuckoo_buckets=4,
+                           cuckoo_arity=4)
+rng = np.random.default_rng(1)
+for n in (1024, 4096, 16384, 65536):
+    h = rng.integers(0, 2 ** 64, size=(n, 2), dtype=np.uint64)
+    dh = torch.from_numpy(h.view(np.int64)).cuda()
+    srt = kvh.HtSorter(geom, n)
+    res = {"n": n}
+    for name, ro in (("ref_order", True), ("total_order", False)):
+        for _ in range(5):
+            srt.sort(dh, dedup=True, ref_order=ro)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(50):
+            srt.sort(dh, dedup=True, ref_order=ro)
+        b.record()
+        torch.cuda.synchronize()
+        res[f"{name}_ms"] = a.elapsed_time(b) / 50
+    if ref is not None:
+        d = np.zeros(1, np.uint64)
+        ts = [ref.ref_ht_sort_bench(geom.ht_size, geom.ht_mod_mask, geom.ht_mod_fraction, geom.ht_mod_shift,
+                                    h.ctypes.data, n, d.ctypes.data) for _ in range(20)]
+        res["reference_cpu_ms_1core"] = float(np.median(ts)) * 1e3
+    print(json.dumps(res), flush=True)
