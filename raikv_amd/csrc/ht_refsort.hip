@@ -54,21 +54,32 @@ struct WaveArea {
   uint8_t li[32];
 };
 
+constexpr uint32_t kFinLds = 32768;  // workgroup nodes up to this size keep fin[] in LDS
+
 struct RefSmem {
   union {
-    uint8_t bdig[kRefMax];  // digits of a workgroup node
-    WaveArea w[kRW];        // per-wave slices (the two phases of a round never overlap)
+    struct {
+      uint8_t bdig[kRefMax];   // digits of a workgroup node (the first 32 KiB when fin is in LDS)
+    };
+    struct {
+      uint8_t bdig_s[kFinLds];
+      uint16_t bfin[kFinLds];  // fin of a workgroup node of <= kFinLds elements
+    };
+    WaveArea w[kRW];           // per-wave slices (the two phases of a round never overlap)
   };
   uint32_t bc[256], bo[256];
   uint32_t nl[2][2];  // node counts [list][0 big, 1 small]
   unsigned long long dups;
 };
 
-struct RefPtrs {
+struct RefPtrs {  // no arrays: a dynamically indexed member would put the struct in scratch (flat accesses)
   uint64_t *slot, *slotT;
   uint32_t *idx, *idxT, *fin;
-  uint64_t* list[2][2];  // [round parity][big, small], capacity cap each
+  uint64_t* lists;  // list (parity, big = 0 / small = 1) at lists + (2 parity + small) cap
   uint32_t cap;
+  __device__ __forceinline__ uint64_t* list(int parity, int small) const {
+    return lists + (size_t)(2 * parity + small) * cap;
+  }
 };
 
 __device__ __forceinline__ void push(RefSmem& S, const RefPtrs& P, int nx, uint32_t off, uint32_t cnt, uint32_t sh) {
@@ -77,44 +88,65 @@ __device__ __forceinline__ void push(RefSmem& S, const RefPtrs& P, int nx, uint3
   if (cnt < 2 || sh == 0) return;
   const int big = cnt > kWaveCap ? 0 : 1;
   const uint32_t k = atomicAdd(&S.nl[nx][big], 1u);
-  P.list[nx][big][k] = pack(off, cnt, sh);
+  P.list(nx, big)[k] = pack(off, cnt, sh);
 }
 
-__device__ __forceinline__ void gsync() {  // global scratch written before, read after, across the workgroup
-  __threadfence();
-  __syncthreads();
-}
+// Global scratch written by some waves of the workgroup and read by others:
+// workgroup scope is enough (the workgroup's waves share one CU and its L1;
+// no device-scope write-back per exchange).
+__device__ __forceinline__ void gsync() { __syncthreads(); }
 
 __device__ __forceinline__ void wsync() {  // the same within one wave
-  __threadfence();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// The American-flag chains of one node (radix_sort.h:231-250), walked by one
-// lane over the node's digits: c[b] counts, o[b] bucket starts on entry.
-// Position p's element ends at fin[p] (node-relative).  The first unplaced
-// slot of bucket b holds its original element (a slot is rewritten only
-// when it is placed), so a chain is: take the element at the slot, send it
-// to the first unplaced slot of its bucket, take that slot's element, ...
-// until one of bucket b comes back to the leader's slot.
+// The American-flag chains of one node (radix_sort.h:231-250), by one wave:
+// the bucket starts (exclusive scan of the counts c, in LDS) in o (LDS),
+// buckets of > 1 element pushed as nodes, then lane 0 walks the chains over
+// the LDS digits: position p's element ends at fin(p) (node-relative).  The
+// first unplaced slot of bucket b holds its original element (a slot is
+// rewritten only when it is placed), so a chain is: take the element at the
+// slot, send it to the first unplaced slot o[d] of its bucket d, take that
+// slot's element, ... until one of bucket b comes back to the leader's slot.
+// A step is two dependent LDS reads (the digit, then its bucket's slot):
+// the walk is sequential by nature, each swap decides the next.
 template <class Fin>
-__device__ void chains(const uint8_t* dig, uint32_t* c, uint32_t* o, uint32_t nb, Fin fin) {
-  for (uint32_t b = 0; b < nb; b++) {
-    while (c[b] > 0) {
-      const uint32_t q = o[b];
-      uint32_t xp = q, d = dig[q];
-      while (d != b) {
-        const uint32_t dst = o[d];
-        o[d] = dst + 1;
-        c[d]--;
-        fin(xp, dst);
-        xp = dst;
-        d = dig[dst];
+__device__ __forceinline__ void chains(RefSmem& S, const RefPtrs& P, int nx, uint32_t off, uint32_t sh2,
+                                       const uint8_t* dig, uint32_t* c, uint32_t* o, uint32_t nb, Fin fin) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t base = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {  // exclusive scan of the counts in bucket order 64 q + lane
+    const uint32_t b = 64u * q + lane;
+    const uint32_t v = b < nb ? c[b] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(inc, d, 64);
+      if (lane >= (uint32_t)d) inc += y;
+    }
+    o[b] = base + inc - v;  // o has 256 entries
+    if (v > 1) push(S, P, nx, off + base + inc - v, v, sh2);
+    base += __shfl(inc, 63, 64);
+  }
+  wave_lds_sync();
+  if (lane == 0) {
+    uint32_t end = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+      end += c[b];
+      for (uint32_t q = o[b]; q < end; q++) {  // o[b] as chains from buckets < b left it
+        uint32_t xp = q, d = dig[q];
+        while (d != b) {
+          const uint32_t dst = o[d];
+          o[d] = dst + 1;
+          fin(xp, dst);
+          xp = dst;
+          d = dig[dst];
+        }
+        fin(xp, q);
       }
-      fin(xp, q);
-      o[b] = q + 1;
-      c[b]--;
     }
   }
 }
@@ -122,7 +154,7 @@ __device__ void chains(const uint8_t* dig, uint32_t* c, uint32_t* o, uint32_t nb
 // the 1-bit pass (radix_sort.h:251-285) on bit 0 (shift 1): Hoare
 // partition; fin must start as the identity
 template <class Fin>
-__device__ void hoare(const uint8_t* bit, uint32_t cnt, Fin fin) {
+__device__ __forceinline__ void hoare(const uint8_t* bit, uint32_t cnt, Fin fin) {
   uint32_t i = 0, j = cnt;
   for (;;) {
     while (i < j && bit[i] == 0) i++;
@@ -138,7 +170,7 @@ __device__ void hoare(const uint8_t* bit, uint32_t cnt, Fin fin) {
 // count < 32 with bits left (radix_sort.h:121-177): compare-exchange
 // sequences for 2-4 elements, gapped insertion passes (48, 21, 7, 3, 1)
 // above; on (slot, local index) pairs in LDS, by one lane
-__device__ void leaf(uint64_t* ls, uint8_t* li, uint32_t cnt) {
+__device__ __forceinline__ void leaf(uint64_t* ls, uint8_t* li, uint32_t cnt) {
   auto cx = [&](int a, int b) {
     if (ls[b] < ls[a]) {
       const uint64_t t = ls[a]; ls[a] = ls[b]; ls[b] = t;
@@ -151,9 +183,9 @@ __device__ void leaf(uint64_t* ls, uint8_t* li, uint32_t cnt) {
     cx(0, 1);
     return;
   }
-  const uint32_t gaps[5] = {48, 21, 7, 3, 1};
+#pragma unroll
   for (int k = 0; k < 5; k++) {
-    const uint32_t h = gaps[k];
+    const uint32_t h = k == 0 ? 48u : k == 1 ? 21u : k == 2 ? 7u : k == 3 ? 3u : 1u;
     for (uint32_t i = h; i < cnt; i++) {
       if (!(ls[i] < ls[i - h])) continue;
       const uint64_t xs = ls[i];
@@ -171,15 +203,20 @@ __device__ void leaf(uint64_t* ls, uint8_t* li, uint32_t cnt) {
 }
 
 // one node above kWaveCap elements, the whole workgroup (uniform control flow)
-__device__ void wg_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node) {
+__device__ __forceinline__ void wg_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node) {
   const uint32_t off = (uint32_t)(node & 0x1ffff), cnt = (uint32_t)((node >> 17) & 0x1ffff),
                  sh = (uint32_t)(node >> 34);
   const uint32_t tid = threadIdx.x;
-  uint32_t* fin = P.fin + off;
+  const bool lf = cnt <= kFinLds;  // fin in LDS (u16), else in global scratch
+  uint32_t* gfin = P.fin + off;
+  uint16_t* lfin = S.bfin;
+  auto setfin = [&](uint32_t from, uint32_t to) { if (lf) lfin[from] = (uint16_t)to; else gfin[from] = to; };
+  auto getfin = [&](uint32_t p) -> uint32_t { return lf ? (uint32_t)lfin[p] : gfin[p]; };
   if (sh > 1) {
     const uint32_t k = sh > 8 ? 8 : sh, sh2 = sh - k, nb = 1u << k;
     for (uint32_t b = tid; b < 256; b += kRT) S.bc[b] = 0;
     __syncthreads();
+#pragma unroll 4
     for (uint32_t p = tid; p < cnt; p += kRT) {
       const uint32_t d = (uint32_t)(P.slot[off + p] >> sh2) & (nb - 1);
       S.bdig[p] = (uint8_t)d;
@@ -191,31 +228,25 @@ __device__ void wg_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node) {
       __syncthreads();
       return;
     }
-    if (tid == 0) {
-      uint32_t base = 0;
-      for (uint32_t b = 0; b < nb; b++) {
-        S.bo[b] = base;
-        if (S.bc[b] > 1) push(S, P, nx, off + base, S.bc[b], sh2);
-        base += S.bc[b];
-      }
-      chains(S.bdig, S.bc, S.bo, nb, [&](uint32_t from, uint32_t to) { fin[from] = to; });
-    }
+    if (tid < 64) chains(S, P, nx, off, sh2, S.bdig, S.bc, S.bo, nb, setfin);
   } else {  // sh == 1
     for (uint32_t p = tid; p < cnt; p += kRT) {
       S.bdig[p] = (uint8_t)(P.slot[off + p] & 1);
-      fin[p] = p;
+      setfin(p, p);
     }
     gsync();
-    if (tid == 0) hoare(S.bdig, cnt, [&](uint32_t from, uint32_t to) { fin[from] = to; });
+    if (tid == 0) hoare(S.bdig, cnt, setfin);
     // children have no bits left: in place
   }
   gsync();
+#pragma unroll 4
   for (uint32_t p = tid; p < cnt; p += kRT) {
-    const uint32_t t = fin[p];
+    const uint32_t t = getfin(p);
     P.slotT[off + t] = P.slot[off + p];
     P.idxT[off + t] = P.idx[off + p];
   }
   gsync();
+#pragma unroll 4
   for (uint32_t p = tid; p < cnt; p += kRT) {
     P.slot[off + p] = P.slotT[off + p];
     P.idx[off + p] = P.idxT[off + p];
@@ -224,15 +255,14 @@ __device__ void wg_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node) {
 }
 
 // one node of <= kWaveCap elements, one wave
-__device__ void wave_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node, WaveArea& W) {
+__device__ __forceinline__ void wave_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node, WaveArea& W) {
   const uint32_t off = (uint32_t)(node & 0x1ffff), cnt = (uint32_t)((node >> 17) & 0x1ffff),
                  sh = (uint32_t)(node >> 34);
   const uint32_t lane = threadIdx.x & 63;
   if (cnt < 32) {  // a tail: sorted on less() by lane 0 (sh >= 1 here)
-    if (lane == 0) {
-      for (uint32_t p = 0; p < cnt; p++) { W.ls[p] = P.slot[off + p]; W.li[p] = (uint8_t)p; }
-      leaf(W.ls, W.li, cnt);
-    }
+    if (lane < cnt) { W.ls[lane] = P.slot[off + lane]; W.li[lane] = (uint8_t)lane; }
+    wave_lds_sync();
+    if (lane == 0) leaf(W.ls, W.li, cnt);
     wave_lds_sync();
     uint64_t s = 0;
     uint32_t ix = 0;
@@ -248,6 +278,7 @@ __device__ void wave_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node, W
     wsync();
     return;
   }
+  auto setfin = [&](uint32_t from, uint32_t to) { W.fin[from] = (uint16_t)to; };
   if (sh > 1) {
     const uint32_t k = sh > 8 ? 8 : sh, sh2 = sh - k, nb = 1u << k;
     for (uint32_t b = lane; b < 256; b += 64) W.c[b] = 0;
@@ -263,22 +294,14 @@ __device__ void wave_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node, W
       wave_lds_sync();
       return;
     }
-    if (lane == 0) {
-      uint32_t base = 0;
-      for (uint32_t b = 0; b < nb; b++) {
-        W.o[b] = base;
-        if (W.c[b] > 1) push(S, P, nx, off + base, W.c[b], sh2);
-        base += W.c[b];
-      }
-      chains(W.dig, W.c, W.o, nb, [&](uint32_t from, uint32_t to) { W.fin[from] = (uint16_t)to; });
-    }
+    chains(S, P, nx, off, sh2, W.dig, W.c, W.o, nb, setfin);
   } else {  // sh == 1
     for (uint32_t p = lane; p < cnt; p += 64) {
       W.dig[p] = (uint8_t)(P.slot[off + p] & 1);
       W.fin[p] = (uint16_t)p;
     }
     wave_lds_sync();
-    if (lane == 0) hoare(W.dig, cnt, [&](uint32_t from, uint32_t to) { W.fin[from] = (uint16_t)to; });
+    if (lane == 0) hoare(W.dig, cnt, setfin);
   }
   wave_lds_sync();
   for (uint32_t p = lane; p < cnt; p += 64) {
@@ -307,8 +330,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
     P.cap = cap;
     P.slot = (uint64_t*)s; s += 8 * (size_t)n;
     P.slotT = (uint64_t*)s; s += 8 * (size_t)n;
-    for (int a = 0; a < 2; a++)
-      for (int b = 0; b < 2; b++) { P.list[a][b] = (uint64_t*)s; s += 8 * (size_t)cap; }
+    P.lists = (uint64_t*)s; s += 4 * 8 * (size_t)cap;
     P.idx = (uint32_t*)s; s += 4 * (size_t)n;
     P.idxT = (uint32_t*)s; s += 4 * (size_t)n;
     P.fin = (uint32_t*)s;
@@ -324,7 +346,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
     if (n >= 32)
       push(S, P, 0, 0, n, bits);
     else if (n >= 2)  // a root of < 32 elements is one tail (even the shift-0 case cannot occur: bits >= 1)
-      S.nl[0][1] = 1, P.list[0][1][0] = pack(0, n, bits);
+      S.nl[0][1] = 1, P.list(0, 1)[0] = pack(0, n, bits);
   }
   gsync();
   for (int cur = 0;; cur ^= 1) {
@@ -334,8 +356,8 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
     __syncthreads();
     if (tid < 2) S.nl[nx][tid] = 0;
     __syncthreads();
-    for (uint32_t k = 0; k < nbig; k++) wg_step(S, P, nx, P.list[cur][0][k]);
-    for (uint32_t k = wv; k < nsmall; k += kRW) wave_step(S, P, nx, P.list[cur][1][k], S.w[wv]);
+    for (uint32_t k = 0; k < nbig; k++) wg_step(S, P, nx, P.list(cur, 0)[k]);
+    for (uint32_t k = wv; k < nsmall; k += kRW) wave_step(S, P, nx, P.list(cur, 1)[k], S.w[wv]);
     gsync();
   }
   // out: the sorted elements; ctest's marking (ctest.c:96-104): an element
