@@ -257,7 +257,11 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 // register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
 // more take wide_window (input order, u64 offsets and lengths).
 
-template <int NT, int NW, int KF, bool PF = false, bool PKY = true, bool CL = false, bool Q = false>
+// AB (experiments build only, knob 7 = 61-66): counter ablations whose
+// outputs are not hashes -- 1 no window sort (records in input order; timed on
+// input already sorted by class within each window), 2-4 meow_a's (see
+// there), 5 the table rounds replaced by one XOR per column, 6 no hashing.
+template <int NT, int NW, int KF, bool PF = false, bool PKY = true, bool CL = false, bool Q = false, int AB = 0>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
        uint64_t* __restrict__ out, uint32_t flags, unsigned long long* __restrict__ tk = nullptr) {
@@ -324,6 +328,13 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       wide_window<NT>(keys, offs, i0, k, M, s1, s2, out, fix, lds);
       continue;
     }
+    uint2 rc0, rc1, rc2, rc3;
+    if constexpr (AB == 1) {
+      rc0 = make_uint2(o[0], (L[0] << 8) | lane);
+      rc1 = make_uint2(o[1], (L[1] << 8) | (64 + lane));
+      rc2 = make_uint2(o[2], (L[2] << 8) | (128 + lane));
+      rc3 = make_uint2(o[3], (L[3] << 8) | (192 + lane));
+    } else {
     // counting sort of the window by 16-byte length class
 #pragma unroll
     for (int q = 0; q < 4; q++) hist[lane * 4 + q] = 0;
@@ -360,8 +371,9 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
     wave_sync();
     // this lane's sorted positions lane, 64 + lane, ... (rotated through
     // scalars below: a register array indexed in a rolled loop is scratch)
-    uint2 rc0 = rec[lane], rc1 = rec[64 + lane], rc2 = rec[128 + lane], rc3 = rec[192 + lane];
+    rc0 = rec[lane]; rc1 = rec[64 + lane]; rc2 = rec[128 + lane]; rc3 = rec[192 + lane];
     wave_sync();  // the stage takes hashes from here on
+    }
     const uint8_t* base = keys + ws;
 #pragma unroll 1
     for (int c = 0; c < M; c++) {
@@ -376,13 +388,27 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       if (valid) {
         const uint8_t* p = base + rc.x;
         const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
-        const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
         Blk h;
-        if (al) h = meow_a<true, 48, PF, PKY, CL>(p, kl, safe, K, T);
-        else if (cm == 48) h = meow_a<false, 48, PF, PKY, CL>(p, kl, safe, K, T);
-        else if (cm == 32) h = meow_a<false, 32, PF, PKY, CL>(p, kl, safe, K, T);
-        else if (cm == 16) h = meow_a<false, 16, PF, PKY, CL>(p, kl, safe, K, T);
-        else h = meow_a<false, 0, PF, PKY, CL>(p, kl, safe, K, T);
+        if constexpr (AB == 6) {
+          h = bzero();
+          h.w[0] = kl;
+        } else if constexpr (AB == 5) {
+          const XorTab X;
+          const LdsKV9<XorTab, KF> K(kfull, kf, kl, s1, s2, X);
+          if (al) h = meow_a<true, 48, PF, PKY, CL>(p, kl, safe, K, X);
+          else if (cm == 48) h = meow_a<false, 48, PF, PKY, CL>(p, kl, safe, K, X);
+          else if (cm == 32) h = meow_a<false, 32, PF, PKY, CL>(p, kl, safe, K, X);
+          else if (cm == 16) h = meow_a<false, 16, PF, PKY, CL>(p, kl, safe, K, X);
+          else h = meow_a<false, 0, PF, PKY, CL>(p, kl, safe, K, X);
+        } else {
+          constexpr int A2 = AB >= 2 && AB <= 4 ? AB : 0;
+          const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
+          if (al) h = meow_a<true, 48, PF, PKY, CL, A2>(p, kl, safe, K, T);
+          else if (cm == 48) h = meow_a<false, 48, PF, PKY, CL, A2>(p, kl, safe, K, T);
+          else if (cm == 32) h = meow_a<false, 32, PF, PKY, CL, A2>(p, kl, safe, K, T);
+          else if (cm == 16) h = meow_a<false, 16, PF, PKY, CL, A2>(p, kl, safe, K, T);
+          else h = meow_a<false, 0, PF, PKY, CL, A2>(p, kl, safe, K, T);
+        }
         stage[rc.y & 255u] = fix ? fixup(h) : h;
       }
     }
@@ -483,6 +509,17 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
                          (uint64_t)n, seed1, seed2, out, flags);
       return launch_done();
+    case 61: case 62: case 63: case 64: case 65: case 66: {  // round-5 counter ablations (outputs not hashes)
+      unsigned long long* tk = nullptr;
+      if (int rc = stream_tickets(st, &tk)) return rc;
+      if (!tk) return set_err(KVH_EINVAL);
+#define KVH_AB(v) \
+  case 60 + v: hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, false, true, v>), dim3(grid), dim3(1024), 0, st, kp, \
+                                  offsets, (uint64_t)n, seed1, seed2, out, flags, tk); break;
+      switch (var) { KVH_AB(1) KVH_AB(2) KVH_AB(3) KVH_AB(4) KVH_AB(5) KVH_AB(6) }
+#undef KVH_AB
+      return launch_done();
+    }
     case 44:  // round-4 A/B: four tables at 16 copies in the same 64 KiB (LdsTab<5>)
       hipLaunchKernelGGL((k_var9<5, 16, 256>), dim3(grid), dim3(1024), 0, st, kp, offsets, (uint64_t)n, seed1, seed2,
                          out, flags);

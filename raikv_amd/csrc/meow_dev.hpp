@@ -130,6 +130,18 @@ struct ConstTab {
   }
 };
 
+// Ablation table (experiments build only, k_var9 AB = 5): a "round" that is
+// one XOR per column -- the kernel's work with the table rounds taken out.
+struct XorTab {
+  __device__ __forceinline__ uint32_t col(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
+    return xor3(a, b, c) ^ d ^ k;
+  }
+  __device__ __forceinline__ static uint32_t prep(uint32_t k) { return k; }
+  __device__ __forceinline__ uint32_t colk(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) const {
+    return col(a, b, c, d, k);
+  }
+};
+
 // Intel AESDEC(s, k) = InvMixColumns(InvSubBytes(InvShiftRows(s))) ^ k.
 // Output column c takes row r from input column (c - r) & 3.
 template <class Tab>
@@ -532,14 +544,35 @@ __device__ __forceinline__ auto f_short(const KGet& K, int i, int) -> decltype(K
 template <class KGet>
 __device__ __forceinline__ Blk f_short(const KGet& K, int i, long) { return K.F(i); }
 
-template <bool AL, int CM, bool PF, bool PKY = false, bool CL = false, class Tab, class KGet, class LenT = uint32_t>
+// AB (experiments build only, counter ablations of C2's non-round work,
+// DESIGN.md §3.3): 2 = groups read without the per-group bounds compare,
+// 3 = the per-lane state selects (bsel) dropped, 4 = the partial piece not
+// masked.  Outputs of AB != 0 are not hashes.
+template <bool AL, int CM, bool PF, bool PKY = false, bool CL = false, int AB = 0, class Tab, class KGet,
+          class LenT = uint32_t>
 __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const KGet& K, const Tab& T) {
   constexpr bool P0 = AL || CM >= 16, P1 = AL || CM >= 32, P2 = AL || CM >= 48;  // state touched by some lane
   const LenT nb = L >> 6;
   const uint32_t C = (uint32_t)L & 48, t = (uint32_t)L & 15;
   const bool first = nb == 0;
   const AChunks A(p, L, safe);
-  auto ch = [&](uint64_t i) { if constexpr (CL) return A.chunk_cl(i); else return A.chunk(i); };
+  auto ch = [&](uint64_t i) {
+    if constexpr (AB == 2) {
+      if (A.safe) {
+        const u32x4_a4 v = A.g[i];
+        Blk r;
+        r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
+        return r;
+      }
+      return A.chunk(i);
+    } else if constexpr (CL) {
+      return A.chunk_cl(i);
+    } else {
+      return A.chunk(i);
+    }
+  };
+  auto bsel = [](bool c, const Blk& a, const Blk& b) { if constexpr (AB == 3) return a; else return kvh::bsel(c, a, b); };
+  auto mask_bytes = [](const Blk& b, uint32_t n) { if constexpr (AB == 4) return b; else return kvh::mask_bytes(b, n); };
   const Blk M = K.M();
   // PKY: keys used in more than one round go through LdsTab::prep once
   PKey MP{};
@@ -551,8 +584,10 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
   };
   // AESDEC(first ? f ^ k : AESDEC(s, k), k)
   auto adT = [&](bool first_, const Blk& f, const Blk& s_, const Blk& k) {
-    if constexpr (PKY) { const PKey kp = pkey(k, T); return aesdec_p(bsel(first_, f, aesdec_p(s_, kp, T)), kp, T); }
-    else return aesdec(bsel(first_, f, aesdec(s_, k, T)), k, T);
+    // (AB 3 keeps the absorbed-state round: the ablation removes selects, not rounds)
+    auto bselr = [](bool c, const Blk& a, const Blk& b) { if constexpr (AB == 3) return b; else return kvh::bsel(c, a, b); };
+    if constexpr (PKY) { const PKey kp = pkey(k, T); return aesdec_p(bselr(first_, f, aesdec_p(s_, kp, T)), kp, T); }
+    else return aesdec(bselr(first_, f, aesdec(s_, k, T)), k, T);
   };
   Blk S0 = bxor(ramp(0), M), S1 = bxor(ramp(1), M), S2 = bxor(ramp(2), M), S3 = bxor(ramp(3), M);
   // groups 4nb .. 4nb+4 (the trail's) once the blocks are absorbed

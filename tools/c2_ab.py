@@ -21,9 +21,15 @@ ap.add_argument("--variants", default="23")
 ap.add_argument("--ablations", default="")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--per", type=int, default=4, help="timed launches per variant per round")
+ap.add_argument("--presorted", action="store_true",
+                help="lengths already sorted by 16-byte class within each 256-key window (the sort ablation 61)")
 a = ap.parse_args()
 torch.cuda.set_device(0)
-offs = offsets_from_lengths(zipf_lengths(a.n, 8, 256, seed=3))
+lens = zipf_lengths(a.n, 8, 256, seed=3)
+if a.presorted:
+    from c2_presort import presort_windows
+    lens = presort_windows(lens)
+offs = offsets_from_lengths(lens)
 g = torch.Generator(device="cuda")
 g.manual_seed(2024)
 keys = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device="cuda", generator=g)

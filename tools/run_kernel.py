@@ -19,6 +19,7 @@ ap.add_argument("--nt", type=int, default=0)
 ap.add_argument("--kpl", type=int, default=0)
 ap.add_argument("--var", type=int, default=-1)
 ap.add_argument("--knob", action="append", default=[], help="kvh_set_tuning K=V (repeatable)")
+ap.add_argument("--presorted", action="store_true", help="c2: lengths pre-sorted by class within each 256-key window")
 a = ap.parse_args()
 for kv in a.knob:
     k, v = kv.split("=")
@@ -75,7 +76,12 @@ elif ar < 0:  # table positions, geometry as bench.py F1_GEOM
         kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=hh, fixup=True)
         f = lambda: kvh.ht_positions(hh, geom, out=pos)
 elif L == 0:
-    offs = offsets_from_lengths(zipf_lengths(n, 8, 256, seed=3))
+    lens = zipf_lengths(n, 8, 256, seed=3)
+    if a.presorted:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from c2_presort import presort_windows
+        lens = presort_windows(lens)
+    offs = offsets_from_lengths(lens)
     keys = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device="cuda", generator=g)
     doff = torch.from_numpy(offs.view(np.int64)).cuda()
     f = lambda: kvh.meow128_var(keys, doff, kvh.STATIC_SEED)
