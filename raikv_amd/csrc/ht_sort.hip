@@ -730,9 +730,13 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
 #pragma unroll
       for (uint32_t j = 0; j < PER; j++) {
         const uint32_t p = tid + j * T;
+        const uint64_t v = p < R ? u.X[ord[p]] : 0ull;
+        // the successor's field: the next lane's (one random LDS gather per
+        // record instead of two), a gather only at a wave's last lane
+        uint64_t nv = (uint64_t)__shfl_down((unsigned long long)v, 1, 64);
+        if (lane == 63 && f < 2 && dedup && p + 1 < R) nv = u.X[ord[p + 1]];
         if (p < R) {
-          const uint64_t v = u.X[ord[p]];
-          const bool eq = f < 2 && dedup && p + 1 < R && u.X[ord[p + 1 < R ? p + 1 : p]] == v;
+          const bool eq = f < 2 && dedup && p + 1 < R && nv == v;
           if (f == 0) {
             h1v[j] = v;
             eq1 |= (eq ? 1u : 0u) << j;

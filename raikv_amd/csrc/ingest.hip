@@ -445,14 +445,14 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
          uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
          const uint64_t* __restrict__ dcount = nullptr) {  // dcount: n = min(n, *dcount), read on the device
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  __shared__ MeowConst kfull[kLT];
+  __shared__ MeowConstL kfull[kLT];
   __shared__ Blk kf[kNF * 4];
   fill_tables<NT>(lds);
   __syncthreads();
   const LdsTab<NT> T(lds);
   for (uint32_t l = threadIdx.x; l < (uint32_t)(kLT + kNF); l += blockDim.x) {
     if (l < (uint32_t)kLT) {
-      kfull[l] = make_const(s1, s2, l, T);
+      static_cast<MeowConst&>(kfull[l]) = make_const(s1, s2, l, T);
     } else {
       const Blk M = mixer(s1, s2, l);
 #pragma unroll
@@ -480,9 +480,9 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
       H = D;
       p = rec + 2;
     }
-    const LdsK<LdsTab<NT>> K(kfull, kf, H, s1, s2, T);
+    const LdsK<LdsTab<NT>, uint32_t, MeowConstL> K(kfull, kf, H, s1, s2, T);
     const MaskLd ld{p + D};
-    store_h(out, i, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>>, MaskLd>(p, H, K, T, ld), fix);
+    store_h(out, i, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>, uint32_t, MeowConstL>, MaskLd>(p, H, K, T, ld), fix);
   }
 }
 
@@ -491,16 +491,16 @@ template <int NT>
 __device__ __forceinline__ void spans_long(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
                                            const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
                                            const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
-                                           uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConst* kfull,
+                                           uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConstL* kfull,
                                            uint64_t s1, uint64_t s2, const LdsTab<NT>& T) {
   if (lane < cnt) {
     const uint32_t e = q[lane];
     const uint64_t j = qbase + (uint64_t)(e / CH) * step + (e % CH);
     const uint8_t* p = buf + offs[j];
     const uint32_t D = lens[j], H = D + nul;
-    const LdsK<LdsTab<NT>> K(kfull, nullptr, H, s1, s2, T);
+    const LdsK<LdsTab<NT>, uint32_t, MeowConstL> K(kfull, nullptr, H, s1, s2, T);
     const MaskLd ld{p + D};
-    store_h(out, j, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>>, MaskLd>(p, H, K, T, ld), fix);
+    store_h(out, j, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>, uint32_t, MeowConstL>, MaskLd>(p, H, K, T, ld), fix);
   }
 }
 
@@ -639,7 +639,7 @@ template <int NT>
 __device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
                                              const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
                                              const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
-                                             uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConst* kfull,
+                                             uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConstL* kfull,
                                              const uint32_t* __restrict__ psel, const LdsTab<NT>& T) {
   if (lane < cnt) {
     const uint32_t e = q[lane];
@@ -665,7 +665,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   // < 64 after a flush and an iteration adds <= CH to the two together
   constexpr uint32_t QCAP = 2 * 64 + CH;
   __shared__ uint32_t lds[LdsTab<NT>::kWords];
-  __shared__ MeowConst kfull[kLT];
+  __shared__ MeowConstL kfull[kLT];
   __shared__ uint32_t queue[NW][QCAP];
   __shared__ uint32_t psel[17 * 4 * 4];  // [D 0..16][p & 3][word] v_perm selectors
   fill_tables<NT>(lds);
@@ -677,7 +677,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   }
   __syncthreads();
   const LdsTab<NT> T(lds);
-  for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) kfull[l] = make_const(s1, s2, l, T);
+  for (uint32_t l = threadIdx.x; l < (uint32_t)kLT; l += blockDim.x) static_cast<MeowConst&>(kfull[l]) = make_const(s1, s2, l, T);
   __shared__ WaveTickets WT;
   if constexpr (Q) wt_init(WT, tk);  // ends with a barrier
   else __syncthreads();

@@ -54,18 +54,26 @@ __device__ __forceinline__ void store_h(uint64_t* __restrict__ out, uint64_t idx
 constexpr int kLT = 64;   // full per-length constant records (L < 64)
 constexpr int kNF = 256;  // F-only records for 64 <= L < 64 + kNF
 
+// MeowConst padded to 13 blocks, for LDS arrays read at a per-lane length: a
+// 52-dword stride puts one field of 16 consecutive lengths on 16 distinct
+// 16-byte bank slots (MeowConst's own 48-dword stride repeats every 4
+// lengths: 4-way conflicts on every ds_read_b128 of a chunk of short spans).
+struct MeowConstL : MeowConst {
+  Blk pad;
+};
+
 // Per-length folding constants of a variable-length batch from LDS tables
 // (k_generic, k_keysrc): full records for L < kLT, first-absorb folds for
 // kLT <= L < kLT + kNF, in-lane folds beyond.  LenT = uint64_t for keys of
 // 4 GiB and more (the Mixer takes the full length, key_hash.c:1418).
-template <class Tab, class LenT = uint32_t>
+template <class Tab, class LenT = uint32_t, class KRec = MeowConst>
 struct LdsK {
-  const MeowConst* full;   // [kLT]
+  const KRec* full;        // [kLT]
   const Blk* ftab;         // [kNF][4], or null: folds in-lane
   LenT L;
   Blk m;
   const Tab& T;
-  __device__ __forceinline__ LdsK(const MeowConst* f, const Blk* ft, LenT len, uint64_t s1,
+  __device__ __forceinline__ LdsK(const KRec* f, const Blk* ft, LenT len, uint64_t s1,
                                   uint64_t s2, const Tab& t)
       : full(f), ftab(ft), L(len), m(mixer(s1, s2, len)), T(t) {}
   __device__ __forceinline__ uint32_t li() const { return L < (LenT)kLT ? (uint32_t)L : (uint32_t)kLT - 1; }

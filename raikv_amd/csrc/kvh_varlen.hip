@@ -257,10 +257,13 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 // register array.  Windows spanning 4 GiB or holding a key of 16 MiB or
 // more take wide_window (input order, u64 offsets and lengths).
 
-// AB (experiments build only, knob 7 = 61-66): counter ablations whose
+// AB (experiments build only, knob 7 = 61-69): counter ablations whose
 // outputs are not hashes -- 1 no window sort (records in input order; timed on
-// input already sorted by class within each window), 2-4 meow_a's (see
-// there), 5 the table rounds replaced by one XOR per column, 6 no hashing.
+// input already sorted by class within each window), 2-4 and 7 meow_a's (see
+// there), 5 the table rounds replaced by one XOR per column, 6 no hashing,
+// 8 every lane's key read from window base + 48 lane (the chunk's loads as
+// coalesced as keys stored contiguously in lane order).  (9, the stable
+// window sort, became the product's in round 5.)
 template <int NT, int NW, int KF, bool PF = false, bool PKY = true, bool CL = false, bool Q = false, int AB = 0>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
@@ -342,9 +345,12 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 #pragma unroll
     for (int m = 0; m < M; m++) {
       const uint32_t j = lane + 64 * m;
-      // 64 length classes x 4 sub-counters by lane & 3: a quarter of the
-      // same-address atomics (a class's keys in one instruction serialise)
-      b[m] = ((L[m] >> 4) < 63u ? (L[m] >> 4) : 63u) * 4u + (lane & 3u);
+      // 64 length classes, one counter each (of four slots: the scan below
+      // reads them as before): the ranks of one instruction's lanes come back
+      // in lane order, so a class's keys keep their input order and a chunk's
+      // loads walk the window forward -- 2 % over four sub-counters by
+      // lane & 3, which spread a class's keys (round 5, profiles/r05/s5/)
+      b[m] = ((L[m] >> 4) < 63u ? (L[m] >> 4) : 63u) * 4u;
       r[m] = j < k ? atomicAdd(&hist[b[m]], 1u) : 0u;
     }
     wave_sync();
@@ -386,8 +392,13 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       const int cm = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
                    : __ballot((kl & 48u) >= 16u) ? 16 : 0;
       if (valid) {
-        const uint8_t* p = base + rc.x;
-        const bool safe = (uint64_t)rc.x + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
+        uint32_t kx = rc.x;
+        if constexpr (AB == 8) {  // pretend the chunk's keys lie back to back in lane order
+          const uint64_t fake = 48ull * lane;
+          if (fake + kl + 16 <= wend) kx = (uint32_t)fake;
+        }
+        const uint8_t* p = base + kx;
+        const bool safe = (uint64_t)kx + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
         Blk h;
         if constexpr (AB == 6) {
           h = bzero();
@@ -401,7 +412,7 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
           else if (cm == 16) h = meow_a<false, 16, PF, PKY, CL>(p, kl, safe, K, X);
           else h = meow_a<false, 0, PF, PKY, CL>(p, kl, safe, K, X);
         } else {
-          constexpr int A2 = AB >= 2 && AB <= 4 ? AB : 0;
+          constexpr int A2 = (AB >= 2 && AB <= 4) || AB == 7 ? AB : 0;
           const LdsKV9<LdsTab<NT>, KF> K(kfull, kf, kl, s1, s2, T);
           if (al) h = meow_a<true, 48, PF, PKY, CL, A2>(p, kl, safe, K, T);
           else if (cm == 48) h = meow_a<false, 48, PF, PKY, CL, A2>(p, kl, safe, K, T);
@@ -509,14 +520,14 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
                          (uint64_t)n, seed1, seed2, out, flags);
       return launch_done();
-    case 61: case 62: case 63: case 64: case 65: case 66: {  // round-5 counter ablations (outputs not hashes)
+    case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69: {  // round-5 ablations (69 hashes)
       unsigned long long* tk = nullptr;
       if (int rc = stream_tickets(st, &tk)) return rc;
       if (!tk) return set_err(KVH_EINVAL);
 #define KVH_AB(v) \
   case 60 + v: hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, false, true, v>), dim3(grid), dim3(1024), 0, st, kp, \
                                   offsets, (uint64_t)n, seed1, seed2, out, flags, tk); break;
-      switch (var) { KVH_AB(1) KVH_AB(2) KVH_AB(3) KVH_AB(4) KVH_AB(5) KVH_AB(6) }
+      switch (var) { KVH_AB(1) KVH_AB(2) KVH_AB(3) KVH_AB(4) KVH_AB(5) KVH_AB(6) KVH_AB(7) KVH_AB(8) KVH_AB(9) }
 #undef KVH_AB
       return launch_done();
     }

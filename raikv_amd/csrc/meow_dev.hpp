@@ -547,7 +547,8 @@ __device__ __forceinline__ Blk f_short(const KGet& K, int i, long) { return K.F(
 // AB (experiments build only, counter ablations of C2's non-round work,
 // DESIGN.md §3.3): 2 = groups read without the per-group bounds compare,
 // 3 = the per-lane state selects (bsel) dropped, 4 = the partial piece not
-// masked.  Outputs of AB != 0 are not hashes.
+// masked, 7 = no key loads (group data made from the address).  Outputs of
+// AB != 0 are not hashes.
 template <bool AL, int CM, bool PF, bool PKY = false, bool CL = false, int AB = 0, class Tab, class KGet,
           class LenT = uint32_t>
 __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const KGet& K, const Tab& T) {
@@ -557,7 +558,12 @@ __device__ __forceinline__ Blk meow_a(const uint8_t* p, LenT L, bool safe, const
   const bool first = nb == 0;
   const AChunks A(p, L, safe);
   auto ch = [&](uint64_t i) {
-    if constexpr (AB == 2) {
+    if constexpr (AB == 7) {  // no key loads: data made from the address
+      Blk r;
+      const uint32_t a = (uint32_t)(uintptr_t)A.g + 16u * (uint32_t)i;
+      r.w[0] = a; r.w[1] = a ^ 0x9e3779b9u; r.w[2] = a + 7u; r.w[3] = a * 3u;
+      return r;
+    } else if constexpr (AB == 2) {
       if (A.safe) {
         const u32x4_a4 v = A.g[i];
         Blk r;
