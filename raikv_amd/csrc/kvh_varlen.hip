@@ -262,8 +262,9 @@ k_var6(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
 // input already sorted by class within each window), 2-4 and 7 meow_a's (see
 // there), 5 the table rounds replaced by one XOR per column, 6 no hashing,
 // 8 every lane's key read from window base + 48 lane (the chunk's loads as
-// coalesced as keys stored contiguously in lane order).  (9, the stable
-// window sort, became the product's in round 5.)
+// coalesced as keys stored contiguously in lane order), 10 the four lanes of
+// each quad read the quad's first key (the line count of a quad-per-key
+// load).  (9, the stable window sort, became the product's in round 5.)
 template <int NT, int NW, int KF, bool PF = false, bool PKY = true, bool CL = false, bool Q = false, int AB = 0>
 __global__ void __launch_bounds__(NW * 64)
 k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n, uint64_t s1, uint64_t s2,
@@ -388,6 +389,11 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
       const uint2 rc = rc0;
       rc0 = rc1; rc1 = rc2; rc2 = rc3;
       const uint32_t kl = valid ? rc.y >> 8 : 0u;
+      uint32_t lead_x = rc.x;
+      if constexpr (AB == 10) {  // the key of the quad's first lane (when it is a valid position)
+        const uint32_t lx = (uint32_t)__shfl((int)rc.x, (int)(lane & ~3u), 64);
+        if ((64 * c + (lane & ~3u)) < k) lead_x = lx;
+      }
       const bool al = __ballot(kl >= 64u) != 0;
       const int cm = __ballot((kl & 48u) == 48u) ? 48 : __ballot((kl & 48u) >= 32u) ? 32
                    : __ballot((kl & 48u) >= 16u) ? 16 : 0;
@@ -396,6 +402,10 @@ k_var9(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint
         if constexpr (AB == 8) {  // pretend the chunk's keys lie back to back in lane order
           const uint64_t fake = 48ull * lane;
           if (fake + kl + 16 <= wend) kx = (uint32_t)fake;
+        }
+        if constexpr (AB == 10) {  // the four lanes of a quad read one key's lines (the access
+          // pattern of a quad-per-key load: 16 keys' lines per load instruction instead of 64)
+          if ((uint64_t)lead_x + kl + 16 <= wend) kx = lead_x;
         }
         const uint8_t* p = base + kx;
         const bool safe = (uint64_t)kx + kl + 16 <= wend;  // whole dwordx4 groups stay in the buffer
@@ -520,14 +530,14 @@ int var_dispatch(const uint8_t* kp, const uint64_t* offsets, uint64_t n, uint64_
       hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, true>), dim3(grid), dim3(1024), 0, st, kp, offsets,
                          (uint64_t)n, seed1, seed2, out, flags);
       return launch_done();
-    case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69: {  // round-5 ablations (69 hashes)
+    case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 70: {  // round-5 ablations (69 hashes)
       unsigned long long* tk = nullptr;
       if (int rc = stream_tickets(st, &tk)) return rc;
       if (!tk) return set_err(KVH_EINVAL);
 #define KVH_AB(v) \
   case 60 + v: hipLaunchKernelGGL((k_var9<2, 16, 256, false, true, false, true, v>), dim3(grid), dim3(1024), 0, st, kp, \
                                   offsets, (uint64_t)n, seed1, seed2, out, flags, tk); break;
-      switch (var) { KVH_AB(1) KVH_AB(2) KVH_AB(3) KVH_AB(4) KVH_AB(5) KVH_AB(6) KVH_AB(7) KVH_AB(8) KVH_AB(9) }
+      switch (var) { KVH_AB(1) KVH_AB(2) KVH_AB(3) KVH_AB(4) KVH_AB(5) KVH_AB(6) KVH_AB(7) KVH_AB(8) KVH_AB(10) }
 #undef KVH_AB
       return launch_done();
     }

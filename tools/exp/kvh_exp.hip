@@ -2828,7 +2828,7 @@ bool exp_var(int var, const uint8_t* kp, const uint64_t* offsets, uint64_t n, ui
   return true;
 }
 
-bool exp_var_knob(int v) { return (v >= 2 && v <= 50) || (v >= 61 && v <= 69); }  // 7, 13, 24, 25, 44, 45, 47-50: var_dispatch under KVH_EXPERIMENTS
+bool exp_var_knob(int v) { return (v >= 2 && v <= 50) || (v >= 61 && v <= 70); }  // 7, 13, 24, 25, 44, 45, 47-50: var_dispatch under KVH_EXPERIMENTS
 
 int exp_set_tuning(int k, int value) {
   auto set = [](Knob& g, int v) { return g.exchange(v, std::memory_order_relaxed); };
