@@ -604,7 +604,11 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
 // the start of this one's LDS phases, so its loads would hit L2 / MALL, was
 // 4 % slower: profiles/r04/s12/; so was taking the buckets in address
 // order from a ticket counter, 2 %: s19/.)
-template <uint32_t CAP, int D, int T = kBkT>
+// W2 (round 5): h1 and h2 leave in ONE field round (16-byte LDS records, one
+// random ds_read_b128 per record and a 16-byte output store) and the item in
+// a second, instead of three 8-byte rounds: two barriers and one ord[] read
+// fewer per record.  The union then holds 56 KiB, 63 KiB per workgroup.
+template <uint32_t CAP, int D, int T = kBkT, bool W2 = false>
 __global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD (512 threads x 2 per CU spill: 87 VGPRs)
 k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
            uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
@@ -621,6 +625,7 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
   union Lds {
     SortArrays s;
     uint64_t X[CAP];  // one field of every record, in record order
+    ulonglong2 X2[W2 ? CAP : 1];  // W2: h1 and h2 of every record
   };
   __shared__ Lds u;
   __shared__ uint16_t ord[CAP];  // sorted position -> record
@@ -717,6 +722,49 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       }
     }
     __syncthreads();  // ord final; the sort arrays are free for the field rounds
+    if constexpr (W2) {
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t r = tid + j * T;
+        if (r < R) u.X2[r] = make_ulonglong2(f0[j], f1[j]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t p = tid + j * T;
+        ulonglong2 v = make_ulonglong2(0ull, 0ull);
+        if (p < R) v = u.X2[ord[p]];
+        // the successor's pair: the next lane's, a gather only at a wave's last lane
+        uint64_t n1 = (uint64_t)__shfl_down((unsigned long long)v.x, 1, 64),
+                 n2 = (uint64_t)__shfl_down((unsigned long long)v.y, 1, 64);
+        if (lane == 63 && dedup && p + 1 < R) {
+          const ulonglong2 w = u.X2[ord[p + 1]];
+          n1 = w.x;
+          n2 = w.y;
+        }
+        if (p < R) {
+          const bool dup = dedup && p + 1 < R && n1 == v.x && n2 == v.y;
+          d_total += dup ? 1u : 0u;
+          *(ulonglong2*)(h_out + 2 * ((uint64_t)base + p)) = make_ulonglong2(dup ? 0ull : v.x, v.y);
+        }
+      }
+      __syncthreads();
+      if (items_out) {
+#pragma unroll
+        for (uint32_t j = 0; j < PER; j++) {
+          const uint32_t r = tid + j * T;
+          if (r < R) u.X[r] = f2[j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < PER; j++) {
+          const uint32_t p = tid + j * T;
+          if (p < R) items_out[(uint64_t)base + p] = u.X[ord[p]];
+        }
+        __syncthreads();
+      }
+      continue;
+    }
     uint64_t h1v[PER];
     uint32_t eq1 = 0;  // bit j: sorted position tid + j * T has the same h1 as its successor
 #pragma unroll
@@ -1664,7 +1712,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
     // knob 23 = 3: half-size buckets (mean <= 3072, up to 15 bits: pass 2 of
     // 8 bits) for the bucket sort at two 512-thread workgroups per CU
     const int b3 = g_tune_sort_b3.load(std::memory_order_relaxed);
-    const bool half = b3 == 3 && engine != 2;
+    const bool half = (b3 == 3 || b3 == 5) && engine != 2;
     uint32_t B = 0;
     while (B < (uint32_t)(half ? kTwMaxB : kBkMaxB) && mean_of(B) > (half ? 3072.0 : 6144.0)) B++;
     // buckets then hold ~mean +- sqrt(mean): the two-per-CU bucket sort (capacity
@@ -1735,11 +1783,16 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       if (small_b && half) {  // half-size buckets: two 512-thread workgroups per CU
         const uint32_t hg = std::min<uint32_t>(nb, 2u * (uint32_t)cus);
         const int hd = g_tune_sort_hd.load(std::memory_order_relaxed);  // knob 25: counting-sort bits
-#define KVH_BKH(Dv)                                                                                                \
-  hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512>), dim3(hg), dim3(512), 0, st, (const R24*)recB, (const uint32_t*)cnt, \
-                     (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,                        \
+#define KVH_BKH(Dv, W2v)                                                                                             \
+  hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512, W2v>), dim3(hg), dim3(512), 0, st, (const R24*)recB,                  \
+                     (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,   \
                      (unsigned long long*)dup_count, novf, ovf)
-        if (hd == 10) KVH_BKH(10); else if (hd == 12) KVH_BKH(12); else KVH_BKH(11);
+#ifdef KVH_EXPERIMENTS
+        if (b3 == 5) {  // the round-4 three 8-byte field rounds (A/B)
+          if (hd == 10) KVH_BKH(10, false); else if (hd == 12) KVH_BKH(12, false); else KVH_BKH(11, false);
+        } else
+#endif
+        if (hd == 10) KVH_BKH(10, true); else if (hd == 12) KVH_BKH(12, true); else KVH_BKH(11, true);
 #undef KVH_BKH
       }
 #ifdef KVH_EXPERIMENTS  // knob 23 = 1 / 2 lost their A/B (round 4): experiments build only
