@@ -1490,17 +1490,26 @@ k_tw_scan2(uint32_t* __restrict__ H2, const uint32_t* __restrict__ tbs, uint32_t
   tw_colscan<ND>(H2, tbs[d1], tbs[d1 + 1], 1u << B2, cnt + (d1 << B2), part);
 }
 
-// start[b] = start1[d1] + the sizes of d1's earlier buckets
-__global__ void __launch_bounds__(kTwD)
+// start[b] = start1[d1] + the sizes of d1's earlier buckets: one workgroup
+// per top digit d1, an exclusive scan of its 2^B2 <= 256 bucket sizes (round
+// 5: one thread per d1 walking them serially took ~50 us per sort)
+__global__ void __launch_bounds__(256)
 k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
             uint32_t* __restrict__ start) {
-  const uint32_t d1 = threadIdx.x, nb2 = 1u << B2;
-  if (d1 >= nb1) return;
-  uint32_t run = start1[d1];
-  for (uint32_t d2 = 0; d2 < nb2; d2++) {
-    start[(d1 << B2) | d2] = run;
-    run += cnt[(d1 << B2) | d2];
+  __shared__ uint32_t wsum[4];
+  const uint32_t d1 = blockIdx.x, d2 = threadIdx.x, nb2 = 1u << B2, lane = d2 & 63, w = d2 >> 6;
+  const uint32_t v = d2 < nb2 ? cnt[(d1 << B2) | d2] : 0u;
+  uint32_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += y;
   }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t wo = 0;
+  for (uint32_t q = 0; q < w; q++) wo += wsum[q];
+  if (d2 < nb2) start[(d1 << B2) | d2] = start1[d1] + wo + inc - v;
 }
 
 // MODE selects how a tile's records are read; the library launches MODE 3.
@@ -1768,7 +1777,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       else
         hipLaunchKernelGGL(k_tw_scan2<kTwD>, dim3(nb1), dim3(1024), 0, st, H2, (const uint32_t*)tbs, B2, cnt);
       if ((rc = launch_done())) return rc;
-      hipLaunchKernelGGL(k_tw_start2, dim3(1), dim3(kTwD), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
+      hipLaunchKernelGGL(k_tw_start2, dim3(nb1), dim3(256), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
                          nb1, B2, start);
       if ((rc = launch_done())) return rc;
       if (d8)
