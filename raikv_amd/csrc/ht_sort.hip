@@ -608,7 +608,12 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
 // random ds_read_b128 per record and a 16-byte output store) and the item in
 // a second, instead of three 8-byte rounds: two barriers and one ord[] read
 // fewer per record.  The union then holds 56 KiB, 63 KiB per workgroup.
-template <uint32_t CAP, int D, int T = kBkT, bool W2 = false>
+// RK (round 5): the histogram atomic returns each record's rank within its
+// digit, kept in a register, so the records are placed with one read of the
+// digit's start: no digit array and no second (returning) atomic pass --
+// two LDS accesses and one random atomic fewer per record.  hist[] then
+// holds the starts, and a run ends at the next digit's start.
+template <uint32_t CAP, int D, int T = kBkT, bool W2 = false, bool RK = false>
 __global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD (512 threads x 2 per CU spill: 87 VGPRs)
 k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
            uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
@@ -658,14 +663,19 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
 #pragma unroll
     for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
     __syncthreads();
+    uint32_t rk[RK ? PER : 1];  // RK: digit << 16 | rank within the digit
 #pragma unroll
     for (uint32_t j = 0; j < PER; j++) {
       const uint32_t r = tid + j * T;
       if (r < R) {
         const uint32_t k32 = (uint32_t)((sort_key64(g, sb, f0[j]) << B) >> 32);
         K[r] = k32;
-        dig[r] = (uint16_t)(k32 >> (32 - D));
-        atomicAdd(&hist[k32 >> (32 - D)], 1u);
+        if constexpr (RK) {
+          rk[j] = (k32 >> (32 - D)) << 16 | atomicAdd(&hist[k32 >> (32 - D)], 1u);
+        } else {
+          dig[r] = (uint16_t)(k32 >> (32 - D));
+          atomicAdd(&hist[k32 >> (32 - D)], 1u);
+        }
       }
     }
     __syncthreads();
@@ -699,13 +709,22 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
     }
     __syncthreads();
-    for (uint32_t t = tid; t < R; t += T) ord[atomicAdd(&hist[dig[t]], 1u)] = (uint16_t)t;
+    if constexpr (RK) {
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t r = tid + j * T;
+        if (r < R) ord[hist[rk[j] >> 16] + (rk[j] & 0xffffu)] = (uint16_t)r;
+      }
+    } else {
+      for (uint32_t t = tid; t < R; t += T) ord[atomicAdd(&hist[dig[t]], 1u)] = (uint16_t)t;
+    }
     __syncthreads();
-    // runs of equal digit (hist[d] is now the end of digit d): full order
+    // runs of equal digit (RK: hist[d] is the start of digit d, else its end): full order
 #pragma unroll
     for (uint32_t j = 0; j < per; j++) {
       const uint32_t d = tid * per + j;
-      const uint32_t e = hist[d], s0 = d ? hist[d - 1] : 0u;
+      const uint32_t e = RK ? (d + 1 < nd ? hist[d + 1] : R) : hist[d];
+      const uint32_t s0 = RK ? hist[d] : d ? hist[d - 1] : 0u;
       for (uint32_t a = s0 + 1; a < e; a++) {
         const uint16_t x = ord[a];
         const uint32_t kx = K[x];
@@ -1721,7 +1740,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
     // knob 23 = 3: half-size buckets (mean <= 3072, up to 15 bits: pass 2 of
     // 8 bits) for the bucket sort at two 512-thread workgroups per CU
     const int b3 = g_tune_sort_b3.load(std::memory_order_relaxed);
-    const bool half = (b3 == 3 || b3 == 5) && engine != 2;
+    const bool half = (b3 == 3 || b3 == 5 || b3 == 6) && engine != 2;
     uint32_t B = 0;
     while (B < (uint32_t)(half ? kTwMaxB : kBkMaxB) && mean_of(B) > (half ? 3072.0 : 6144.0)) B++;
     // buckets then hold ~mean +- sqrt(mean): the two-per-CU bucket sort (capacity
@@ -1796,12 +1815,19 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512, W2v>), dim3(hg), dim3(512), 0, st, (const R24*)recB,                  \
                      (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,   \
                      (unsigned long long*)dup_count, novf, ovf)
+#define KVH_BKH2(Dv)                                                                                                 \
+  hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512, true, true>), dim3(hg), dim3(512), 0, st, (const R24*)recB,          \
+                     (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,   \
+                     (unsigned long long*)dup_count, novf, ovf)
 #ifdef KVH_EXPERIMENTS
         if (b3 == 5) {  // the round-4 three 8-byte field rounds (A/B)
           if (hd == 10) KVH_BKH(10, false); else if (hd == 12) KVH_BKH(12, false); else KVH_BKH(11, false);
+        } else if (b3 == 6) {  // the round-5 W2 form before RK (A/B)
+          if (hd == 10) KVH_BKH(10, true); else if (hd == 12) KVH_BKH(12, true); else KVH_BKH(11, true);
         } else
 #endif
-        if (hd == 10) KVH_BKH(10, true); else if (hd == 12) KVH_BKH(12, true); else KVH_BKH(11, true);
+        if (hd == 10) KVH_BKH2(10); else if (hd == 12) KVH_BKH2(12); else KVH_BKH2(11);
+#undef KVH_BKH2
 #undef KVH_BKH
       }
 #ifdef KVH_EXPERIMENTS  // knob 23 = 1 / 2 lost their A/B (round 4): experiments build only
