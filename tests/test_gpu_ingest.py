@@ -222,6 +222,40 @@ def test_tokenize_hash_fused_vs_oracle(kvh, max_token):
         np.testing.assert_array_equal(host(hc), G["hashes"][:100])
 
 
+def _token_text(rng, n, lo, hi):
+    """Tokens of lo..hi-1 bytes separated by single separators."""
+    parts, size = [], 0
+    while size < n:
+        k = int(rng.integers(lo, hi))
+        parts.append(bytes(rng.integers(33, 127, k, dtype=np.uint8)))
+        parts.append(bytes(rng.choice(np.frombuffer(b" \n\t", dtype=np.uint8), 1)))
+        size += k + 1
+    return np.frombuffer(b"".join(parts)[:n], dtype=np.uint8).copy()
+
+
+@pytest.mark.parametrize("lo,hi", [(1, 2), (14, 18), (15, 32), (28, 36), (30, 300), (1, 40)])
+def test_tokenize_hash_length_mixes(kvh, lo, hi):
+    """Token-length mixes that load each path of the span hash: one-byte
+    tokens (512 per tokenizer pass), all-medium tokens (the medium queue
+    flushing every chunk), the short/medium seam at 15/16 and the
+    medium/long seam at 31/32 hashed bytes, mostly long tokens, and a cap
+    that cuts the tokens mid-chunk.  Poisoned outputs, against the oracle."""
+    rng = np.random.default_rng(lo * 1000 + hi)
+    for shift, n, nul in ((0, 1 << 19, True), (7, 200003, False)):
+        arr = np.concatenate([np.full(shift, 35, np.uint8), _token_text(rng, n, lo, hi)])
+        dev = torch.from_numpy(arr).cuda()[shift:]
+        wo, wl = orc_tokenize(ORC, arr[shift:], 256)
+        want = orc_hash_spans(ORC, arr[shift:], wo, wl, SEED, nul=nul)
+        o, l, h = kvh.tokenize_hash(dev, SEED, 256, nulterm=nul)
+        np.testing.assert_array_equal(host(o), wo)
+        np.testing.assert_array_equal(host(l), wl)
+        np.testing.assert_array_equal(host(h), want)
+        cap = int(wo.size * 0.6) + 7
+        o, l, h = kvh.tokenize_hash(dev, SEED, 256, cap=cap, nulterm=nul)
+        np.testing.assert_array_equal(host(o), wo[:cap])
+        np.testing.assert_array_equal(host(h), want[:cap])
+
+
 def test_tokenize_hash_large_text(kvh):
     """1 GiB of f3 text: one-call hashes equal tokenize + span hash, bit for bit."""
     n = 1 << 30
