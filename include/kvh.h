@@ -306,7 +306,12 @@ int kvh_meow128_fixed_positions(const void *keys, uint32_t key_len, size_t n,
  * then input order, all duplicates are adjacent and the count is the true
  * one (reference fixtures:
  * 99 vs 500 on the 600-entry table, 992 vs 1000 on a 64 MiB one; tests/golden/
- * sort_*.npz).  Not a bit-identical drop-in for kv_ht_radix_sort.
+ * sort_*.npz).  That default is not a bit-identical drop-in for
+ * kv_ht_radix_sort.  KVH_REF_ORDER (n <= 65536, ctest's batch sizes) and
+ * kvh_ht_sort_batched ARE: they step RadixSort::sort's own algorithm
+ * (radix_sort.h:89-298) on the device and leave the reference's exact
+ * element order, so the duplicate count is the reference's too (99 on the
+ * 600-entry fixture).
  * ------------------------------------------------------------------- */
 #define KVH_DEDUP     0x8u  /* zero h1 of an element equal (h1,h2) to its successor, count it */
 #define KVH_REF_ORDER 0x10u /* kvh_ht_sort: the reference's exact element order, n <= 65536 */
@@ -335,10 +340,27 @@ int kvh_ht_sort(const uint64_t *hashes, const uint64_t *items, size_t n,
                 const kvh_ht_geom_t *geom, uint64_t *hashes_out,
                 uint64_t *items_out, uint64_t *dup_count, uint32_t flags,
                 void *scratch, size_t scratch_bytes, void *stream);
+/* Many kv_ht_radix_sort calls in one launch (ctest sorts its fragments in
+ * batches, test/ctest.c:34, :90, then marks duplicates, :96-104): the n
+ * pairs are cut into batches of `batch` (1..65536; the last may be
+ * shorter), and each batch is sorted on its own workgroup in the
+ * reference's exact element order (KVH_REF_ORDER's algorithm), as a
+ * separate kv_ht_radix_sort call on it would leave it.  flags: KVH_DEDUP
+ * marks and counts duplicates per batch into dup_counts[b] (device u64,
+ * ceil(n / batch) entries; NULL: not written).  items NULL: the global
+ * input index.  Asynchronous on stream.  scratch: a device buffer of
+ * kvh_ht_sort_batched_scratch_bytes(n, batch) (0: batch out of range). */
+size_t kvh_ht_sort_batched_scratch_bytes(size_t n, uint32_t batch);
+int kvh_ht_sort_batched(const uint64_t *hashes, const uint64_t *items,
+                        size_t n, uint32_t batch, const kvh_ht_geom_t *geom,
+                        uint64_t *hashes_out, uint64_t *items_out,
+                        uint64_t *dup_counts, uint32_t flags, void *scratch,
+                        size_t scratch_bytes, void *stream);
 /* host form of kv_ht_radix_sort(ar, ar_size, ht) (radix_sort.h:19-20):
  * sorts ar[] in place (synchronous, on the current GPU); the table is
- * given by its geometry.  Same slot order as the reference; tie order as
- * described above (the reference's is not reproduced). */
+ * given by its geometry.  Up to 65536 elements (ctest's batches) in the
+ * reference's exact order (KVH_REF_ORDER); beyond that the same slot order
+ * with the tie order described above. */
 int kvh_ht_radix_sort(kvh_ht_sort_t *ar, uint32_t ar_size,
                       const kvh_ht_geom_t *geom);
 

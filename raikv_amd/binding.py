@@ -131,6 +131,8 @@ def _load():
         "kvh_frags_hash": (I, [P, SZ, U64, U64, U32, P, P, SZ, P, P, SZ, P]),
         "kvh_ht_sort_scratch_bytes": (SZ, [SZ]),
         "kvh_ht_sort": (I, [P, P, SZ, P, P, P, P, U32, P, SZ, P]),
+        "kvh_ht_sort_batched_scratch_bytes": (SZ, [SZ, U32]),
+        "kvh_ht_sort_batched": (I, [P, P, SZ, U32, P, P, P, P, U32, P, SZ, P]),
         "kvh_ht_radix_sort": (I, [P, U32, P]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
@@ -308,6 +310,28 @@ class HtSorter:
                               _dev_ptr(self.scratch),
                               self.scratch.numel() * 8, _stream_ptr(stream)), "kvh_ht_sort")
         return out, items_out
+
+
+def ht_sort_batched(hashes, geom: "HtGeom", batch: int = 16384, items=None, dedup: bool = False, stream=None):
+    """kvh_ht_sort_batched: the (n, 2) device pairs cut into batches of
+    `batch` (<= 65536), each in kv_ht_radix_sort's exact order (ctest's batch
+    loop, ctest.c:34, :90, :96-104) -> (hashes_out, items_out, dup_counts per
+    batch)."""
+    n = hashes.numel() // 2
+    nb = (n + batch - 1) // batch
+    sb = lib.kvh_ht_sort_batched_scratch_bytes(n, batch)
+    if sb == 0:
+        raise KvhError(f"kvh_ht_sort_batched: batch {batch} out of range")
+    scratch = torch.empty((sb + 7) // 8, dtype=torch.int64, device=hashes.device)
+    out = _new_out((n, 2), hashes)
+    items_out = _empty((n,), torch.int64, hashes.device)
+    dups = _empty((max(nb, 1),), torch.int64, hashes.device)
+    check(lib.kvh_ht_sort_batched(_dev_ptr(hashes) if n else None, _dev_ptr(items) if items is not None else None, n,
+                                  batch, C.byref(geom), _dev_ptr(out) if n else None,
+                                  _dev_ptr(items_out) if n else None, _dev_ptr(dups) if dedup else None,
+                                  KVH_DEDUP if dedup else 0, _dev_ptr(scratch), scratch.numel() * 8,
+                                  _stream_ptr(stream)), "kvh_ht_sort_batched")
+    return out, items_out, dups[:nb]
 
 
 def tokenize(text, max_token: int = 256, cap: Optional[int] = None, stream=None):

@@ -39,7 +39,7 @@ namespace {
 
 constexpr uint32_t kRefMax = 65536;  // elements per call
 constexpr uint32_t kWaveCap = 2048;  // nodes up to this size: one wave each
-constexpr int kRT = 1024, kRW = kRT / 64;
+constexpr uint32_t kSmallMax = 16384;  // batches up to this size: the small-workgroup form
 
 // node = off | count << 17 | shift << 34 (off < 2^16 + 1, count <= 2^16, shift <= 64)
 __device__ __forceinline__ uint64_t pack(uint32_t off, uint32_t cnt, uint32_t sh) {
@@ -54,18 +54,33 @@ struct WaveArea {
   uint8_t li[32];
 };
 
-constexpr uint32_t kFinLds = 32768;  // workgroup nodes up to this size keep fin[] in LDS
+// One sort per workgroup of RT threads, batches of up to MAXN elements;
+// workgroup nodes of up to FINLDS elements keep fin[] in LDS (u16), larger
+// ones in global scratch.  The single-call form (kvh_ht_sort KVH_REF_ORDER):
+// 1024 threads, 64K elements, fin in LDS up to 32K -- one workgroup per CU.
+// The batched form for batches of <= 16K: 256 threads, fin always global
+// (the walk's stores are off its dependency chain: digit, then bucket slot),
+// 36 KiB of LDS, so four sorts share a CU and their chain walks interleave.
+template <int RT_, uint32_t MAXN_, uint32_t FINLDS_>
+struct RefCfg {
+  static constexpr int RT = RT_, RW = RT_ / 64;
+  static constexpr uint32_t MAXN = MAXN_, FINLDS = FINLDS_;
+};
+using RefBig = RefCfg<1024, kRefMax, 32768>;
+using RefSmall = RefCfg<256, kSmallMax, 1>;
 
+template <class Cf>
 struct RefSmem {
+  using C = Cf;
   union {
     struct {
-      uint8_t bdig[kRefMax];   // digits of a workgroup node (the first 32 KiB when fin is in LDS)
+      uint8_t bdig[C::MAXN];   // digits of a workgroup node (the first FINLDS bytes when fin is in LDS)
     };
     struct {
-      uint8_t bdig_s[kFinLds];
-      uint16_t bfin[kFinLds];  // fin of a workgroup node of <= kFinLds elements
+      uint8_t bdig_s[C::FINLDS];
+      uint16_t bfin[C::FINLDS];  // fin of a workgroup node of <= FINLDS elements
     };
-    WaveArea w[kRW];           // per-wave slices (the two phases of a round never overlap)
+    WaveArea w[C::RW];           // per-wave slices (the two phases of a round never overlap)
   };
   uint32_t bc[256], bo[256];
   uint32_t nl[2][2];  // node counts [list][0 big, 1 small]
@@ -82,7 +97,8 @@ struct RefPtrs {  // no arrays: a dynamically indexed member would put the struc
   }
 };
 
-__device__ __forceinline__ void push(RefSmem& S, const RefPtrs& P, int nx, uint32_t off, uint32_t cnt, uint32_t sh) {
+template <class Sm>
+__device__ __forceinline__ void push(Sm& S, const RefPtrs& P, int nx, uint32_t off, uint32_t cnt, uint32_t sh) {
   // a node of < 2 elements, or with no bits left (the reference sorts equal
   // slots by nothing: no sub key), is already in place
   if (cnt < 2 || sh == 0) return;
@@ -112,8 +128,8 @@ __device__ __forceinline__ void wsync() {  // the same within one wave
 // slot's element, ... until one of bucket b comes back to the leader's slot.
 // A step is two dependent LDS reads (the digit, then its bucket's slot):
 // the walk is sequential by nature, each swap decides the next.
-template <class Fin>
-__device__ __forceinline__ void chains(RefSmem& S, const RefPtrs& P, int nx, uint32_t off, uint32_t sh2,
+template <class Sm, class Fin>
+__device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t off, uint32_t sh2,
                                        const uint8_t* dig, uint32_t* c, uint32_t* o, uint32_t nb, Fin fin) {
   const uint32_t lane = threadIdx.x & 63;
   uint32_t base = 0;
@@ -203,11 +219,13 @@ __device__ __forceinline__ void leaf(uint64_t* ls, uint8_t* li, uint32_t cnt) {
 }
 
 // one node above kWaveCap elements, the whole workgroup (uniform control flow)
-__device__ __forceinline__ void wg_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node) {
+template <class Sm>
+__device__ __forceinline__ void wg_step(Sm& S, const RefPtrs& P, int nx, uint64_t node) {
+  constexpr int kRT = Sm::C::RT;
   const uint32_t off = (uint32_t)(node & 0x1ffff), cnt = (uint32_t)((node >> 17) & 0x1ffff),
                  sh = (uint32_t)(node >> 34);
   const uint32_t tid = threadIdx.x;
-  const bool lf = cnt <= kFinLds;  // fin in LDS (u16), else in global scratch
+  const bool lf = cnt <= Sm::C::FINLDS;  // fin in LDS (u16), else in global scratch
   uint32_t* gfin = P.fin + off;
   uint16_t* lfin = S.bfin;
   auto setfin = [&](uint32_t from, uint32_t to) { if (lf) lfin[from] = (uint16_t)to; else gfin[from] = to; };
@@ -255,7 +273,8 @@ __device__ __forceinline__ void wg_step(RefSmem& S, const RefPtrs& P, int nx, ui
 }
 
 // one node of <= kWaveCap elements, one wave
-__device__ __forceinline__ void wave_step(RefSmem& S, const RefPtrs& P, int nx, uint64_t node, WaveArea& W) {
+template <class Sm>
+__device__ __forceinline__ void wave_step(Sm& S, const RefPtrs& P, int nx, uint64_t node, WaveArea& W) {
   const uint32_t off = (uint32_t)(node & 0x1ffff), cnt = (uint32_t)((node >> 17) & 0x1ffff),
                  sh = (uint32_t)(node >> 34);
   const uint32_t lane = threadIdx.x & 63;
@@ -317,11 +336,24 @@ __device__ __forceinline__ void wave_step(RefSmem& S, const RefPtrs& P, int nx, 
   wsync();
 }
 
-__global__ void __launch_bounds__(kRT)
-k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ items, uint32_t n, HtGeom g,
-          uint32_t bits, uint64_t* __restrict__ h_out, uint64_t* __restrict__ items_out,
-          unsigned long long* __restrict__ dup_count, uint32_t dedup, uint8_t* __restrict__ scratch) {
-  __shared__ RefSmem S;
+template <class Cf>
+__global__ void __launch_bounds__(Cf::RT)
+k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ items, uint64_t ntot, uint32_t B,
+          HtGeom g, uint32_t bits, uint64_t* __restrict__ h_out, uint64_t* __restrict__ items_out,
+          unsigned long long* __restrict__ dup_count, uint32_t dedup, uint8_t* __restrict__ scratch,
+          uint64_t sstride) {
+  // workgroup b sorts batch b: elements [b * B, min(ntot, (b + 1) * B)), on its own scratch slice
+  // (one batch, the kvh_ht_sort form: B = ntot, one workgroup)
+  const uint64_t b0 = (uint64_t)blockIdx.x * B;
+  const uint32_t n = (uint32_t)(ntot - b0 < B ? ntot - b0 : B);
+  hashes += 2 * b0;
+  if (items) items += b0;
+  h_out += 2 * b0;
+  if (items_out) items_out += b0;
+  if (dup_count) dup_count += blockIdx.x;
+  scratch += blockIdx.x * sstride;
+  constexpr int kRT = Cf::RT, kRW = Cf::RW;
+  __shared__ RefSmem<Cf> S;
   const uint32_t tid = threadIdx.x, wv = tid >> 6;
   RefPtrs P;
   {
@@ -376,7 +408,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
     }
     h_out[2 * (size_t)k] = h1;
     h_out[2 * (size_t)k + 1] = h2;
-    if (items_out) items_out[k] = items ? items[i] : (uint64_t)i;
+    if (items_out) items_out[k] = items ? items[i] : b0 + i;
   }
   if (dedup) {
     if (local) atomicAdd(&S.dups, (unsigned long long)local);
@@ -395,20 +427,64 @@ size_t refsort_scratch_bytes(size_t n) {
   return 16 * n + 32 * cap + 12 * n + 256;
 }
 
-int refsort_launch(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh_ht_geom_t* geom,
-                   uint64_t* h_out, uint64_t* items_out, uint64_t* dup_count, bool dedup, void* scratch,
-                   size_t scratch_bytes, hipStream_t st) {
-  if (n > kRefMax || scratch_bytes < refsort_scratch_bytes(n)) return set_err(KVH_EINVAL);
+namespace {
+HtGeom ref_geom(const kvh_ht_geom_t* geom, uint32_t* bits) {
   HtGeom g;
   g.size = geom->ht_size;
   g.mask = geom->ht_mod_mask;
   g.frac = (uint32_t)geom->ht_mod_fraction;
   g.shift = geom->ht_mod_shift;
   g.buckets = geom->cuckoo_buckets;
-  uint32_t bits = 1;  // radix_sort.h:75-77: 1 + floor(log2 ht_size)
-  for (uint64_t m = geom->ht_size; m > 1; m >>= 1) bits++;
-  hipLaunchKernelGGL(k_refsort, dim3(1), dim3(kRT), 0, st, hashes, items, (uint32_t)n, g, bits, h_out, items_out,
-                     (unsigned long long*)(dedup ? dup_count : nullptr), dedup ? 1u : 0u, (uint8_t*)scratch);
+  uint32_t b = 1;  // radix_sort.h:75-77: 1 + floor(log2 ht_size)
+  for (uint64_t m = geom->ht_size; m > 1; m >>= 1) b++;
+  *bits = b;
+  return g;
+}
+}  // namespace
+
+int refsort_launch(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh_ht_geom_t* geom,
+                   uint64_t* h_out, uint64_t* items_out, uint64_t* dup_count, bool dedup, void* scratch,
+                   size_t scratch_bytes, hipStream_t st) {
+  if (n > kRefMax || scratch_bytes < refsort_scratch_bytes(n)) return set_err(KVH_EINVAL);
+  uint32_t bits;
+  const HtGeom g = ref_geom(geom, &bits);
+  hipLaunchKernelGGL(k_refsort<RefBig>, dim3(1), dim3(RefBig::RT), 0, st, hashes, items, (uint64_t)n, (uint32_t)n, g, bits, h_out,
+                     items_out, (unsigned long long*)(dedup ? dup_count : nullptr), dedup ? 1u : 0u,
+                     (uint8_t*)scratch, (uint64_t)0);
+  return launch_done();
+}
+
+// per-batch scratch slices, 256-byte aligned
+static size_t batch_stride(uint32_t batch) { return (refsort_scratch_bytes(batch) + 255) & ~(size_t)255; }
+
+size_t refsort_batched_scratch_bytes(size_t n, uint32_t batch) {
+  if (batch == 0 || batch > kRefMax) return 0;
+  const size_t nb = (n + batch - 1) / batch;
+  return (nb ? nb : 1) * batch_stride(batch);  // nonzero for every valid batch size, n = 0 included
+}
+
+int refsort_batched_launch(const uint64_t* hashes, const uint64_t* items, size_t n, uint32_t batch,
+                           const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out, uint64_t* dup_counts,
+                           bool dedup, void* scratch, size_t scratch_bytes, hipStream_t st) {
+  if (batch == 0 || batch > kRefMax || n >= (1ull << 40)) return set_err(KVH_EINVAL);
+  if (n == 0) return set_err(0);
+  if (scratch_bytes < refsort_batched_scratch_bytes(n, batch)) return set_err(KVH_EINVAL);
+  const uint64_t nb = (n + batch - 1) / batch;
+  if (nb > 0x7fffffffull) return set_err(KVH_EINVAL);
+  uint32_t bits;
+  const HtGeom g = ref_geom(geom, &bits);
+  int cus = 0;
+  if (int rc = device_cus(&cus)) return rc;
+  // up to one batch per CU: the 1024-thread form is faster per batch (2.5 vs 3.8 ms at 16K);
+  // beyond that four 256-thread sorts per CU give twice the throughput
+  if (batch <= kSmallMax && nb > (uint64_t)cus)
+    hipLaunchKernelGGL(k_refsort<RefSmall>, dim3((uint32_t)nb), dim3(RefSmall::RT), 0, st, hashes, items, (uint64_t)n,
+                       batch, g, bits, h_out, items_out, (unsigned long long*)(dedup ? dup_counts : nullptr),
+                       dedup ? 1u : 0u, (uint8_t*)scratch, (uint64_t)batch_stride(batch));
+  else
+    hipLaunchKernelGGL(k_refsort<RefBig>, dim3((uint32_t)nb), dim3(RefBig::RT), 0, st, hashes, items, (uint64_t)n,
+                       batch, g, bits, h_out, items_out, (unsigned long long*)(dedup ? dup_counts : nullptr),
+                       dedup ? 1u : 0u, (uint8_t*)scratch, (uint64_t)batch_stride(batch));
   return launch_done();
 }
 

@@ -173,6 +173,51 @@ def test_ref_order_every_step_vs_oracle(kvh):
         assert int(srt.dups.item()) == wd
 
 
+@pytest.mark.parametrize("batch,nb", [(16384, 3), (5000, 3), (32, 3), (65536, 3), (64, 301), (4096, 300)])
+def test_batched_ref_order_vs_oracle(kvh, batch, nb):
+    """kvh_ht_sort_batched: ctest's batch loop (ctest.c:34, :90, :96-104) in
+    one launch -- every batch equals a separate exact-order sort of it (the
+    pinned restatement), duplicate counts per batch, global input indices as
+    items, a short last batch; poisoned outputs.  Up to one batch per CU runs
+    the 1024-thread form, more (nb = 300, 301) the 256-thread form."""
+    rng = np.random.default_rng(batch + nb)
+    ms = 5 << 20
+    g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
+    og = orc_geom(ORC, ms, 64, 1.0, 4, 4)
+    n = nb * batch + batch // 3 + 7
+    h = rng.integers(0, 2 ** 64, size=(n, 2), dtype=np.uint64)
+    h[rng.integers(0, n, n // 50)] = h[rng.integers(0, n, n // 50)]  # duplicates, some across batches
+    oh, oi, dc = kvh.ht_sort_batched(dev(h), g, batch=batch, dedup=True)
+    oh, oi, dc = host(oh), host(oi), host(dc)
+    assert dc.size == (n + batch - 1) // batch
+    check = range(dc.size) if dc.size < 20 or batch <= 64 else \
+        sorted(set([0, 1, dc.size - 2, dc.size - 1] + list(rng.integers(0, dc.size, 12))))
+    for b in check:
+        lo, hi = b * batch, min(n, (b + 1) * batch)
+        wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, h[lo:hi], dedup=True)
+        np.testing.assert_array_equal(oi[lo:hi], wi + np.uint64(lo), err_msg=f"batch {b}")
+        np.testing.assert_array_equal(oh[lo:hi], wh, err_msg=f"batch {b}")
+        assert int(dc[b]) == wd
+    # items carried, no dedup
+    items = rng.integers(0, 2 ** 63, n, dtype=np.uint64)
+    oh, oi, _ = kvh.ht_sort_batched(dev(h), g, batch=batch, items=dev(items))
+    oh, oi = host(oh), host(oi)
+    lo, hi = batch, min(n, 2 * batch)
+    wh, wi, _ = orc_ht_radix_sort_ref(ORC, og, h[lo:hi], items=items[lo:hi])
+    np.testing.assert_array_equal(oi[lo:hi], wi)
+    np.testing.assert_array_equal(oh[lo:hi], wh)
+
+
+def test_batched_bounds(kvh):
+    g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
+    assert kvh.lib.kvh_ht_sort_batched_scratch_bytes(1000, 0) == 0
+    assert kvh.lib.kvh_ht_sort_batched_scratch_bytes(1000, 65537) == 0
+    with pytest.raises(kvh.KvhError):
+        kvh.ht_sort_batched(dev(np.ones((10, 2), dtype=np.uint64)), g, batch=65537)
+    oh, oi, dc = kvh.ht_sort_batched(dev(np.zeros((0, 2), dtype=np.uint64)), g, batch=16384, dedup=True)
+    assert oh.shape[0] == 0 and dc.numel() == 0
+
+
 def test_ref_order_bounds(kvh):
     g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
     srt = kvh.HtSorter(g, 65537)

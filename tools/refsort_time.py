@@ -43,3 +43,30 @@ for n in (1024, 4096, 16384, 65536):
                                     h.ctypes.data, n, d.ctypes.data) for _ in range(20)]
         res["reference_cpu_ms_1core"] = float(np.median(ts)) * 1e3
     print(json.dumps(res), flush=True)
+
+# ctest's batch loop in one launch (kvh_ht_sort_batched): throughput over
+# many 16K batches, one workgroup per batch, against the same sort on one core
+for nb in (1, 64, 1024):
+    n = nb * 16384
+    h = rng.integers(0, 2 ** 64, size=(n, 2), dtype=np.uint64)
+    dh = torch.from_numpy(h.view(np.int64)).cuda()
+    for _ in range(3):
+        kvh.ht_sort_batched(dh, geom, batch=16384, dedup=True)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    a.record()
+    for _ in range(reps):
+        kvh.ht_sort_batched(dh, geom, batch=16384, dedup=True)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    res = {"batched_16k": nb, "n": n, "ms": ms, "G_pairs_s": n / ms / 1e6}
+    if ref is not None:
+        d = np.zeros(1, np.uint64)
+        hb = np.ascontiguousarray(h[:16384])
+        t1 = float(np.median([ref.ref_ht_sort_bench(geom.ht_size, geom.ht_mod_mask, geom.ht_mod_fraction,
+                                                    geom.ht_mod_shift, hb.ctypes.data, 16384, d.ctypes.data)
+                              for _ in range(10)]))
+        res["reference_cpu_G_pairs_s_1core"] = 16384 / t1 / 1e9
+    print(json.dumps(res), flush=True)

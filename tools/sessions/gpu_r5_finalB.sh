@@ -2,7 +2,7 @@
 # Round-5 measurement, part B: rocprofv3 kernel-trace summaries of the bench
 # commands (timed-dispatch averages) and the PMC passes, per config.
 set -o pipefail
-O=${1:-gpurun_out/r5finalB}; PCFGS=${2:-"c1 c2 c3 c4 c64 f1 f2 f3 f4"}
+O=${1:-gpurun_out/r5finalB}; PCFGS=${2:-"c1 c2 c3 c4 c64 f1 f2 f3 f4 f4v"}
 cd ${GRAFT_REPO_ROOT:-.}; mkdir -p $O; export TMPDIR=/tmp
 tools/make_profiles.sh $O/prof $PCFGS || exit 1
 for c in $PCFGS; do python3 tools/timed_avg.py $O/prof/$c/trace 20 > $O/prof/$c/timed_avg.json || exit 1; done
