@@ -147,3 +147,23 @@ tools/scatter2_real: tools/scatter2_real.hip raikv_amd/csrc/ht_sort.hip $(PROBE_
 # f2 pass-2 write-pattern probe
 tools/scatter2_probe: tools/scatter2_probe.hip
 	$(HIPCC) $(HIPFLAGS) -Wno-unused-result -o $@ $<
+
+# Host-code sanitizers (AddressSanitizer + UndefinedBehaviorSanitizer on the
+# host side only; the device code is built as usual): the library and the C++
+# programs that drive its host paths -- pipelines, ticket pool, streams,
+# graphs, the C++ API -- for a run on the GPU box (tools/sessions/gpu_r5_asan.sh)
+ASAN_DIR  := tools/asan
+ASAN_HOST := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer
+ASAN_OBJS := $(patsubst raikv_amd/csrc/%.hip,$(ASAN_DIR)/obj/%.o,$(SRCS))
+ASAN_CXX  := /opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=address,undefined -fno-gpu-sanitize -fno-omit-frame-pointer
+ASAN_PROGS := $(ASAN_DIR)/streams_gpu $(ASAN_DIR)/e2e_host $(ASAN_DIR)/paths_gpu $(ASAN_DIR)/hash_test_gpu
+$(ASAN_DIR)/obj/%.o: raikv_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(ASAN_DIR)/obj
+	$(HIPCC) $(HIPFLAGS) $(ASAN_HOST) $(INC) -c -o $@ $<
+$(ASAN_DIR)/libkvh.so: $(ASAN_OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) $(ASAN_HOST) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(ASAN_OBJS)
+$(ASAN_DIR)/%: tests/cpp/%.cpp $(ASAN_DIR)/libkvh.so include/kvh.h include/raikv_amd/key_hash.hpp oracle
+	$(ASAN_CXX) $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L $(ASAN_DIR) -lkvh -L oracle -loracle -L/opt/rocm/lib -lamdhip64 -lpthread -ldl \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../oracle' -Wl,-rpath,/opt/rocm/lib
+asan: $(ASAN_PROGS)
