@@ -167,3 +167,20 @@ $(ASAN_DIR)/%: tests/cpp/%.cpp $(ASAN_DIR)/libkvh.so include/kvh.h include/raikv
 	    -L $(ASAN_DIR) -lkvh -L oracle -loracle -L/opt/rocm/lib -lamdhip64 -lpthread -ldl \
 	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../oracle' -Wl,-rpath,/opt/rocm/lib
 asan: $(ASAN_PROGS)
+
+# ThreadSanitizer on the host code, for the multi-threaded programs (the
+# streams program's host threads and the multi-pipeline host path)
+TSAN_DIR  := tools/tsan
+TSAN_HOST := -Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer
+TSAN_OBJS := $(patsubst raikv_amd/csrc/%.hip,$(TSAN_DIR)/obj/%.o,$(SRCS))
+TSAN_CXX  := /opt/rocm/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=thread -fno-gpu-sanitize -fno-omit-frame-pointer
+$(TSAN_DIR)/obj/%.o: raikv_amd/csrc/%.hip $(HDRS)
+	@mkdir -p $(TSAN_DIR)/obj
+	$(HIPCC) $(HIPFLAGS) $(TSAN_HOST) $(INC) -c -o $@ $<
+$(TSAN_DIR)/libkvh.so: $(TSAN_OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) $(TSAN_HOST) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(TSAN_OBJS)
+$(TSAN_DIR)/%: tests/cpp/%.cpp $(TSAN_DIR)/libkvh.so include/kvh.h oracle
+	$(TSAN_CXX) $(INC) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -o $@ $< \
+	    -L $(TSAN_DIR) -lkvh -L oracle -loracle -L/opt/rocm/lib -lamdhip64 -lpthread -ldl \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../oracle' -Wl,-rpath,/opt/rocm/lib
+tsan: $(TSAN_DIR)/streams_gpu $(TSAN_DIR)/e2e_host
