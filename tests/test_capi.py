@@ -40,6 +40,29 @@ def test_binding_loads_without_gpu():
     assert raikv_amd.lib.kvh_set_tuning(0, 3) == -22
 
 
+def test_batched_sort_scratch_and_validation_without_gpu():
+    """kvh_ht_sort_batched's scratch size and argument checks are host-only:
+    batch 1..65536, one slice per batch (a nonzero size for n = 0), and the
+    bad calls fail before any device work."""
+    import ctypes as C
+    import raikv_amd
+    lib = raikv_amd.lib
+    assert lib.kvh_ht_sort_batched_scratch_bytes(1000, 0) == 0
+    assert lib.kvh_ht_sort_batched_scratch_bytes(1000, 65537) == 0
+    one = lib.kvh_ht_sort_batched_scratch_bytes(16384, 16384)
+    assert one > 0 and one % 256 == 0
+    assert lib.kvh_ht_sort_batched_scratch_bytes(0, 16384) == one
+    assert lib.kvh_ht_sort_batched_scratch_bytes(16385, 16384) == 2 * one
+    assert lib.kvh_ht_sort_batched_scratch_bytes(1024 * 16384, 16384) == 1024 * one
+    g = raikv_amd.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
+    # geometry missing, unknown flags, NULL buffers with n > 0, batch out of range
+    assert lib.kvh_ht_sort_batched(None, None, 0, 16384, None, None, None, None, 0, None, 0, None) == -22
+    assert lib.kvh_ht_sort_batched(None, None, 0, 16384, C.byref(g), None, None, None, 0x4, None, 0, None) == -22
+    assert lib.kvh_ht_sort_batched(None, None, 10, 16384, C.byref(g), None, None, None, 0, None, 0, None) == -22
+    assert lib.kvh_ht_sort_batched(None, None, 0, 0, C.byref(g), None, None, None, 0, None, 0, None) == -22
+    assert lib.kvh_ht_sort_batched(None, None, 0, 16384, C.byref(g), None, None, None, 0x8, None, 0, None) == 0
+
+
 def test_product_library_exports_only_the_header():
     """libkvh.so exports exactly what include/kvh.h declares; the research
     kernels and ablation builds (outputs that are not hashes) are not
