@@ -346,9 +346,10 @@ int kvh_ht_sort(const uint64_t *hashes, const uint64_t *items, size_t n,
  * shorter), and each batch is sorted on its own workgroup in the
  * reference's exact element order (KVH_REF_ORDER's algorithm), as a
  * separate kv_ht_radix_sort call on it would leave it.  flags: KVH_DEDUP
- * marks and counts duplicates per batch into dup_counts[b] (device u64,
- * ceil(n / batch) entries; NULL: not written).  items NULL: the global
- * input index.  Asynchronous on stream.  scratch: a device buffer of
+ * marks and counts duplicates per batch: dup_counts[b] (device u64,
+ * ceil(n / batch) entries; NULL: not written) gets batch b's count (0
+ * without KVH_DEDUP).  items NULL: the global input index.  Asynchronous
+ * on stream.  scratch: a device buffer of
  * kvh_ht_sort_batched_scratch_bytes(n, batch) (0: batch out of range). */
 size_t kvh_ht_sort_batched_scratch_bytes(size_t n, uint32_t batch);
 int kvh_ht_sort_batched(const uint64_t *hashes, const uint64_t *items,
@@ -356,6 +357,19 @@ int kvh_ht_sort_batched(const uint64_t *hashes, const uint64_t *items,
                         uint64_t *hashes_out, uint64_t *items_out,
                         uint64_t *dup_counts, uint32_t flags, void *scratch,
                         size_t scratch_bytes, void *stream);
+/* The same over batches of any sizes: batch b is elements [seg_offs[b],
+ * seg_offs[b+1]) (device u64, nseg + 1 entries, non-decreasing), each of
+ * at most max_seg (1..65536) elements -- ctest's batches end when 16K frags
+ * or its 64 KiB frag buffer fill (ctest.c:31-34, :214-222).  A batch longer
+ * than max_seg is left unsorted and flagged dup_counts[b] = ~0.  scratch:
+ * kvh_ht_sort_segments_scratch_bytes(nseg, max_seg). */
+size_t kvh_ht_sort_segments_scratch_bytes(size_t nseg, uint32_t max_seg);
+int kvh_ht_sort_segments(const uint64_t *hashes, const uint64_t *items,
+                         const uint64_t *seg_offs, size_t nseg,
+                         uint32_t max_seg, const kvh_ht_geom_t *geom,
+                         uint64_t *hashes_out, uint64_t *items_out,
+                         uint64_t *dup_counts, uint32_t flags, void *scratch,
+                         size_t scratch_bytes, void *stream);
 /* host form of kv_ht_radix_sort(ar, ar_size, ht) (radix_sort.h:19-20):
  * sorts ar[] in place (synchronous, on the current GPU); the table is
  * given by its geometry.  Up to 65536 elements (ctest's batches) in the

@@ -18,6 +18,7 @@ from .binding import (  # noqa: F401
     frags_hash,
     HtSorter,
     ht_sort_batched,
+    ht_sort_segments,
     KVH_DEDUP,
     KVH_REF_ORDER,
     set_poison_outputs,
@@ -52,5 +53,5 @@ __all__ = [
     "meow128_multiseed", "meow128_var_seeded", "meow128_fixed_host", "meow128_var_host", "meow128_host_multi", "shard_bounds", "host_empty", "kv_hash_meow128",
     "kv_hash_meow64", "HashSeed", "KeyFragment", "STATIC_SEED", "KVH_POS32", "HtGeom", "ht_positions",
     "meow128_fixed_positions", "crc_c_fixed", "crc_c_var", "kv_crc_c",
-    "tokenize", "tokenize_hash", "frag_offsets", "frags_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "ht_sort_batched", "KVH_DEDUP", "KVH_REF_ORDER", "set_poison_outputs",
+    "tokenize", "tokenize_hash", "frag_offsets", "frags_hash", "meow128_spans", "meow128_frags", "KVH_NULTERM", "HtSorter", "ht_sort_batched", "ht_sort_segments", "KVH_DEDUP", "KVH_REF_ORDER", "set_poison_outputs",
 ]

@@ -133,6 +133,8 @@ def _load():
         "kvh_ht_sort": (I, [P, P, SZ, P, P, P, P, U32, P, SZ, P]),
         "kvh_ht_sort_batched_scratch_bytes": (SZ, [SZ, U32]),
         "kvh_ht_sort_batched": (I, [P, P, SZ, U32, P, P, P, P, U32, P, SZ, P]),
+        "kvh_ht_sort_segments_scratch_bytes": (SZ, [SZ, U32]),
+        "kvh_ht_sort_segments": (I, [P, P, P, SZ, U32, P, P, P, P, U32, P, SZ, P]),
         "kvh_ht_radix_sort": (I, [P, U32, P]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
@@ -328,10 +330,33 @@ def ht_sort_batched(hashes, geom: "HtGeom", batch: int = 16384, items=None, dedu
     dups = _empty((max(nb, 1),), torch.int64, hashes.device)
     check(lib.kvh_ht_sort_batched(_dev_ptr(hashes) if n else None, _dev_ptr(items) if items is not None else None, n,
                                   batch, C.byref(geom), _dev_ptr(out) if n else None,
-                                  _dev_ptr(items_out) if n else None, _dev_ptr(dups) if dedup else None,
+                                  _dev_ptr(items_out) if n else None, _dev_ptr(dups),
                                   KVH_DEDUP if dedup else 0, _dev_ptr(scratch), scratch.numel() * 8,
                                   _stream_ptr(stream)), "kvh_ht_sort_batched")
     return out, items_out, dups[:nb]
+
+
+def ht_sort_segments(hashes, geom: "HtGeom", seg_offs, max_seg: int = 16384, items=None, dedup: bool = False,
+                     stream=None):
+    """kvh_ht_sort_segments: batches of any sizes, batch b = pairs
+    [seg_offs[b], seg_offs[b+1]) (int64 device tensor, nseg + 1 entries), each
+    in kv_ht_radix_sort's exact order -> (hashes_out, items_out, dup_counts;
+    ~0 flags a batch longer than max_seg)."""
+    n = hashes.numel() // 2
+    nseg = max(seg_offs.numel() - 1, 0)
+    sb = lib.kvh_ht_sort_segments_scratch_bytes(nseg, max_seg)
+    if sb == 0:
+        raise KvhError(f"kvh_ht_sort_segments: max_seg {max_seg} out of range")
+    scratch = torch.empty((sb + 7) // 8, dtype=torch.int64, device=hashes.device)
+    out = _new_out((n, 2), hashes)
+    items_out = _empty((n,), torch.int64, hashes.device)
+    dups = _empty((max(nseg, 1),), torch.int64, hashes.device)
+    check(lib.kvh_ht_sort_segments(_dev_ptr(hashes) if n else None, _dev_ptr(items) if items is not None else None,
+                                   _dev_ptr(seg_offs) if nseg else None, nseg, max_seg, C.byref(geom),
+                                   _dev_ptr(out) if n else None, _dev_ptr(items_out) if n else None, _dev_ptr(dups),
+                                   KVH_DEDUP if dedup else 0, _dev_ptr(scratch), scratch.numel() * 8,
+                                   _stream_ptr(stream)), "kvh_ht_sort_segments")
+    return out, items_out, dups[:nseg]
 
 
 def tokenize(text, max_token: int = 256, cap: Optional[int] = None, stream=None):

@@ -339,13 +339,25 @@ __device__ __forceinline__ void wave_step(Sm& S, const RefPtrs& P, int nx, uint6
 template <class Cf>
 __global__ void __launch_bounds__(Cf::RT)
 k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ items, uint64_t ntot, uint32_t B,
-          HtGeom g, uint32_t bits, uint64_t* __restrict__ h_out, uint64_t* __restrict__ items_out,
-          unsigned long long* __restrict__ dup_count, uint32_t dedup, uint8_t* __restrict__ scratch,
-          uint64_t sstride) {
-  // workgroup b sorts batch b: elements [b * B, min(ntot, (b + 1) * B)), on its own scratch slice
-  // (one batch, the kvh_ht_sort form: B = ntot, one workgroup)
-  const uint64_t b0 = (uint64_t)blockIdx.x * B;
-  const uint32_t n = (uint32_t)(ntot - b0 < B ? ntot - b0 : B);
+          const uint64_t* __restrict__ segs, HtGeom g, uint32_t bits, uint64_t* __restrict__ h_out,
+          uint64_t* __restrict__ items_out, unsigned long long* __restrict__ dup_count, uint32_t dedup,
+          uint8_t* __restrict__ scratch, uint64_t sstride) {
+  // workgroup b sorts batch b: elements [b * B, min(ntot, (b + 1) * B)), or with segs the
+  // segment [segs[b], segs[b + 1]) of at most B elements, on its own scratch slice (one batch,
+  // the kvh_ht_sort form: B = ntot, one workgroup).  dup_count[b], when given, gets the batch's
+  // duplicate count (0 without dedup); a segment longer than B (or reversed) is left unsorted and
+  // flagged with ~0.
+  uint64_t b0 = (uint64_t)blockIdx.x * B, nb64 = ntot - b0 < B ? ntot - b0 : B;
+  if (segs) {
+    b0 = segs[blockIdx.x];
+    const uint64_t e = segs[blockIdx.x + 1];
+    nb64 = e - b0;
+    if (e < b0 || nb64 > B) {  // workgroup-uniform
+      if (threadIdx.x == 0 && dup_count) dup_count[blockIdx.x] = ~0ull;
+      return;
+    }
+  }
+  const uint32_t n = (uint32_t)nb64;
   hashes += 2 * b0;
   if (items) items += b0;
   h_out += 2 * b0;
@@ -410,11 +422,9 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
     h_out[2 * (size_t)k + 1] = h2;
     if (items_out) items_out[k] = items ? items[i] : b0 + i;
   }
-  if (dedup) {
-    if (local) atomicAdd(&S.dups, (unsigned long long)local);
-    __syncthreads();
-    if (tid == 0 && dup_count) *dup_count = S.dups;
-  }
+  if (dedup && local) atomicAdd(&S.dups, (unsigned long long)local);
+  __syncthreads();
+  if (tid == 0 && dup_count) *dup_count = dedup ? S.dups : 0ull;
 }
 
 }  // namespace
@@ -448,9 +458,10 @@ int refsort_launch(const uint64_t* hashes, const uint64_t* items, size_t n, cons
   if (n > kRefMax || scratch_bytes < refsort_scratch_bytes(n)) return set_err(KVH_EINVAL);
   uint32_t bits;
   const HtGeom g = ref_geom(geom, &bits);
-  hipLaunchKernelGGL(k_refsort<RefBig>, dim3(1), dim3(RefBig::RT), 0, st, hashes, items, (uint64_t)n, (uint32_t)n, g, bits, h_out,
-                     items_out, (unsigned long long*)(dedup ? dup_count : nullptr), dedup ? 1u : 0u,
-                     (uint8_t*)scratch, (uint64_t)0);
+  hipLaunchKernelGGL(k_refsort<RefBig>, dim3(1), dim3(RefBig::RT), 0, st, hashes, items, (uint64_t)n, (uint32_t)n,
+                     (const uint64_t*)nullptr, g, bits, h_out, items_out,
+                     (unsigned long long*)(dedup ? dup_count : nullptr), dedup ? 1u : 0u, (uint8_t*)scratch,
+                     (uint64_t)0);
   return launch_done();
 }
 
@@ -463,6 +474,26 @@ size_t refsort_batched_scratch_bytes(size_t n, uint32_t batch) {
   return (nb ? nb : 1) * batch_stride(batch);  // nonzero for every valid batch size, n = 0 included
 }
 
+// one workgroup per batch: up to one batch per CU the 1024-thread form is faster per batch (2.5 vs
+// 3.8 ms at 16K); beyond that four 256-thread sorts per CU give twice the throughput
+static int launch_many(const uint64_t* hashes, const uint64_t* items, uint64_t ntot, uint32_t B,
+                       const uint64_t* segs, uint64_t nb, const kvh_ht_geom_t* geom, uint64_t* h_out,
+                       uint64_t* items_out, uint64_t* dup_counts, bool dedup, void* scratch, hipStream_t st) {
+  uint32_t bits;
+  const HtGeom g = ref_geom(geom, &bits);
+  int cus = 0;
+  if (int rc = device_cus(&cus)) return rc;
+  if (B <= kSmallMax && nb > (uint64_t)cus)
+    hipLaunchKernelGGL(k_refsort<RefSmall>, dim3((uint32_t)nb), dim3(RefSmall::RT), 0, st, hashes, items, ntot, B,
+                       segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+  else
+    hipLaunchKernelGGL(k_refsort<RefBig>, dim3((uint32_t)nb), dim3(RefBig::RT), 0, st, hashes, items, ntot, B,
+                       segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+  return launch_done();
+}
+
 int refsort_batched_launch(const uint64_t* hashes, const uint64_t* items, size_t n, uint32_t batch,
                            const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out, uint64_t* dup_counts,
                            bool dedup, void* scratch, size_t scratch_bytes, hipStream_t st) {
@@ -471,21 +502,22 @@ int refsort_batched_launch(const uint64_t* hashes, const uint64_t* items, size_t
   if (scratch_bytes < refsort_batched_scratch_bytes(n, batch)) return set_err(KVH_EINVAL);
   const uint64_t nb = (n + batch - 1) / batch;
   if (nb > 0x7fffffffull) return set_err(KVH_EINVAL);
-  uint32_t bits;
-  const HtGeom g = ref_geom(geom, &bits);
-  int cus = 0;
-  if (int rc = device_cus(&cus)) return rc;
-  // up to one batch per CU: the 1024-thread form is faster per batch (2.5 vs 3.8 ms at 16K);
-  // beyond that four 256-thread sorts per CU give twice the throughput
-  if (batch <= kSmallMax && nb > (uint64_t)cus)
-    hipLaunchKernelGGL(k_refsort<RefSmall>, dim3((uint32_t)nb), dim3(RefSmall::RT), 0, st, hashes, items, (uint64_t)n,
-                       batch, g, bits, h_out, items_out, (unsigned long long*)(dedup ? dup_counts : nullptr),
-                       dedup ? 1u : 0u, (uint8_t*)scratch, (uint64_t)batch_stride(batch));
-  else
-    hipLaunchKernelGGL(k_refsort<RefBig>, dim3((uint32_t)nb), dim3(RefBig::RT), 0, st, hashes, items, (uint64_t)n,
-                       batch, g, bits, h_out, items_out, (unsigned long long*)(dedup ? dup_counts : nullptr),
-                       dedup ? 1u : 0u, (uint8_t*)scratch, (uint64_t)batch_stride(batch));
-  return launch_done();
+  return launch_many(hashes, items, n, batch, nullptr, nb, geom, h_out, items_out, dup_counts, dedup, scratch, st);
+}
+
+size_t refsort_segments_scratch_bytes(size_t nseg, uint32_t max_seg) {
+  if (max_seg == 0 || max_seg > kRefMax) return 0;
+  return (nseg ? nseg : 1) * batch_stride(max_seg);
+}
+
+int refsort_segments_launch(const uint64_t* hashes, const uint64_t* items, const uint64_t* seg_offs, size_t nseg,
+                            uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out,
+                            uint64_t* dup_counts, bool dedup, void* scratch, size_t scratch_bytes, hipStream_t st) {
+  if (max_seg == 0 || max_seg > kRefMax || nseg > 0x7fffffffull) return set_err(KVH_EINVAL);
+  if (nseg == 0) return set_err(0);
+  if (!seg_offs || scratch_bytes < refsort_segments_scratch_bytes(nseg, max_seg)) return set_err(KVH_EINVAL);
+  return launch_many(hashes, items, ~0ull, max_seg, seg_offs, nseg, geom, h_out, items_out, dup_counts, dedup,
+                     scratch, st);
 }
 
 }  // namespace rt

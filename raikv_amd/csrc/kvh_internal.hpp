@@ -210,6 +210,10 @@ int stream_tickets(hipStream_t st, unsigned long long** tk);
 // kvh_stream_release: synchronise `st` and hand its ticket words back
 int stream_release(hipStream_t st);
 // kv_ht_radix_sort's exact order on the device, n <= 64K (ht_refsort.hip)
+size_t refsort_segments_scratch_bytes(size_t nseg, uint32_t max_seg);
+int refsort_segments_launch(const uint64_t* hashes, const uint64_t* items, const uint64_t* seg_offs, size_t nseg,
+                            uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out,
+                            uint64_t* dup_counts, bool dedup, void* scratch, size_t scratch_bytes, hipStream_t st);
 size_t refsort_batched_scratch_bytes(size_t n, uint32_t batch);
 int refsort_batched_launch(const uint64_t* hashes, const uint64_t* items, size_t n, uint32_t batch,
                            const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out, uint64_t* dup_counts,

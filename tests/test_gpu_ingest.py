@@ -272,6 +272,52 @@ def test_tokenize_hash_large_text(kvh):
     assert torch.equal(h, h2)
 
 
+def test_ctest_pipeline_on_device(kvh):
+    """ctest's whole ingest on the device, as raikv's test program runs it
+    (ctest.c:73-104, :202-233) over one input block: tokenize, NUL-terminated frag hashes with the
+    table's seed (kvh_tokenize_hash), then each of ctest's batches in
+    kv_ht_radix_sort's exact order with its adjacent-duplicate marking
+    (kvh_ht_sort_segments).  Every batch equals the pinned restatement of the
+    reference sort, some also the reference compiled from its sources, and
+    the total is ctest's dup_count."""
+    from ctest_batches import ctest_batches
+    from oracle_lib import load_ref_ht, orc_geom, orc_ht_radix_sort_ref, ref_ht_sort
+    rng = np.random.default_rng(11)
+    ms = 64 << 20
+    og = orc_geom(ORC, ms, 64, 1.0, 4, 4)
+    g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
+    ref = load_ref_ht()
+    # the golden text (the reference's own hashes pinned above) and 3 MB of words, many repeated
+    words = [bytes(rng.integers(97, 123, int(k), dtype=np.uint8)) for k in rng.integers(1, 14, 4000)]
+    parts = [words[int(i)] + (b" " if j % 9 else b"\n") for j, i in enumerate(rng.integers(0, 4000, 400000))]
+    for text in (G["text"], np.frombuffer(b"".join(parts), dtype=np.uint8).copy()):
+        dt = torch.from_numpy(text).cuda()
+        o, l, h = kvh.tokenize_hash(dt, SEED, 256)
+        lens = host(l)
+        cuts = ctest_batches(lens)
+        hs, oi, dc = kvh.ht_sort_segments(h.contiguous(), g, dev64(cuts), max_seg=16 * 1024, dedup=True)
+        hs, oi, dc, hh = host(hs).reshape(-1, 2), host(oi), host(dc), host(h).reshape(-1, 2)
+        total = 0
+        for b in range(len(cuts) - 1):
+            lo, hi = int(cuts[b]), int(cuts[b + 1])
+            wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, hh[lo:hi], dedup=True)
+            np.testing.assert_array_equal(oi[lo:hi], wi + np.uint64(lo), err_msg=f"batch {b}")
+            np.testing.assert_array_equal(hs[lo:hi], wh, err_msg=f"batch {b}")
+            assert int(dc[b]) == wd
+            if ref is not None and b < 3:  # the reference's own kv_ht_radix_sort + ctest marking
+                rh, ri, rd = ref_ht_sort(ref, ms, hh[lo:hi])
+                np.testing.assert_array_equal(hs[lo:hi], rh)
+                np.testing.assert_array_equal(oi[lo:hi], ri + np.uint64(lo))
+                assert int(dc[b]) == rd
+            total += wd
+        assert int(dc.sum()) == total
+    assert total > 0 and len(cuts) > 10
+
+
+def dev64(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64)).cuda()
+
+
 def _pack_frags(rng, lens, truncate=0):
     """kv_key_frag_t records {u16 keylen, bytes, pad to 2} back to back."""
     parts, offs, o = [], [], 0

@@ -208,6 +208,38 @@ def test_batched_ref_order_vs_oracle(kvh, batch, nb):
     np.testing.assert_array_equal(oh[lo:hi], wh)
 
 
+@pytest.mark.parametrize("nseg", [40, 300])
+def test_segments_vs_oracle(kvh, nseg):
+    """kvh_ht_sort_segments: batches of any sizes (0, 1, 2, 31, 32, 2049,
+    16384 and random ones), each equal to a separate exact-order sort of it,
+    per-batch duplicate counts; a batch longer than max_seg is flagged ~0 and
+    the others are unaffected.  nseg 40 runs the 1024-thread form, 300 the
+    256-thread form."""
+    rng = np.random.default_rng(nseg)
+    ms = 64 << 20
+    g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
+    og = orc_geom(ORC, ms, 64, 1.0, 4, 4)
+    sizes = list(rng.integers(0, 3000, nseg))
+    sizes[:8] = [0, 1, 2, 31, 32, 2049, 16384, 0]
+    big = 5
+    sizes[big] = 16385  # longer than max_seg
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    n = int(offs[-1])
+    h = rng.integers(0, 2 ** 64, size=(n, 2), dtype=np.uint64)
+    h[rng.integers(0, n, n // 40)] = h[rng.integers(0, n, n // 40)]
+    oh, oi, dc = kvh.ht_sort_segments(dev(h), g, dev(offs), max_seg=16384, dedup=True)
+    oh, oi, dc = host(oh), host(oi), host(dc)
+    assert dc.size == nseg and int(dc[big]) == 2 ** 64 - 1
+    for b in range(nseg):
+        if b == big:
+            continue
+        lo, hi = int(offs[b]), int(offs[b + 1])
+        wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, h[lo:hi], dedup=True)
+        np.testing.assert_array_equal(oi[lo:hi], wi + np.uint64(lo), err_msg=f"segment {b}")
+        np.testing.assert_array_equal(oh[lo:hi], wh, err_msg=f"segment {b}")
+        assert int(dc[b]) == wd, b
+
+
 def test_batched_bounds(kvh):
     g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
     assert kvh.lib.kvh_ht_sort_batched_scratch_bytes(1000, 0) == 0
