@@ -68,6 +68,7 @@ struct RefCfg {
 };
 using RefBig = RefCfg<1024, kRefMax, 32768>;
 using RefSmall = RefCfg<256, kSmallMax, 1>;
+using RefTiny = RefCfg<128, kSmallMax, 1>;  // 19 KiB: eight sorts per CU
 
 template <class Cf>
 struct RefSmem {
@@ -483,7 +484,11 @@ static int launch_many(const uint64_t* hashes, const uint64_t* items, uint64_t n
   const HtGeom g = ref_geom(geom, &bits);
   int cus = 0;
   if (int rc = device_cus(&cus)) return rc;
-  if (B <= kSmallMax && nb > (uint64_t)cus)
+  if (B <= kSmallMax && nb > 4 * (uint64_t)cus && knob(g_tune_refwg) != 256)
+    hipLaunchKernelGGL(k_refsort<RefTiny>, dim3((uint32_t)nb), dim3(RefTiny::RT), 0, st, hashes, items, ntot, B,
+                       segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+  else if (B <= kSmallMax && nb > (uint64_t)cus)
     hipLaunchKernelGGL(k_refsort<RefSmall>, dim3((uint32_t)nb), dim3(RefSmall::RT), 0, st, hashes, items, ntot, B,
                        segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
                        (uint8_t*)scratch, (uint64_t)batch_stride(B));

@@ -173,13 +173,15 @@ def test_ref_order_every_step_vs_oracle(kvh):
         assert int(srt.dups.item()) == wd
 
 
-@pytest.mark.parametrize("batch,nb", [(16384, 3), (5000, 3), (32, 3), (65536, 3), (64, 301), (4096, 300)])
+@pytest.mark.parametrize("batch,nb", [(16384, 3), (5000, 3), (32, 3), (65536, 3), (64, 301), (4096, 300),
+                                      (64, 1100), (2048, 1030)])
 def test_batched_ref_order_vs_oracle(kvh, batch, nb):
     """kvh_ht_sort_batched: ctest's batch loop (ctest.c:34, :90, :96-104) in
     one launch -- every batch equals a separate exact-order sort of it (the
     pinned restatement), duplicate counts per batch, global input indices as
     items, a short last batch; poisoned outputs.  Up to one batch per CU runs
-    the 1024-thread form, more (nb = 300, 301) the 256-thread form."""
+    the 1024-thread form, up to four per CU (nb = 300, 301) the 256-thread
+    form, more (1030, 1100) the 128-thread form."""
     rng = np.random.default_rng(batch + nb)
     ms = 5 << 20
     g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
@@ -208,13 +210,13 @@ def test_batched_ref_order_vs_oracle(kvh, batch, nb):
     np.testing.assert_array_equal(oh[lo:hi], wh)
 
 
-@pytest.mark.parametrize("nseg", [40, 300])
+@pytest.mark.parametrize("nseg", [40, 300, 1100])
 def test_segments_vs_oracle(kvh, nseg):
     """kvh_ht_sort_segments: batches of any sizes (0, 1, 2, 31, 32, 2049,
     16384 and random ones), each equal to a separate exact-order sort of it,
     per-batch duplicate counts; a batch longer than max_seg is flagged ~0 and
     the others are unaffected.  nseg 40 runs the 1024-thread form, 300 the
-    256-thread form."""
+    256-thread form, 1100 the 128-thread form."""
     rng = np.random.default_rng(nseg)
     ms = 64 << 20
     g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
