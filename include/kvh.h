@@ -542,8 +542,8 @@ int         kvh_stream_release(void *stream);
  * Returns the previous value or KVH_EINVAL.  The kernels that lost their A/B
  * (knobs 0 and 3: tables per LDS and keys per lane other than the per-length
  * defaults; knob 7 = 7, 13, 24, 25, 44, 45, 47-50; knob 14 = 1-5; knob 23 =
- * 1, 2, 5, 6; knob 24 = 3-5; knob 27 = 256, the exact-order batched sort
- * without its 128-thread form) and the ablation builds whose outputs are not
+ * 1, 2, 5, 6; knob 24 = 3-5; knob 27 = 128, 256: the exact-order batched
+ * sort's earlier many-batch forms) and the ablation builds whose outputs are not
  * hashes exist only in the experiments build, tools/libkvh_exp.so, never in
  * libkvh.so, which rejects those values. */
 int         kvh_set_tuning(int knob, int value);

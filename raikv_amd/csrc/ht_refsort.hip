@@ -46,9 +46,10 @@ __device__ __forceinline__ uint64_t pack(uint32_t off, uint32_t cnt, uint32_t sh
   return (uint64_t)off | ((uint64_t)cnt << 17) | ((uint64_t)sh << 34);
 }
 
+template <uint32_t WCAP>
 struct WaveArea {
-  uint8_t dig[kWaveCap];
-  uint16_t fin[kWaveCap];
+  uint8_t dig[WCAP];
+  uint16_t fin[WCAP];
   uint32_t c[256], o[256];
   uint64_t ls[32];
   uint8_t li[32];
@@ -58,17 +59,24 @@ struct WaveArea {
 // workgroup nodes of up to FINLDS elements keep fin[] in LDS (u16), larger
 // ones in global scratch.  The single-call form (kvh_ht_sort KVH_REF_ORDER):
 // 1024 threads, 64K elements, fin in LDS up to 32K -- one workgroup per CU.
-// The batched form for batches of <= 16K: 256 threads, fin always global
-// (the walk's stores are off its dependency chain: digit, then bucket slot),
-// 36 KiB of LDS, so four sorts share a CU and their chain walks interleave.
-template <int RT_, uint32_t MAXN_, uint32_t FINLDS_>
+// The many-batch form for batches of <= 16K (RefMany): 256 threads, fin
+// always global (the walk's stores are off its dependency chain: digit, then
+// bucket slot), wave nodes up to 512 elements, 18 KiB of LDS, so seven or
+// eight sorts share a CU and their chain walks interleave.
+template <int RT_, uint32_t MAXN_, uint32_t FINLDS_, uint32_t WCAP_ = kWaveCap>
 struct RefCfg {
   static constexpr int RT = RT_, RW = RT_ / 64;
-  static constexpr uint32_t MAXN = MAXN_, FINLDS = FINLDS_;
+  static constexpr uint32_t MAXN = MAXN_, FINLDS = FINLDS_, WCAP = WCAP_;  // WCAP: nodes up to this size: one wave
 };
 using RefBig = RefCfg<1024, kRefMax, 32768>;
-using RefSmall = RefCfg<256, kSmallMax, 1>;
-using RefTiny = RefCfg<128, kSmallMax, 1>;  // 19 KiB: eight sorts per CU
+// Many batches: 256 threads, fin always global, nodes of <= 512 elements to
+// one wave (ctest's ~8K batches split into ~34-element nodes below the
+// root): 18 KiB of LDS, seven or eight sorts per CU
+using RefMany = RefCfg<256, kSmallMax, 1, 512>;
+#ifdef KVH_EXPERIMENTS  // the forms RefMany replaced (round 5 A/B, knob 27)
+using RefSmall = RefCfg<256, kSmallMax, 1>;  // 36 KiB: four sorts per CU
+using RefTiny = RefCfg<128, kSmallMax, 1>;   // 19 KiB: eight two-wave sorts per CU
+#endif
 
 template <class Cf>
 struct RefSmem {
@@ -81,7 +89,7 @@ struct RefSmem {
       uint8_t bdig_s[C::FINLDS];
       uint16_t bfin[C::FINLDS];  // fin of a workgroup node of <= FINLDS elements
     };
-    WaveArea w[C::RW];           // per-wave slices (the two phases of a round never overlap)
+    WaveArea<C::WCAP> w[C::RW];  // per-wave slices (the two phases of a round never overlap)
   };
   uint32_t bc[256], bo[256];
   uint32_t nl[2][2];  // node counts [list][0 big, 1 small]
@@ -103,7 +111,7 @@ __device__ __forceinline__ void push(Sm& S, const RefPtrs& P, int nx, uint32_t o
   // a node of < 2 elements, or with no bits left (the reference sorts equal
   // slots by nothing: no sub key), is already in place
   if (cnt < 2 || sh == 0) return;
-  const int big = cnt > kWaveCap ? 0 : 1;
+  const int big = cnt > Sm::C::WCAP ? 0 : 1;
   const uint32_t k = atomicAdd(&S.nl[nx][big], 1u);
   P.list(nx, big)[k] = pack(off, cnt, sh);
 }
@@ -274,8 +282,8 @@ __device__ __forceinline__ void wg_step(Sm& S, const RefPtrs& P, int nx, uint64_
 }
 
 // one node of <= kWaveCap elements, one wave
-template <class Sm>
-__device__ __forceinline__ void wave_step(Sm& S, const RefPtrs& P, int nx, uint64_t node, WaveArea& W) {
+template <class Sm, class WA>
+__device__ __forceinline__ void wave_step(Sm& S, const RefPtrs& P, int nx, uint64_t node, WA& W) {
   const uint32_t off = (uint32_t)(node & 0x1ffff), cnt = (uint32_t)((node >> 17) & 0x1ffff),
                  sh = (uint32_t)(node >> 34);
   const uint32_t lane = threadIdx.x & 63;
@@ -475,8 +483,8 @@ size_t refsort_batched_scratch_bytes(size_t n, uint32_t batch) {
   return (nb ? nb : 1) * batch_stride(batch);  // nonzero for every valid batch size, n = 0 included
 }
 
-// one workgroup per batch: up to one batch per CU the 1024-thread form is faster per batch (2.5 vs
-// 3.8 ms at 16K); beyond that four 256-thread sorts per CU give twice the throughput
+// one workgroup per batch: up to one batch per CU the 1024-thread form is faster per batch; beyond
+// that seven or eight RefMany sorts per CU interleave their chain walks
 static int launch_many(const uint64_t* hashes, const uint64_t* items, uint64_t ntot, uint32_t B,
                        const uint64_t* segs, uint64_t nb, const kvh_ht_geom_t* geom, uint64_t* h_out,
                        uint64_t* items_out, uint64_t* dup_counts, bool dedup, void* scratch, hipStream_t st) {
@@ -484,12 +492,20 @@ static int launch_many(const uint64_t* hashes, const uint64_t* items, uint64_t n
   const HtGeom g = ref_geom(geom, &bits);
   int cus = 0;
   if (int rc = device_cus(&cus)) return rc;
-  if (B <= kSmallMax && nb > 4 * (uint64_t)cus && knob(g_tune_refwg) != 256)
+#ifdef KVH_EXPERIMENTS
+  const int form = knob(g_tune_refwg);
+  if (B <= kSmallMax && nb > (uint64_t)cus && form == 128)
     hipLaunchKernelGGL(k_refsort<RefTiny>, dim3((uint32_t)nb), dim3(RefTiny::RT), 0, st, hashes, items, ntot, B,
                        segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
                        (uint8_t*)scratch, (uint64_t)batch_stride(B));
-  else if (B <= kSmallMax && nb > (uint64_t)cus)
+  else if (B <= kSmallMax && nb > (uint64_t)cus && form == 256)
     hipLaunchKernelGGL(k_refsort<RefSmall>, dim3((uint32_t)nb), dim3(RefSmall::RT), 0, st, hashes, items, ntot, B,
+                       segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+  else
+#endif
+  if (B <= kSmallMax && nb > (uint64_t)cus)
+    hipLaunchKernelGGL(k_refsort<RefMany>, dim3((uint32_t)nb), dim3(RefMany::RT), 0, st, hashes, items, ntot, B,
                        segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
                        (uint8_t*)scratch, (uint64_t)batch_stride(B));
   else

@@ -183,7 +183,7 @@ struct TicketPool {
 };
 TicketPool g_tickets[kTkDev];
 std::atomic<int> g_tune_tkdbg{0};  // knob 26: test-only ticket fetch delay (tickets.hpp word 2)
-std::atomic<int> g_tune_refwg{0};  // knob 27 (experiments build): 256 = no 128-thread exact-order form
+std::atomic<int> g_tune_refwg{0};  // knob 27 (experiments build): earlier many-batch exact-order forms (128, 256)
 
 // four zeroed words of device `dev` with word 2 = dbg; caller holds P.mu
 int new_words(TicketPool& P, uint32_t dbg, unsigned long long** out) {
@@ -1127,7 +1127,7 @@ int kvh_set_tuning(int k, int value) {
     case 24: if (value < 0 || value > (kExperiments ? 5 : 2)) return KVH_EINVAL; return set(g_tune_order, value);
     case 25: if (value != 0 && value != 10 && value != 11 && value != 12) return KVH_EINVAL; return set(g_tune_sort_hd, value);
     case 26: if (value < 0 || value > 0xffff) return KVH_EINVAL; return g_tune_tkdbg.exchange(value);
-    case 27: if (!kExperiments || (value != 0 && value != 256)) return KVH_EINVAL; return set(g_tune_refwg, value);
+    case 27: if (!kExperiments || (value != 0 && value != 128 && value != 256)) return KVH_EINVAL; return set(g_tune_refwg, value);
     default: return g_exp.set_tuning ? g_exp.set_tuning(k, value) : KVH_EINVAL;
   }
 }

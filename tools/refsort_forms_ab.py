@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the exact-order batched forms beyond four batches per CU (experiments
-build, knob 27: 0 = the 128-thread form, 256 = the 256-thread form) on
+build, knob 27: 0 = the four-wave form with 512-element wave nodes, 128 = the
+two-wave form, 256 = the 256-thread form at four per CU) on
 ctest's batches of bench.py's f3 text and on 4096 uniform 16K batches;
 outputs asserted equal, medians of 5."""
 import json, os, sys
@@ -37,7 +38,7 @@ def timed(f, reps=5):
 
 
 ref = {}
-for v in (0, 256, 0, 256):
+for v in (0, 128, 256, 0, 128, 256):
     assert kvh.lib.kvh_set_tuning(27, v) >= 0
     for name, f in (("ctest_segments", lambda: kvh.ht_sort_segments(h, geom, cuts, max_seg=16384, dedup=True)),
                     ("uniform_16k_x4096", lambda: kvh.ht_sort_batched(hu, geom, batch=16384, dedup=True))):
