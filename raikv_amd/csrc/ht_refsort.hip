@@ -81,6 +81,11 @@ using RefTiny = RefCfg<128, kSmallMax, 1>;   // 19 KiB: eight two-wave sorts per
 template <class Cf>
 struct RefSmem {
   using C = Cf;
+  // first, at LDS addresses below 64 KiB: the walk's bucket words fold their
+  // base into the ds_read / ds_write offset field
+  uint32_t bc[256], bo[256];
+  uint32_t nl[2][2];  // node counts [list][0 big, 1 small]
+  unsigned long long dups;
   union {
     struct {
       uint8_t bdig[C::MAXN];   // digits of a workgroup node (the first FINLDS bytes when fin is in LDS)
@@ -91,9 +96,7 @@ struct RefSmem {
     };
     WaveArea<C::WCAP> w[C::RW];  // per-wave slices (the two phases of a round never overlap)
   };
-  uint32_t bc[256], bo[256];
-  uint32_t nl[2][2];  // node counts [list][0 big, 1 small]
-  unsigned long long dups;
+  uint8_t tail[4];  // dig[cnt] may be read (a head past its region): in the allocation
 };
 
 struct RefPtrs {  // no arrays: a dynamically indexed member would put the struct in scratch (flat accesses)
@@ -135,8 +138,13 @@ __device__ __forceinline__ void wsync() {  // the same within one wave
 // rewritten only when it is placed), so a chain is: take the element at the
 // slot, send it to the first unplaced slot o[d] of its bucket d, take that
 // slot's element, ... until one of bucket b comes back to the leader's slot.
-// A step is two dependent LDS reads (the digit, then its bucket's slot):
-// the walk is sequential by nature, each swap decides the next.
+// The walk is sequential by nature, each swap decides the next.  Each bucket
+// head is kept with the digit of the element it holds (o[d] | dig[o[d]] <<
+// 17, one LDS word), so a step is ONE LDS round trip: the word of the
+// element's bucket gives the slot and the next digit; the next bucket's word
+// and the digit behind the slot (for the head's new word) are read together.
+// (Node-relative positions are <= 65536: 17 bits.  A head past its region
+// reads a digit beyond it, never used: the counts are exact.)
 template <class Sm, class Fin>
 __device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t off, uint32_t sh2,
                                        const uint8_t* dig, uint32_t* c, uint32_t* o, uint32_t nb, Fin fin) {
@@ -152,8 +160,9 @@ __device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t
       const uint32_t y = __shfl_up(inc, d, 64);
       if (lane >= (uint32_t)d) inc += y;
     }
-    o[b] = base + inc - v;  // o has 256 entries
-    if (v > 1) push(S, P, nx, off + base + inc - v, v, sh2);
+    const uint32_t st = base + inc - v;
+    o[b] = st | (uint32_t)dig[st] << 17;  // o has 256 entries
+    if (v > 1) push(S, P, nx, off + st, v, sh2);
     base += __shfl(inc, 63, 64);
   }
   wave_lds_sync();
@@ -161,14 +170,26 @@ __device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t
     uint32_t end = 0;
     for (uint32_t b = 0; b < nb; b++) {
       end += c[b];
-      for (uint32_t q = o[b]; q < end; q++) {  // o[b] as chains from buckets < b left it
+      for (uint32_t q = o[b] & 0x1ffffu; q < end; q++) {  // o[b] as chains from buckets < b left it
         uint32_t xp = q, d = dig[q];
-        while (d != b) {
-          const uint32_t dst = o[d];
-          o[d] = dst + 1;
-          fin(xp, dst);
-          xp = dst;
-          d = dig[dst];
+        if (d != b) {
+          // the word is decoded before the loop and at the end of each step, so
+          // the loop head waits for nothing: a step's only wait is for its own
+          // two reads (LDS completes in order, the previous step's writes with them)
+          const uint32_t w0 = __builtin_amdgcn_readfirstlane(o[d]);  // waited for here, not at the loop head
+          uint32_t dst = w0 & 0x1ffffu, nd = w0 >> 17;
+          for (;;) {
+            const uint32_t wn = o[nd];  // stale if nd == d: replaced below
+            const uint32_t upd = (dst + 1) | (uint32_t)dig[dst + 1] << 17;
+            o[d] = upd;
+            fin(xp, dst);
+            xp = dst;
+            if (nd == b) break;
+            const uint32_t w = nd == d ? upd : wn;
+            d = nd;
+            dst = w & 0x1ffffu;
+            nd = w >> 17;
+          }
         }
         fin(xp, q);
       }
@@ -255,7 +276,12 @@ __device__ __forceinline__ void wg_step(Sm& S, const RefPtrs& P, int nx, uint64_
       __syncthreads();
       return;
     }
-    if (tid < 64) chains(S, P, nx, off, sh2, S.bdig, S.bc, S.bo, nb, setfin);
+    if (tid < 64) {  // the walk specialised on where fin lives (no branch per step)
+      if (lf)
+        chains(S, P, nx, off, sh2, S.bdig, S.bc, S.bo, nb, [&](uint32_t f, uint32_t t) { lfin[f] = (uint16_t)t; });
+      else
+        chains(S, P, nx, off, sh2, S.bdig, S.bc, S.bo, nb, [&](uint32_t f, uint32_t t) { gfin[f] = t; });
+    }
   } else {  // sh == 1
     for (uint32_t p = tid; p < cnt; p += kRT) {
       S.bdig[p] = (uint8_t)(P.slot[off + p] & 1);
