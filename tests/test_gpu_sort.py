@@ -242,6 +242,32 @@ def test_segments_vs_oracle(kvh, nseg):
         assert int(dc[b]) == wd, b
 
 
+def test_segments_every_step_many_batch_form(kvh):
+    """The many-batch form (more batches than CUs: 256 threads, wave nodes
+    <= 512, fin in global memory) on the batches that reach every step of
+    RadixSort::sort -- hot slots re-pushed down to no bits, clustered slots,
+    duplicates, the 1-bit pass, tails -- for each geometry, padded with small
+    batches past the CU count; against the pinned restatement."""
+    rng = np.random.default_rng(21)
+    cases = ref_order_cases(seed=21)
+    for ms in sorted(set(m for m, _ in cases)):
+        g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
+        og = orc_geom(ORC, ms, 64, 1.0, 4, 4)
+        segs = [h for m, h in cases if m == ms]
+        segs += [rng.integers(0, 2 ** 64, (int(k), 2), dtype=np.uint64) for k in rng.integers(0, 40, 400)]
+        sizes = [len(x) for x in segs]
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+        h = np.concatenate(segs).astype(np.uint64)
+        oh, oi, dc = kvh.ht_sort_segments(dev(h), g, dev(offs), max_seg=16384, dedup=True)
+        oh, oi, dc = host(oh), host(oi), host(dc)
+        for b in range(len(segs)):
+            lo, hi = int(offs[b]), int(offs[b + 1])
+            wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, h[lo:hi], dedup=True)
+            np.testing.assert_array_equal(oi[lo:hi], wi + np.uint64(lo), err_msg=f"map {ms} segment {b}")
+            np.testing.assert_array_equal(oh[lo:hi], wh, err_msg=f"map {ms} segment {b}")
+            assert int(dc[b]) == wd
+
+
 def test_batched_bounds(kvh):
     g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
     assert kvh.lib.kvh_ht_sort_batched_scratch_bytes(1000, 0) == 0
