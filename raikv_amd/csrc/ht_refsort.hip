@@ -170,8 +170,14 @@ __device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t
     uint32_t end = 0;
     for (uint32_t b = 0; b < nb; b++) {
       end += c[b];
-      for (uint32_t q = o[b] & 0x1ffffu; q < end; q++) {  // o[b] as chains from buckets < b left it
-        uint32_t xp = q, d = dig[q];
+      uint32_t q = o[b] & 0x1ffffu;  // o[b] as chains from buckets < b left it
+      // The leaders' digits are read one ahead: bucket b's unplaced slots are
+      // not written while its own chains run (those fill other buckets).
+      uint32_t dq = q < end ? (uint32_t)dig[q] : 0u;
+      for (; q < end; q++) {
+        const uint32_t dnext = dig[q + 1];  // past the region: read, never used
+        uint32_t xp = q, d = dq;
+        dq = dnext;
         if (d != b) {
           // the word is decoded before the loop and at the end of each step, so
           // the loop head waits for nothing: a step's only wait is for its own
