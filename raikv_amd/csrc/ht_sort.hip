@@ -613,7 +613,11 @@ k_bk_sort(const RT* __restrict__ recs, const uint32_t* __restrict__ cnt, const u
 // digit's start: no digit array and no second (returning) atomic pass --
 // two LDS accesses and one random atomic fewer per record.  hist[] then
 // holds the starts, and a run ends at the next digit's start.
-template <uint32_t CAP, int D, int T = kBkT, bool W2 = false, bool RK = false>
+// AB (experiments build, knob 23 = 7-10: phase ablations, outputs not sorted):
+// 1 no run insertion sort, 2 no output field rounds (linear stores of the
+// loaded records), 3 no counting sort (ord = identity), 4 no record loads
+// (records made from their index).
+template <uint32_t CAP, int D, int T = kBkT, bool W2 = false, bool RK = false, int AB = 0>
 __global__ void __launch_bounds__(T, 4)  // 4 waves per SIMD (512 threads x 2 per CU spill: 87 VGPRs)
 k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
            uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
@@ -654,10 +658,15 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       const uint32_t r = tid + j * T;
       f0[j] = f1[j] = f2[j] = 0;
       if (r < R) {  // non-temporal: read once, and they must not push the outputs out of L2
-        const uint64_t* q = (const uint64_t*)(rb + r);
-        f0[j] = __builtin_nontemporal_load(q);
-        f1[j] = __builtin_nontemporal_load(q + 1);
-        f2[j] = __builtin_nontemporal_load(q + 2);
+        if constexpr (AB == 4) {
+          const uint64_t x = (uint64_t)(base + r) * 0x9E3779B97F4A7C15ull;
+          f0[j] = x; f1[j] = x ^ 0x5555; f2[j] = base + r;
+        } else {
+          const uint64_t* q = (const uint64_t*)(rb + r);
+          f0[j] = __builtin_nontemporal_load(q);
+          f1[j] = __builtin_nontemporal_load(q + 1);
+          f2[j] = __builtin_nontemporal_load(q + 2);
+        }
       }
     }
 #pragma unroll
@@ -709,7 +718,9 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
     }
     __syncthreads();
-    if constexpr (RK) {
+    if constexpr (AB == 3) {
+      for (uint32_t t = tid; t < R; t += T) ord[t] = (uint16_t)t;
+    } else if constexpr (RK) {
 #pragma unroll
       for (uint32_t j = 0; j < PER; j++) {
         const uint32_t r = tid + j * T;
@@ -721,7 +732,7 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
     __syncthreads();
     // runs of equal digit (RK: hist[d] is the start of digit d, else its end): full order
 #pragma unroll
-    for (uint32_t j = 0; j < per; j++) {
+    for (uint32_t j = 0; j < (AB == 1 || AB == 3 ? 0u : per); j++) {
       const uint32_t d = tid * per + j;
       const uint32_t e = RK ? (d + 1 < nd ? hist[d + 1] : R) : hist[d];
       const uint32_t s0 = RK ? hist[d] : d ? hist[d - 1] : 0u;
@@ -741,6 +752,18 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       }
     }
     __syncthreads();  // ord final; the sort arrays are free for the field rounds
+    if constexpr (AB == 2) {  // linear stores of the loaded records, no LDS rounds
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t p = tid + j * T;
+        if (p < R) {
+          *(ulonglong2*)(h_out + 2 * ((uint64_t)base + p)) = make_ulonglong2(f0[j], f1[j]);
+          if (items_out) items_out[(uint64_t)base + p] = f2[j];
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     if constexpr (W2) {
 #pragma unroll
       for (uint32_t j = 0; j < PER; j++) {
@@ -817,6 +840,183 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
             items_out[(uint64_t)base + p] = v;
           }
         }
+      }
+      __syncthreads();
+    }
+  }
+  if (dedup && dups) {
+    const uint32_t t = block_sum<T>(d_total, wsum);
+    if (tid == 0 && t) atomicAdd(dups, (unsigned long long)t);
+  }
+}
+
+// B3x (round 5): k_bk_sortr with every record's (h1, h2) in LDS from the
+// start.  The phase ablations (profiles/r05/s21/) put 0.74 of the bucket
+// sort's 1.73 ms in its run insertion sort (per-thread chains of dependent
+// LDS reads over a wave's longest runs, and ties of the 32 key bits -- f2's
+// 1 % duplicate pairs -- through global loads).  Here each record ranks
+// itself in its run with independent comparisons against the pairs in LDS
+// (the 64-bit key recomputed from h1: a multiply), so nothing is chained
+// and no tie leaves the CU.  The 32-bit key array is gone (the
+// pairs replace it) and the rank comes from the histogram atomic (RK), so
+// the LDS is 56 KiB of pairs + 8 KiB of counts + 7 KiB of ranks: two
+// workgroups per CU as before.  The h1/h2 output round reads the pairs
+// already there; the items round reuses their space.
+template <uint32_t CAP, int D, int T = 512>
+__global__ void __launch_bounds__(T, 4)
+k_bk_sortx(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
+           uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
+           uint64_t* __restrict__ items_out, uint32_t dedup, unsigned long long* __restrict__ dups,
+           uint32_t* __restrict__ novf, uint32_t* __restrict__ ovf) {
+  static_assert(CAP % T == 0, "records per thread");
+  constexpr uint32_t PER = CAP / T;
+  constexpr uint32_t nd = 1u << D, per = nd / T;
+  union Pairs {
+    ulonglong2 X2[CAP];  // (h1, h2) of every record, in record order
+    uint64_t X[CAP];     // then the items, for their output round
+  };
+  __shared__ Pairs u;
+  __shared__ uint32_t hist[nd];   // digit counts -> starts
+  __shared__ uint16_t ord[CAP];   // sorted position -> record
+  __shared__ uint32_t wsum[T / 64], wmax[T / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t d_total = 0;
+  // the full order on records in LDS: key64, then (h1 << 1, h1, h2), then the position
+  auto less_at = [&](uint32_t x, uint32_t y) {
+    const ulonglong2 a = u.X2[x], b = u.X2[y];
+    const uint64_t ka = sort_key64(g, sb, a.x), kb = sort_key64(g, sb, b.x);
+    if (ka != kb) return ka < kb;
+    if (a.x != b.x || a.y != b.y) return rec_less(a.x, a.y, b.x, b.y);
+    return x < y;
+  };
+  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t R = cnt[b], base = start[b];
+    if (R == 0) continue;
+    if (R > CAP) {
+      if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+      continue;
+    }
+    const R24* rb = recs + base;
+    uint64_t f2[PER];  // items stay in registers until their round
+    uint32_t rk[PER];  // digit << 16 | rank within the digit
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tid + j * T;
+      f2[j] = 0;
+      if (r < R) {  // non-temporal: read once, and they must not push the outputs out of L2
+        const uint64_t* q = (const uint64_t*)(rb + r);
+        const uint64_t h1 = __builtin_nontemporal_load(q), h2 = __builtin_nontemporal_load(q + 1);
+        f2[j] = __builtin_nontemporal_load(q + 2);
+        u.X2[r] = make_ulonglong2(h1, h2);
+        const uint32_t k32 = (uint32_t)((sort_key64(g, sb, h1) << B) >> 32);
+        rk[j] = (k32 >> (32 - D)) << 16 | atomicAdd(&hist[k32 >> (32 - D)], 1u);
+      }
+    }
+    __syncthreads();
+    {  // exclusive scan of the digit counts, and the longest run
+      uint32_t v[per], s = 0, mx = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { v[j] = hist[tid * per + j]; s += v[j]; mx = max(mx, v[j]); }
+      uint32_t inc = s;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+      if (lane == 63) wsum[w] = inc;
+      if (lane == 0) wmax[w] = mx;
+      __syncthreads();
+      uint32_t wo = 0, bm = 0;
+      for (uint32_t q = 0; q < T / 64; q++) {
+        if (q < w) wo += wsum[q];
+        bm = max(bm, wmax[q]);
+      }
+      if (bm > kBkRun) {  // a run too long for insertion sort: the bitonic path
+        if (tid == 0) ovf[atomicAdd(novf, 1u)] = b;
+        __syncthreads();
+        continue;
+      }
+      uint32_t run = wo + inc - s;
+#pragma unroll
+      for (uint32_t j = 0; j < per; j++) { hist[tid * per + j] = run; run += v[j]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tid + j * T;
+      if (r < R) ord[hist[rk[j] >> 16] + (rk[j] & 0xffffu)] = (uint16_t)r;
+    }
+    __syncthreads();
+    // Runs of equal digit (hist[d] is the start of digit d), in the full
+    // order: each record counts the members of its run that precede it --
+    // independent LDS reads, no per-thread insertion chain -- and takes that
+    // rank as its place (the order is total: ranks are distinct).
+    uint32_t pos[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tid + j * T;
+      pos[j] = 0;
+      if (r < R) {
+        const uint32_t d = rk[j] >> 16, s0 = hist[d], e = d + 1 < nd ? hist[d + 1] : R;
+        uint32_t rank = 0;
+        if (e - s0 > 1) {
+          const ulonglong2 me = u.X2[r];
+          const uint64_t km = sort_key64(g, sb, me.x);
+          for (uint32_t a = s0; a < e; a++) {
+            const uint32_t y = ord[a];
+            const ulonglong2 o = u.X2[y];
+            const uint64_t ko = sort_key64(g, sb, o.x);
+            const bool lt = ko != km ? ko < km
+                                     : (o.x != me.x || o.y != me.y) ? rec_less(o.x, o.y, me.x, me.y) : y < r;
+            rank += (y != r && lt) ? 1u : 0u;
+          }
+        }
+        pos[j] = s0 + rank;
+      }
+    }
+    __syncthreads();  // every run read before any place is written
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tid + j * T;
+      if (r < R) ord[pos[j]] = (uint16_t)r;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {  // h1, h2 out, from the pairs already in LDS
+      const uint32_t p = tid + j * T;
+      ulonglong2 v = make_ulonglong2(0ull, 0ull);
+      if (p < R) v = u.X2[ord[p]];
+      // the successor's pair: the next lane's, a gather only at a wave's last lane
+      uint64_t n1 = (uint64_t)__shfl_down((unsigned long long)v.x, 1, 64),
+               n2 = (uint64_t)__shfl_down((unsigned long long)v.y, 1, 64);
+      if (lane == 63 && dedup && p + 1 < R) {
+        const ulonglong2 nx = u.X2[ord[p + 1]];
+        n1 = nx.x;
+        n2 = nx.y;
+      }
+      if (p < R) {
+        const bool dup = dedup && p + 1 < R && n1 == v.x && n2 == v.y;
+        d_total += dup ? 1u : 0u;
+        *(ulonglong2*)(h_out + 2 * ((uint64_t)base + p)) = make_ulonglong2(dup ? 0ull : v.x, v.y);
+      }
+    }
+    __syncthreads();
+    if (items_out) {
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t r = tid + j * T;
+        if (r < R) u.X[r] = f2[j];
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t p = tid + j * T;
+        if (p < R) items_out[(uint64_t)base + p] = u.X[ord[p]];
       }
       __syncthreads();
     }
@@ -1740,7 +1940,7 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
     // knob 23 = 3: half-size buckets (mean <= 3072, up to 15 bits: pass 2 of
     // 8 bits) for the bucket sort at two 512-thread workgroups per CU
     const int b3 = g_tune_sort_b3.load(std::memory_order_relaxed);
-    const bool half = (b3 == 3 || b3 == 5 || b3 == 6) && engine != 2;
+    const bool half = (b3 == 3 || b3 >= 5) && engine != 2;
     uint32_t B = 0;
     while (B < (uint32_t)(half ? kTwMaxB : kBkMaxB) && mean_of(B) > (half ? 3072.0 : 6144.0)) B++;
     // buckets then hold ~mean +- sqrt(mean): the two-per-CU bucket sort (capacity
@@ -1815,19 +2015,34 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
   hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512, W2v>), dim3(hg), dim3(512), 0, st, (const R24*)recB,                  \
                      (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,   \
                      (unsigned long long*)dup_count, novf, ovf)
+#define KVH_BKX(Dv)                                                                                                  \
+  hipLaunchKernelGGL((k_bk_sortx<3584, Dv, 512>), dim3(hg), dim3(512), 0, st, (const R24*)recB, (const uint32_t*)cnt, \
+                     (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,                         \
+                     (unsigned long long*)dup_count, novf, ovf)
 #define KVH_BKH2(Dv)                                                                                                 \
   hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512, true, true>), dim3(hg), dim3(512), 0, st, (const R24*)recB,          \
                      (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,   \
                      (unsigned long long*)dup_count, novf, ovf)
 #ifdef KVH_EXPERIMENTS
+#define KVH_BKAB(Dv, A)                                                                                              \
+  hipLaunchKernelGGL((k_bk_sortr<3584, Dv, 512, true, true, A>), dim3(hg), dim3(512), 0, st, (const R24*)recB,       \
+                     (const uint32_t*)cnt, (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,   \
+                     (unsigned long long*)dup_count, novf, ovf)
+        if (b3 >= 7 && b3 <= 10) {  // phase ablations, outputs not sorted
+          if (b3 == 7) KVH_BKAB(11, 1); else if (b3 == 8) KVH_BKAB(11, 2); else if (b3 == 9) KVH_BKAB(11, 3); else KVH_BKAB(11, 4);
+        } else
+#undef KVH_BKAB
         if (b3 == 5) {  // the round-4 three 8-byte field rounds (A/B)
           if (hd == 10) KVH_BKH(10, false); else if (hd == 12) KVH_BKH(12, false); else KVH_BKH(11, false);
         } else if (b3 == 6) {  // the round-5 W2 form before RK (A/B)
           if (hd == 10) KVH_BKH(10, true); else if (hd == 12) KVH_BKH(12, true); else KVH_BKH(11, true);
+        } else if (b3 == 11) {  // the W2 + RK form before the pairs stayed in LDS (A/B)
+          if (hd == 10) KVH_BKH2(10); else if (hd == 12) KVH_BKH2(12); else KVH_BKH2(11);
         } else
 #endif
-        if (hd == 10) KVH_BKH2(10); else if (hd == 12) KVH_BKH2(12); else KVH_BKH2(11);
+        if (hd == 10) KVH_BKX(10); else if (hd == 12) KVH_BKX(12); else KVH_BKX(11);
 #undef KVH_BKH2
+#undef KVH_BKX
 #undef KVH_BKH
       }
 #ifdef KVH_EXPERIMENTS  // knob 23 = 1 / 2 lost their A/B (round 4): experiments build only
