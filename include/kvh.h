@@ -534,8 +534,8 @@ int         kvh_stream_release(void *stream);
  *       variable-length, CRC32C and span kernel takes its chunks in address
  *       order through per-stream wave tickets; 1 the static per-wave order
  *       everywhere),
- *  25 = counting-sort bits of the knob-23 = 3 bucket sort (0 default = 11,
- *       10, 12),
+ *  25 = counting-sort bits of the knob-23 = 3 bucket sort (0 default = 12,
+ *       10, 11),
  *  26 = TEST ONLY: the first takers of every other wave ticket sleep
  *       value x ~4 us before fetching the next one (0 default, up to 65535);
  *       slows the in-order kernels, never changes their output.

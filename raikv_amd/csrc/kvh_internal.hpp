@@ -235,7 +235,7 @@ extern std::atomic<int> g_tune_sort_engine;
 // one-per-CU kernel (capacity 12288)
 extern std::atomic<int> g_tune_sort_cap;
 extern std::atomic<int> g_tune_refwg;    // knob 27 (experiments build): exact-order batched form A/B
-extern std::atomic<int> g_tune_sort_hd;  // knob 25: counting-sort bits of the half-size bucket sort (0 = 11, 10, 12)
+extern std::atomic<int> g_tune_sort_hd;  // knob 25: counting-sort bits of the half-size bucket sort (0 = 12, 10, 11)
 extern std::atomic<int> g_tune_sort_b3;  // knob 23: two-pass bucket sort 0 = k_bk_sort, 1 = k_bk_sortr, 2 = k_bk_sortr2, 3 = half-size buckets (up to 15 bits) and k_bk_sortr at two 512-thread workgroups per CU (default)
 // span hashing: 2 / 1 = wave-chunked kernel with the short-key path, two / one spans per lane
 // (default 2), 0 = lane per span
