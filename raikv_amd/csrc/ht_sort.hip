@@ -862,7 +862,11 @@ k_bk_sortr(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
 // the LDS is 56 KiB of pairs + 8 KiB of counts + 7 KiB of ranks: two
 // workgroups per CU as before.  The h1/h2 output round reads the pairs
 // already there; the items round reuses their space.
-template <uint32_t CAP, int D, int T = 512>
+// AB (experiments build, knob 23 = 12-15: phase ablations, outputs not
+// sorted): 1 no run ranking, 2 no output rounds (the records stored back
+// linearly), 3 no counting sort and no ranking (identity order), 4 no record
+// loads (records made from their index).
+template <uint32_t CAP, int D, int T = 512, int AB = 0>
 __global__ void __launch_bounds__(T, 4)
 k_bk_sortx(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start,
            uint32_t nb, uint32_t B, HtGeom g, uint32_t sb, uint64_t* __restrict__ h_out,
@@ -908,8 +912,16 @@ k_bk_sortx(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       f2[j] = 0;
       if (r < R) {  // non-temporal: read once, and they must not push the outputs out of L2
         const uint64_t* q = (const uint64_t*)(rb + r);
-        const uint64_t h1 = __builtin_nontemporal_load(q), h2 = __builtin_nontemporal_load(q + 1);
-        f2[j] = __builtin_nontemporal_load(q + 2);
+        uint64_t h1, h2;
+        if constexpr (AB == 4) {
+          h1 = (uint64_t)(base + r) * 0x9E3779B97F4A7C15ull;
+          h2 = h1 ^ 0x5555;
+          f2[j] = base + r;
+        } else {
+          h1 = __builtin_nontemporal_load(q);
+          h2 = __builtin_nontemporal_load(q + 1);
+          f2[j] = __builtin_nontemporal_load(q + 2);
+        }
         u.X2[r] = make_ulonglong2(h1, h2);
         const uint32_t k32 = (uint32_t)((sort_key64(g, sb, h1) << B) >> 32);
         rk[j] = (k32 >> (32 - D)) << 16 | atomicAdd(&hist[k32 >> (32 - D)], 1u);
@@ -949,9 +961,10 @@ k_bk_sortx(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
 #pragma unroll
     for (uint32_t j = 0; j < PER; j++) {
       const uint32_t r = tid + j * T;
-      if (r < R) ord[hist[rk[j] >> 16] + (rk[j] & 0xffffu)] = (uint16_t)r;
+      if (r < R) ord[AB == 3 ? r : hist[rk[j] >> 16] + (rk[j] & 0xffffu)] = (uint16_t)r;
     }
     __syncthreads();
+    if constexpr (AB != 1 && AB != 3) {
     // Runs of equal digit (hist[d] is the start of digit d), in the full
     // order: each record counts the members of its run that precede it --
     // independent LDS reads, no per-thread insertion chain -- and takes that
@@ -986,6 +999,19 @@ k_bk_sortx(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
       if (r < R) ord[pos[j]] = (uint16_t)r;
     }
     __syncthreads();
+    }  // AB
+    if constexpr (AB == 2) {  // linear stores of the records, no output rounds
+#pragma unroll
+      for (uint32_t j = 0; j < PER; j++) {
+        const uint32_t p = tid + j * T;
+        if (p < R) {
+          *(ulonglong2*)(h_out + 2 * ((uint64_t)base + p)) = u.X2[p];
+          if (items_out) items_out[(uint64_t)base + p] = f2[j];
+        }
+      }
+      __syncthreads();
+      continue;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < PER; j++) {  // h1, h2 out, from the pairs already in LDS
       const uint32_t p = tid + j * T;
@@ -2036,6 +2062,13 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
           if (hd == 10) KVH_BKH(10, false); else if (hd == 12) KVH_BKH(12, false); else KVH_BKH(11, false);
         } else if (b3 == 6) {  // the round-5 W2 form before RK (A/B)
           if (hd == 10) KVH_BKH(10, true); else if (hd == 12) KVH_BKH(12, true); else KVH_BKH(11, true);
+        } else if (b3 >= 12 && b3 <= 15) {  // k_bk_sortx phase ablations, outputs not sorted
+#define KVH_BKXAB(A)                                                                                                 \
+  hipLaunchKernelGGL((k_bk_sortx<3584, 12, 512, A>), dim3(hg), dim3(512), 0, st, (const R24*)recB, (const uint32_t*)cnt, \
+                     (const uint32_t*)start, nb, B, g, sb, h_out, items_out, dedup ? 1u : 0u,                         \
+                     (unsigned long long*)dup_count, novf, ovf)
+          if (b3 == 12) KVH_BKXAB(1); else if (b3 == 13) KVH_BKXAB(2); else if (b3 == 14) KVH_BKXAB(3); else KVH_BKXAB(4);
+#undef KVH_BKXAB
         } else if (b3 == 11) {  // the W2 + RK form before the pairs stayed in LDS (A/B)
           if (hd == 10) KVH_BKH2(10); else if (hd == 12) KVH_BKH2(12); else KVH_BKH2(11);
         } else
