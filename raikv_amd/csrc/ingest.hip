@@ -117,6 +117,38 @@ __device__ __forceinline__ uint32_t wave_sum_scan(uint32_t v, uint32_t lane) {
   return v;
 }
 
+// The same scans and neighbour moves on DPP (the wave tokenizer, k_tok2):
+// row shifts, then row broadcasts 15 and 31 (GFX9 data-parallel primitives),
+// instead of ds_bpermute round trips through the LDS crossbar.  Lanes with
+// no source keep `fill`.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp(uint32_t v, uint32_t fill) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, CTRL, ROWS, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v, uint32_t fill) { return dpp<0x138>(v, fill); }  // wave_shr:1
+__device__ __forceinline__ uint32_t lane_next(uint32_t v, uint32_t fill) { return dpp<0x130>(v, fill); }  // wave_shl:1
+__device__ __forceinline__ int32_t dpp_max_scan32(int32_t v) {  // inclusive, over the wave's 64 lanes
+  constexpr uint32_t id = 0x80000000u;  // INT32_MIN
+  auto mx = [](int32_t a, uint32_t b) { return a > (int32_t)b ? a : (int32_t)b; };
+  v = mx(v, dpp<0x111>((uint32_t)v, id));  // row_shr:1
+  v = mx(v, dpp<0x112>((uint32_t)v, id));  // row_shr:2
+  v = mx(v, dpp<0x114>((uint32_t)v, id));  // row_shr:4
+  v = mx(v, dpp<0x118>((uint32_t)v, id));  // row_shr:8
+  v = mx(v, dpp<0x142, 0xa>((uint32_t)v, id));  // row_bcast:15 into rows 1, 3
+  v = mx(v, dpp<0x143, 0xc>((uint32_t)v, id));  // row_bcast:31 into rows 2, 3
+  return v;
+}
+__device__ __forceinline__ uint32_t dpp_sum_scan(uint32_t v) {  // inclusive
+  v += dpp<0x111>(v, 0u);
+  v += dpp<0x112>(v, 0u);
+  v += dpp<0x114>(v, 0u);
+  v += dpp<0x118>(v, 0u);
+  v += dpp<0x142, 0xa>(v, 0u);
+  v += dpp<0x143, 0xc>(v, 0u);
+  return v;
+}
+__device__ __forceinline__ uint32_t lane_get(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
 // One kernel for both passes.  Per 16-byte segment: separator mask W,
 // token starts S = ~W & (W << 1 | ws before), token ends E = ~W & (W >> 1 |
 // ws after << 15).  A token is attributed to its END; its start is the
@@ -296,9 +328,9 @@ k_tok2(const uint8_t* __restrict__ t, TokGeo G, uint32_t max_token, uint64_t* __
 #pragma unroll
     for (uint32_t d = 0; d + 1 < kPf; d++) raw[d] = raw[d + 1];
     if (ps + 1 + kPf < kTok2Passes) raw[kPf - 1] = seg_ld(G, g0 + (ps + 1 + kPf) * 64 + lane);
-    const uint32_t Wp = __shfl_up(Wc, 1, 64), Wn = __shfl_down(Wc, 1, 64);
-    const uint32_t prev63 = ps ? (uint32_t)__shfl(prevW, 63, 64) >> 15 & 1u : before_chunk;
-    const uint32_t next0 = ps + 1 < kTok2Passes ? (uint32_t)__shfl(Wnx, 0, 64) & 1u : after_chunk;
+    const uint32_t Wp = lane_prev(Wc, 0u), Wn = lane_next(Wc, 0u);
+    const uint32_t prev63 = ps ? lane_get(prevW, 63) >> 15 & 1u : before_chunk;
+    const uint32_t next0 = ps + 1 < kTok2Passes ? lane_get(Wnx, 0) & 1u : after_chunk;
     const uint32_t before = lane ? (Wp >> 15) & 1u : prev63;
     const uint32_t after = lane < 63 ? Wn & 1u : next0;
     const uint32_t S = ~Wc & ((Wc << 1) | before) & 0xffffu;
@@ -307,12 +339,11 @@ k_tok2(const uint8_t* __restrict__ t, TokGeo G, uint32_t max_token, uint64_t* __
     // (-1: none in the pass so far, then the carry from earlier passes)
     const int64_t pp = p + (int64_t)(16 * 64 * ps);
     const int32_t mine = S ? (int32_t)(16 * lane + 31 - __builtin_clz(S)) : -1;
-    const int32_t inc = wave_max_scan32(mine, lane);
-    const int32_t up = __shfl_up(inc, 1, 64);  // all lanes: a source lane must be active
-    const int32_t exr = lane ? up : -1;
+    const int32_t inc = dpp_max_scan32(mine);
+    const int32_t exr = (int32_t)lane_prev((uint32_t)inc, 0xffffffffu);  // lane 0: -1
     const int64_t ex = exr >= 0 ? pp + exr : carry;
     {
-      const int32_t last = __shfl(inc, 63, 64);
+      const int32_t last = (int32_t)lane_get((uint32_t)inc, 63);
       if (last >= 0) carry = pp + last;
     }
     uint32_t c;
@@ -334,8 +365,8 @@ k_tok2(const uint8_t* __restrict__ t, TokGeo G, uint32_t max_token, uint64_t* __
       }
     }
     if constexpr (EMIT) {
-      const uint32_t ci = wave_sum_scan(c, lane);
-      const uint32_t tot = (uint32_t)__shfl(ci, 63, 64);
+      const uint32_t ci = dpp_sum_scan(c);
+      const uint32_t tot = lane_get(ci, 63);
       uint32_t slot = ci - c;
       for (uint32_t e = c ? E : 0u; e; e &= e - 1) {
         const uint32_t i = (uint32_t)__builtin_ctz(e);
