@@ -563,19 +563,23 @@ struct ShortRaw {
   uint32_t s, D;  // p & 15, span bytes (0: nothing loaded)
 };
 
+// a 16-byte aligned target for the lanes with nothing to load: every lane
+// issues its two loads, so the load count is the same on every path and the
+// compiler's in-order vmcnt waits never cover loads issued after the ones a
+// use needs (a branch around the loads made them wait for the next chunk's
+// offsets too)
+__device__ v4u g_no_span[1];
+
 __device__ __forceinline__ ShortRaw short_issue(const uint8_t* __restrict__ p, uint32_t D, bool load) {
   ShortRaw r;
-  const uint32_t a = (uint32_t)(uintptr_t)p & 15u;
+  const uint8_t* q = load ? p : (const uint8_t*)g_no_span;
+  const uint32_t a = (uint32_t)(uintptr_t)q & 15u;
+  const uint32_t e = load ? D - 1 : 0u;
   r.s = a;
   r.D = load ? D : 0u;
-  if (load) {  // pointer arithmetic (not integer masks) keeps these global loads
-    const uint32_t e = D - 1;
-    r.A = *(const v4u*)(p - a);
-    r.B = *(const v4u*)(p + e - ((a + e) & 15u));
-  } else {
-    r.A = v4u{0, 0, 0, 0};
-    r.B = r.A;
-  }
+  // pointer arithmetic (not integer masks) keeps these global loads
+  r.A = *(const v4u*)(q - a);
+  r.B = *(const v4u*)(q + e - ((a + e) & 15u));
   return r;
 }
 
