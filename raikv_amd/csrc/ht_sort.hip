@@ -906,23 +906,32 @@ k_bk_sortx(const R24* __restrict__ recs, const uint32_t* __restrict__ cnt, const
 #pragma unroll
     for (uint32_t j = 0; j < per; j++) hist[tid * per + j] = 0;
     __syncthreads();
+    // every record load of the bucket in flight before the first use (clamped
+    // indices, not a branch per record: a branch made each of the PER loads
+    // its own memory round trip)
+    uint64_t la[PER], lb[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; j++) {
+      const uint32_t r = tid + j * T, rc = r < R ? r : R - 1;
+      if constexpr (AB == 4) {
+        la[j] = (uint64_t)(base + r) * 0x9E3779B97F4A7C15ull;
+        lb[j] = la[j] ^ 0x5555;
+        f2[j] = base + r;
+      } else {  // non-temporal: read once, and they must not push the outputs out of L2
+        const uint64_t* q = (const uint64_t*)(rb + rc);
+        la[j] = __builtin_nontemporal_load(q);
+        lb[j] = __builtin_nontemporal_load(q + 1);
+        f2[j] = __builtin_nontemporal_load(q + 2);
+      }
+    }
 #pragma unroll
     for (uint32_t j = 0; j < PER; j++) {
       const uint32_t r = tid + j * T;
-      f2[j] = 0;
-      if (r < R) {  // non-temporal: read once, and they must not push the outputs out of L2
-        const uint64_t* q = (const uint64_t*)(rb + r);
-        uint64_t h1, h2;
-        if constexpr (AB == 4) {
-          h1 = (uint64_t)(base + r) * 0x9E3779B97F4A7C15ull;
-          h2 = h1 ^ 0x5555;
-          f2[j] = base + r;
-        } else {
-          h1 = __builtin_nontemporal_load(q);
-          h2 = __builtin_nontemporal_load(q + 1);
-          f2[j] = __builtin_nontemporal_load(q + 2);
-        }
-        u.X2[r] = make_ulonglong2(h1, h2);
+      // stored on every lane (r < CAP; slots past R are never read), so the
+      // compiler cannot sink a load into the branch below
+      u.X2[r] = make_ulonglong2(la[j], lb[j]);
+      if (r < R) {
+        const uint64_t h1 = la[j];
         const uint32_t k32 = (uint32_t)((sort_key64(g, sb, h1) << B) >> 32);
         rk[j] = (k32 >> (32 - D)) << 16 | atomicAdd(&hist[k32 >> (32 - D)], 1u);
       }
@@ -1560,11 +1569,14 @@ k_tw_hist1(const uint64_t* __restrict__ h, uint64_t n, HtGeom g, uint32_t sb, ui
   if (tid < (uint32_t)kTwD) hist[tid] = 0;
   __syncthreads();
   const uint64_t i0 = (uint64_t)tile * kTwTile;
+  // every load issued before the first use (indices clamped, not branched
+  // around: a branch made each one its own memory round trip)
+  uint64_t hv[kTwPer];
 #pragma unroll
-  for (int k = 0; k < kTwPer; k++) {
-    const uint64_t i = i0 + (uint64_t)k * kTwT + tid;
-    if (i < n) atomicAdd(&hist[bk_of(sort_key64(g, sb, h[2 * i]), B) >> B2], 1u);
-  }
+  for (int k = 0; k < kTwPer; k++) hv[k] = h[2 * min<uint64_t>(i0 + (uint64_t)k * kTwT + tid, n - 1)];
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++)
+    if (i0 + (uint64_t)k * kTwT + tid < n) atomicAdd(&hist[bk_of(sort_key64(g, sb, hv[k]), B) >> B2], 1u);
   __syncthreads();
   if (tid < nb1) H[(uint64_t)tile * nb1 + tid] = hist[tid];
 }
@@ -1579,21 +1591,23 @@ k_tw_scatter1(const uint64_t* __restrict__ h, const uint64_t* __restrict__ items
   R24 r[kTwPer];
   uint32_t dg[kTwPer], bk[kTwPer], pos[kTwPer];
   bool v[kTwPer];
+  // all the tile's loads in flight together (clamped indices; a branch
+  // around each element's loads made them four memory round trips)
 #pragma unroll
   for (int k = 0; k < kTwPer; k++) {
-    const uint64_t i = i0 + (uint64_t)k * kTwT + tid;
+    const uint64_t i = i0 + (uint64_t)k * kTwT + tid, ic = min<uint64_t>(i, n - 1);
     v[k] = i < n;
-    if (v[k]) {
-      r[k].h1 = h[2 * i];
-      r[k].h2 = h[2 * i + 1];
-      r[k].item = items ? items[i] : i;
-      bk[k] = bk_of(sort_key64(g, sb, r[k].h1), B);
-    } else {
-      bk[k] = 0;
-    }
+    r[k].h1 = h[2 * ic];
+    r[k].h2 = h[2 * ic + 1];
+    r[k].item = items ? items[ic] : i;
+  }
+  const uint32_t go = tid < nb1 ? H[(uint64_t)tile * nb1 + tid] : 0u;
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++) {
+    bk[k] = v[k] ? bk_of(sort_key64(g, sb, r[k].h1), B) : 0u;
     dg[k] = bk[k] >> B2;
   }
-  if (tid < nb1) S.gofs[tid] = H[(uint64_t)tile * nb1 + tid];
+  if (tid < nb1) S.gofs[tid] = go;
   tw_rank(dg, v, S, pos);
 #pragma unroll
   for (int k = 0; k < kTwPer; k++)
@@ -1662,7 +1676,13 @@ k_tw_hist2(const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs, co
   if (!tw_tile2(blockIdx.x, tbs, nb1, cnt1, start1, &d1, &p0, &p1)) return;  // workgroup-uniform
   if (tid < ND) hist[tid] = 0;
   __syncthreads();
-  for (uint32_t p = p0 + tid; p < p1; p += kTwT) atomicAdd(&hist[bA[p] & (nb2 - 1)], 1u);
+  // a tile is <= kTwTile = kTwPer x kTwT records: every load before the first atomic
+  uint32_t bv[kTwPer];
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++) bv[k] = bA[min(p0 + (uint32_t)k * kTwT + tid, p1 - 1)];
+#pragma unroll
+  for (int k = 0; k < kTwPer; k++)
+    if (p0 + (uint32_t)k * kTwT + tid < p1) atomicAdd(&hist[bv[k] & (nb2 - 1)], 1u);
   __syncthreads();
   if (tid < nb2) H2[(uint64_t)blockIdx.x * nb2 + tid] = hist[tid];
 }
@@ -1812,16 +1832,26 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
         r[k].h1 = p; r[k].h2 = ~(uint64_t)p; r[k].item = p;
         dg[k] = (p * 2654435761u >> 9) & (nb2 - 1);
       } else if constexpr (MODE == 3) {
-        const uint64_t* q = (const uint64_t*)(recA + p);
-        r[k].h1 = __builtin_nontemporal_load(q);
-        r[k].h2 = __builtin_nontemporal_load(q + 1);
-        r[k].item = __builtin_nontemporal_load(q + 2);
-        dg[k] = __builtin_nontemporal_load(bA + p) & (nb2 - 1);
+        // (loaded below, outside the branch)
       } else {
         r[k] = recA[p];
         dg[k] = bA[p] & (nb2 - 1);
       }
     }
+  }
+  if constexpr (MODE == 3) {  // every load of the tile in flight together: clamped, not branched around
+    uint32_t bv[kTwPer];
+#pragma unroll
+    for (int k = 0; k < kTwPer; k++) {
+      const uint32_t pc = min(p0 + (uint32_t)k * kTwT + tid, p1 - 1);
+      const uint64_t* q = (const uint64_t*)(recA + pc);
+      r[k].h1 = __builtin_nontemporal_load(q);
+      r[k].h2 = __builtin_nontemporal_load(q + 1);
+      r[k].item = __builtin_nontemporal_load(q + 2);
+      bv[k] = __builtin_nontemporal_load(bA + pc);
+    }
+#pragma unroll
+    for (int k = 0; k < kTwPer; k++) dg[k] = v[k] ? bv[k] & (nb2 - 1) : 0u;
   }
   if (tid < nb2) S.gofs[tid] = start[(d1 << B2) | tid] + H2[(uint64_t)j * nb2 + tid];
   tw_rank<ND>(dg, v, S, pos);
