@@ -291,37 +291,6 @@ __device__ __forceinline__ uint32_t crc_key_g2(const AChunks& A, uint32_t len, u
   }
   return r;
 }
-// crc_key_g2 for a key whose whole groups lie inside the buffer (A.safe):
-// the group two ahead is read clamped to the key's last group (chunk_cl)
-// instead of zero-filled, so the loop's load is one unconditional dwordx4 and
-// the compiler's in-order wait leaves it in flight (the zero-filled form's
-// branches around its loads made the loop wait for the group it had just
-// asked for, every 16 bytes).  Bytes past the key reach only T.tail, which
-// reads the low n bytes of its word.
-template <class Tab>
-__device__ __forceinline__ uint32_t crc_key_g2c(const AChunks& A, uint32_t len, uint32_t r, const Tab& T, Blk cur,
-                                                Blk nxt) {
-  uint32_t k = 0;
-  for (; 16 * k + 16 <= len; k++) {
-    const Blk nn = A.chunk_cl(k + 2);
-    const Blk b = A.piece(cur, nxt);
-    r = T.word(r, b.w[0]); r = T.word(r, b.w[1]);
-    r = T.word(r, b.w[2]); r = T.word(r, b.w[3]);
-    cur = nxt;
-    nxt = nn;
-  }
-  const uint32_t t = len - 16 * k;
-  if (t) {
-    const Blk b = A.piece(cur, nxt);
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int left = (int)t - 4 * c;
-      if (left >= 4) r = T.word(r, b.w[c]);
-      else if (left > 0) r = T.tail(r, b.w[c], (uint32_t)left);
-    }
-  }
-  return r;
-}
 template <class Tab>
 __device__ __forceinline__ uint32_t crc_key_g(const uint8_t* p, uint32_t len, bool safe, uint32_t r,
                                               const Tab& T) {
@@ -443,10 +412,8 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
         if constexpr (G == 2) {
           const uint64_t a = ws + roff_s[wv][pos];
           if (len < 65535u) {
-            const bool sf = a + len + 16 <= kend;
-            const AChunks A(keys + a, len, sf);
-            const uint32_t sd = seeds ? seeds[i0 + j] : seed;
-            crc[c] = sf ? crc_key_g2c(A, (uint32_t)len, sd, T, pf0, pf1) : crc_key_g2(A, (uint32_t)len, sd, T, pf0, pf1);
+            const AChunks A(keys + a, len, a + len + 16 <= kend);
+            crc[c] = crc_key_g2(A, (uint32_t)len, seeds ? seeds[i0 + j] : seed, T, pf0, pf1);
           } else {
             len = offs[i0 + j + 1] - offs[i0 + j];
             if (len < (1u << 31)) crc[c] = crc_key_g(keys + a, (uint32_t)len, a + len + 16 <= kend, seeds ? seeds[i0 + j] : seed, T);
