@@ -295,7 +295,11 @@ def test_ctest_pipeline_on_device(kvh):
         o, l, h = kvh.tokenize_hash(dt, SEED, 256)
         lens = host(l)
         cuts = ctest_batches(lens)
-        hs, oi, dc = kvh.ht_sort_segments(h.contiguous(), g, dev64(cuts), max_seg=16 * 1024, dedup=True)
+        segs = dev64(cuts)
+        # attribution only (the rare illegal address): a fault in the copy is
+        # reported here, one in the sort at the next host()
+        torch.cuda.synchronize()
+        hs, oi, dc = kvh.ht_sort_segments(h.contiguous(), g, segs, max_seg=16 * 1024, dedup=True)
         hs, oi, dc, hh = host(hs).reshape(-1, 2), host(oi), host(dc), host(h).reshape(-1, 2)
         total = 0
         for b in range(len(cuts) - 1):
