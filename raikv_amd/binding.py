@@ -190,11 +190,24 @@ def _np_empty(shape, dtype=np.uint64):
     return a
 
 
-def _stream_ptr(stream) -> Optional[int]:
+def _stream_ptr(stream, *keep) -> Optional[int]:
+    """The launch stream.  A caller's own stream first waits for torch's
+    current stream: this call's outputs and scratch were just allocated (and
+    poisoned) there, and the caching allocator may have handed out a block
+    that work still queued on the current stream was using.  Tensors in
+    `keep` (scratch dropped on return) are recorded on the caller's stream, so
+    the allocator does not reuse them before the launch reading them is done."""
     if stream is not None:
-        if _POISON and torch is not None and hasattr(stream, "wait_stream"):
-            stream.wait_stream(torch.cuda.current_stream())  # the poison fill first
-        return int(getattr(stream, "cuda_stream", stream))
+        ptr = int(getattr(stream, "cuda_stream", stream))
+        if torch is not None and torch.cuda.is_available():
+            cur = torch.cuda.current_stream()
+            if ptr != int(cur.cuda_stream):
+                ts = _as_torch_stream(stream)
+                ts.wait_stream(cur)
+                for t in keep:
+                    if t is not None and t.is_cuda:
+                        t.record_stream(ts)
+        return ptr
     if torch is not None and torch.cuda.is_available():
         return int(torch.cuda.current_stream().cuda_stream)
     return None
@@ -332,7 +345,7 @@ def ht_sort_batched(hashes, geom: "HtGeom", batch: int = 16384, items=None, dedu
                                   batch, C.byref(geom), _dev_ptr(out) if n else None,
                                   _dev_ptr(items_out) if n else None, _dev_ptr(dups),
                                   KVH_DEDUP if dedup else 0, _dev_ptr(scratch), scratch.numel() * 8,
-                                  _stream_ptr(stream)), "kvh_ht_sort_batched")
+                                  _stream_ptr(stream, scratch, out, items_out, dups)), "kvh_ht_sort_batched")
     return out, items_out, dups[:nb]
 
 
@@ -355,7 +368,7 @@ def ht_sort_segments(hashes, geom: "HtGeom", seg_offs, max_seg: int = 16384, ite
                                    _dev_ptr(seg_offs) if nseg else None, nseg, max_seg, C.byref(geom),
                                    _dev_ptr(out) if n else None, _dev_ptr(items_out) if n else None, _dev_ptr(dups),
                                    KVH_DEDUP if dedup else 0, _dev_ptr(scratch), scratch.numel() * 8,
-                                   _stream_ptr(stream)), "kvh_ht_sort_segments")
+                                   _stream_ptr(stream, scratch, out, items_out, dups)), "kvh_ht_sort_segments")
     return out, items_out, dups[:nseg]
 
 

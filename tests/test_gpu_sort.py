@@ -268,6 +268,42 @@ def test_segments_every_step_many_batch_form(kvh):
             assert int(dc[b]) == wd
 
 
+def test_batched_on_a_callers_stream_keeps_its_scratch(kvh):
+    """kvh_ht_sort_batched / _segments on a caller's stream return before the
+    sort has run, dropping the scratch slices that hold its element indices.
+    The binding records them (and the outputs) on that stream, so torch's
+    caching allocator does not hand them to work on the current stream while
+    the sort still reads them: here the current stream at once fills fresh
+    blocks of the same sizes with 0xFF (indices far out of range) while the
+    side stream sorts; the results equal the current-stream sort."""
+    rng = np.random.default_rng(5)
+    ms = 64 << 20
+    g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
+    batch, nb = 16384, 600
+    n = batch * nb
+    h = dev(rng.integers(0, 2 ** 64, size=(n, 2), dtype=np.uint64))
+    sizes = rng.integers(0, 16385, 700)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    offs = dev(offs[offs <= n])
+    want_b = [host(x) for x in kvh.ht_sort_batched(h, g, batch=batch, dedup=True)]
+    want_s = [host(x) for x in kvh.ht_sort_segments(h, g, offs, max_seg=16384, dedup=True)]
+    sb = kvh.lib.kvh_ht_sort_batched_scratch_bytes(n, batch)
+    ss = kvh.lib.kvh_ht_sort_segments_scratch_bytes(offs.numel() - 1, 16384)
+    side = torch.cuda.Stream()
+    for _ in range(3):
+        got_b = kvh.ht_sort_batched(h, g, batch=batch, dedup=True, stream=side)
+        got_s = kvh.ht_sort_segments(h, g, offs, max_seg=16384, dedup=True, stream=side)
+        junk = [torch.empty((b + 7) // 8, dtype=torch.int64, device="cuda") for b in (sb, ss)]
+        for j in junk:
+            j.fill_(-1)
+        del junk
+        side.synchronize()
+        for w, x in zip(want_b, got_b):
+            np.testing.assert_array_equal(host(x), w)
+        for w, x in zip(want_s, got_s):
+            np.testing.assert_array_equal(host(x), w)
+
+
 def test_batched_bounds(kvh):
     g = kvh.HtGeom.from_map(64 << 20, 64, 1.0, 4, 4)
     assert kvh.lib.kvh_ht_sort_batched_scratch_bytes(1000, 0) == 0
