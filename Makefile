@@ -68,6 +68,19 @@ $(UNO_LIB): $(UNO_OBJS) raikv_amd/csrc/kvh.map
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(UNO_OBJS)
 unordered: $(UNO_LIB)
 
+# DEBUG BUILD (not the product): the product sources with device-side bounds
+# checks (-DKVH_CHECKED; kvh_internal.hpp KVH_CHK) on the exact-order sort and
+# the ingest kernels; kvh_debug_checks reads the first failed check.  Used once
+# by tests/test_gpu_checked.py through KVH_LIB.
+CHK_LIB  := tools/libkvh_checked.so
+CHK_OBJS := $(patsubst raikv_amd/csrc/%.hip,tools/chk/%.o,$(SRCS))
+tools/chk/%.o: raikv_amd/csrc/%.hip $(HDRS)
+	@mkdir -p tools/chk
+	$(HIPCC) $(HIPFLAGS) -DKVH_CHECKED $(INC) -c -o $@ $<
+$(CHK_LIB): $(CHK_OBJS) raikv_amd/csrc/kvh.map
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(CHK_OBJS)
+checked: $(CHK_LIB)
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -135,7 +148,7 @@ clean:
 	rm -f $(LIB) $(KV_LIB) $(OBJS) $(CPP_TESTS) $(EXP_LIB) $(EXP_OBJS) $(EXP_POBJS) $(UNO_LIB) $(UNO_OBJS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle cpptests clean experiments unordered
+.PHONY: checked all oracle cpptests clean experiments unordered
 
 # f2: the real k_tw_scatter2 under ablations: ht_sort.hip
 # compiled into the probe, the product's other objects linked

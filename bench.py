@@ -382,6 +382,56 @@ def load_traffic(config_name: str):
     return None, None
 
 
+ANCHOR = "c4g"  # BASELINE configs[4]: the workload of the N > 1 lines
+
+
+def measure_anchor(kvh, seed, steps: int = 10, settle_ms: float = 300.0) -> dict:
+    """The scaling anchor: the WHOLE c4g global batch
+    (1B x 32-byte keys) hashed on this one GPU, timed like the main line
+    (settle, then `steps` launches between synchronizes; HIP events on the
+    launch stream for the kernel time).  At N = 1 it follows the C1 timed
+    region, so the default line carries the 1-GPU point of the N > 1 curve;
+    at N > 1 every rank measures it alone on its own GPU, one rank at a time."""
+    import torch
+    cfg = CONFIGS[ANCHOR]
+    n, L = cfg["n"], cfg["key_len"]
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(4242)
+    keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=gen)
+    out = torch.empty((n, 2), dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream()
+    t_s = time.perf_counter()
+    while (time.perf_counter() - t_s) * 1e3 < settle_ms:
+        kvh.meow128_fixed(keys, L, seed, out=out)
+        torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(st)
+        kvh.meow128_fixed(keys, L, seed, out=out)
+        b.record(st)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    km = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    del keys, out
+    torch.cuda.empty_cache()
+    return {"config": ANCHOR, "workload": cfg["workload"] + "; all of it on ONE GPU", "keys": n, "key_len": L,
+            "steps": steps, "ms_per_step": wall / steps * 1e3, "kernel_ms": km,
+            "hashes_per_s": n * steps / wall, "hashes_per_s_kernel": n / (km * 1e-3)}
+
+
+def anchor_efficiency(world: int, value: float, per_gpu, anchors) -> dict:
+    """Strong-scaling efficiency of an N-rank c4g line against the 1-GPU c4g
+    anchor: aggregate / (N x anchor rate), the anchors being each rank's own
+    GPU; per rank, its shard's kernel rate / its anchor's kernel rate."""
+    ref = float(np.mean([a["hashes_per_s"] for a in anchors]))
+    return {"efficiency_vs_anchor": value / (world * ref),
+            "per_rank": [{"rank": p["rank"], "efficiency_vs_anchor": p["hashes_per_s"] / a["hashes_per_s_kernel"]}
+                         for p, a in zip(per_gpu, anchors)],
+            "anchor_hashes_per_s_mean": ref}
+
+
 def free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -477,6 +527,8 @@ def main():
                     help="untimed launches before the warmup, until the engine clock has left its post-idle "
                          "power transient (DESIGN.md §4.5); 0 disables")
     ap.add_argument("--no-copy-peak", action="store_true", help="skip the achievable-peak copy probe")
+    ap.add_argument("--no-anchor", action="store_true",
+                    help="skip the 1-GPU c4g scaling anchor (measured after c1 at N=1 and by every rank at N>1)")
     ap.add_argument("--parity-keys", type=int, default=20_000,
                     help="keys of the timed launch's output checked against the reference after the timed region")
     args = ap.parse_args()
@@ -646,6 +698,19 @@ def main():
             par["full_compare"] = {"ok": False, "error": repr(e)[:300]}
     del T
     per_rank = kdist.gather({"rank": rank, "kernel_ms": kern_ms, "keys": n, "parity": par}, world)
+    # the scaling anchor: the c4g workload on ONE GPU (N = 1: after the c1 line; N > 1: each rank in turn)
+    anchors = None
+    if not args.no_anchor and ((world == 1 and args.config == "c1") or (world > 1 and cfg.get("global_batch"))):
+        a = None
+        for r in range(world):
+            kdist.barrier(world)
+            if r == rank:
+                try:
+                    a = measure_anchor(kvh, seed)
+                except Exception as e:  # reported, never hidden
+                    a = {"error": repr(e)[:300]}
+        kdist.barrier(world)
+        anchors = kdist.gather(a, world)
 
     units = cfg["tokens"] if cfg.get("ingest") else n * arity
     # keys for the f1/f3/f4 configs; a global batch counts its keys once
@@ -698,6 +763,10 @@ def main():
     if world > 1:
         res["per_gpu"] = [{"rank": p["rank"], "keys": p["keys"], "kernel_ms": p["kernel_ms"],
                            "hashes_per_s": p["keys"] * arity / (p["kernel_ms"] * 1e-3)} for p in per_rank]
+    if anchors is not None:
+        res["scaling_anchor"] = anchors[0] if world == 1 else {"per_rank": anchors}
+        if world > 1 and all("hashes_per_s" in a for a in anchors):
+            res.update(anchor_efficiency(world, value, res["per_gpu"], anchors))
     res["roofline"]["guide_copy_peak"] = GUIDE_COPY_GBS
     res["roofline"]["frac_vs_guide_copy"] = achieved / GUIDE_COPY_GBS
     if rank == 0 and world == 1 and not args.no_copy_peak:

@@ -358,14 +358,17 @@ int kvh_ht_sort_batched(const uint64_t *hashes, const uint64_t *items,
                         uint64_t *dup_counts, uint32_t flags, void *scratch,
                         size_t scratch_bytes, void *stream);
 /* The same over batches of any sizes: batch b is elements [seg_offs[b],
- * seg_offs[b+1]) (device u64, nseg + 1 entries, non-decreasing), each of
- * at most max_seg (1..65536) elements -- ctest's batches end when 16K frags
- * or its 64 KiB frag buffer fill (ctest.c:31-34, :214-222).  A batch longer
- * than max_seg is left unsorted and flagged dup_counts[b] = ~0.  scratch:
- * kvh_ht_sort_segments_scratch_bytes(nseg, max_seg). */
+ * seg_offs[b+1]) of the n pairs (device u64, nseg + 1 entries,
+ * non-decreasing, last <= n), each of at most max_seg (1..65536) elements --
+ * ctest's batches end when 16K frags or its 64 KiB frag buffer fill
+ * (ctest.c:31-34, :214-222).  The offsets are read on the device, so they
+ * are checked there: a batch longer than max_seg is copied through in input
+ * order, unmarked, and flagged dup_counts[b] = ~0; a batch that is reversed
+ * or ends past n is flagged ~0 and its output is NOT written (it may not
+ * even exist).  scratch: kvh_ht_sort_segments_scratch_bytes(nseg, max_seg). */
 size_t kvh_ht_sort_segments_scratch_bytes(size_t nseg, uint32_t max_seg);
 int kvh_ht_sort_segments(const uint64_t *hashes, const uint64_t *items,
-                         const uint64_t *seg_offs, size_t nseg,
+                         size_t n, const uint64_t *seg_offs, size_t nseg,
                          uint32_t max_seg, const kvh_ht_geom_t *geom,
                          uint64_t *hashes_out, uint64_t *items_out,
                          uint64_t *dup_counts, uint32_t flags, void *scratch,
@@ -488,13 +491,26 @@ const char *kvh_strerror(int err);
 const char *kvh_version(void);
 /* synchronise the current device (host wall-clock timing helpers) */
 int         kvh_device_synchronize(void);
+/* Bounds-checked build (`make checked`, tools/libkvh_checked.so, a debug
+ * build of these same sources): out[0..3] = (failed checks, site, value,
+ * limit) of the first failed device-side index check since the last call
+ * (exact-order sort and ingest kernels), then cleared.  Returns 1 from the
+ * checked build, 0 from the product build (which checks nothing: out is all
+ * zero), or a negative error. */
+int         kvh_debug_checks(uint64_t out[4]);
 /* Streams.  The in-order streaming kernels (fixed and variable length,
  * multi-seed, fused positions, CRC32C, span hashing) take their chunks in
- * address order through ticket words kept per (device, stream): made on a
- * stream's first call (synchronous hipMalloc / hipMemset, once per 256
- * streams), reset by each launch's last workgroup, so launches on one
+ * address order through ticket words kept per (device, stream), taken on a
+ * stream's first call from a per-device pool of 1024 sets (allocated once,
+ * on the device's first such call, and zeroed asynchronously on that call's
+ * stream: nothing on a launch synchronises the device or another stream;
+ * while the pool is dry a call takes the static chunk order, with the same
+ * results), reset by each launch's last workgroup, so launches on one
  * stream need nothing else.  hipStreamPerThread gets words per calling
- * thread.  A call on a stream that is being captured into a graph launches
+ * thread, returned when the thread exits.  That one hipMalloc per device is
+ * the only allocation: make the first call on each device before another
+ * thread starts a hipStreamCaptureModeGlobal capture.  A call on a stream
+ * that is being captured into a graph launches
  * the static-order form of its kernel (no shared words: the graph may be
  * replayed on any stream, and concurrently).  kvh_stream_release
  * synchronises `stream` and hands its words back; call it before destroying

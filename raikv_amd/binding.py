@@ -134,12 +134,13 @@ def _load():
         "kvh_ht_sort_batched_scratch_bytes": (SZ, [SZ, U32]),
         "kvh_ht_sort_batched": (I, [P, P, SZ, U32, P, P, P, P, U32, P, SZ, P]),
         "kvh_ht_sort_segments_scratch_bytes": (SZ, [SZ, U32]),
-        "kvh_ht_sort_segments": (I, [P, P, P, SZ, U32, P, P, P, P, U32, P, SZ, P]),
+        "kvh_ht_sort_segments": (I, [P, P, SZ, P, SZ, U32, P, P, P, P, U32, P, SZ, P]),
         "kvh_ht_radix_sort": (I, [P, U32, P]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
         "kvh_version": (C.c_char_p, []),
         "kvh_device_synchronize": (I, []),
+        "kvh_debug_checks": (I, [P]),
         "kvh_set_tuning": (I, [I, I]),
         "kvh_stream_release": (I, [P]),
     }
@@ -323,7 +324,9 @@ class HtSorter:
                               C.byref(self.geom), _dev_ptr(out) if n else None, _dev_ptr(items_out) if n else None,
                               _dev_ptr(self.dups), (KVH_DEDUP if dedup else 0) | (KVH_REF_ORDER if ref_order else 0),
                               _dev_ptr(self.scratch),
-                              self.scratch.numel() * 8, _stream_ptr(stream)), "kvh_ht_sort")
+                              self.scratch.numel() * 8,
+                              _stream_ptr(stream, self.scratch, self.dups, out, items_out, hashes, items)),
+              "kvh_ht_sort")
         return out, items_out
 
 
@@ -345,7 +348,8 @@ def ht_sort_batched(hashes, geom: "HtGeom", batch: int = 16384, items=None, dedu
                                   batch, C.byref(geom), _dev_ptr(out) if n else None,
                                   _dev_ptr(items_out) if n else None, _dev_ptr(dups),
                                   KVH_DEDUP if dedup else 0, _dev_ptr(scratch), scratch.numel() * 8,
-                                  _stream_ptr(stream, scratch, out, items_out, dups)), "kvh_ht_sort_batched")
+                                  _stream_ptr(stream, scratch, out, items_out, dups, hashes, items)),
+          "kvh_ht_sort_batched")
     return out, items_out, dups[:nb]
 
 
@@ -356,6 +360,8 @@ def ht_sort_segments(hashes, geom: "HtGeom", seg_offs, max_seg: int = 16384, ite
     in kv_ht_radix_sort's exact order -> (hashes_out, items_out, dup_counts;
     ~0 flags a batch longer than max_seg)."""
     n = hashes.numel() // 2
+    if not seg_offs.is_cuda or seg_offs.dtype not in (torch.int64, torch.uint64) or not seg_offs.is_contiguous():
+        raise KvhError("seg_offs: a contiguous int64/uint64 device tensor of nseg + 1 offsets")
     nseg = max(seg_offs.numel() - 1, 0)
     sb = lib.kvh_ht_sort_segments_scratch_bytes(nseg, max_seg)
     if sb == 0:
@@ -365,10 +371,11 @@ def ht_sort_segments(hashes, geom: "HtGeom", seg_offs, max_seg: int = 16384, ite
     items_out = _empty((n,), torch.int64, hashes.device)
     dups = _empty((max(nseg, 1),), torch.int64, hashes.device)
     check(lib.kvh_ht_sort_segments(_dev_ptr(hashes) if n else None, _dev_ptr(items) if items is not None else None,
-                                   _dev_ptr(seg_offs) if nseg else None, nseg, max_seg, C.byref(geom),
+                                   n, _dev_ptr(seg_offs) if nseg else None, nseg, max_seg, C.byref(geom),
                                    _dev_ptr(out) if n else None, _dev_ptr(items_out) if n else None, _dev_ptr(dups),
                                    KVH_DEDUP if dedup else 0, _dev_ptr(scratch), scratch.numel() * 8,
-                                   _stream_ptr(stream, scratch, out, items_out, dups)), "kvh_ht_sort_segments")
+                                   _stream_ptr(stream, scratch, out, items_out, dups, hashes, items, seg_offs)),
+          "kvh_ht_sort_segments")
     return out, items_out, dups[:nseg]
 
 

@@ -37,6 +37,10 @@ using namespace kvh::rt;
 
 namespace {
 
+KVH_CHK_DECL  // checked build: the first failed bounds check of this unit
+// check sites (kvh_debug_checks' out[1])
+enum : unsigned { kChkSeg = 1, kChkScratch, kChkHashes, kChkElem, kChkList, kChkDig, kChkFin, kChkOut };
+
 constexpr uint32_t kRefMax = 65536;  // elements per call
 constexpr uint32_t kWaveCap = 2048;  // nodes up to this size: one wave each
 constexpr uint32_t kSmallMax = 16384;  // batches up to this size: the small-workgroup form
@@ -63,6 +67,12 @@ struct WaveArea {
 // always global (the walk's stores are off its dependency chain: digit, then
 // bucket slot), wave nodes up to 512 elements, 18 KiB of LDS, so seven or
 // eight sorts share a CU and their chain walks interleave.
+// scratch of one sort of n elements: slot, slotT (u64), four node lists of n/2 + 2, idx, idxT, fin (u32)
+__host__ __device__ inline uint64_t refsort_need(uint64_t n) {
+  const uint64_t cap = n / 2 + 2;
+  return 16 * n + 32 * cap + 12 * n + 256;
+}
+
 template <int RT_, uint32_t MAXN_, uint32_t FINLDS_, uint32_t WCAP_ = kWaveCap>
 struct RefCfg {
   static constexpr int RT = RT_, RW = RT_ / 64;
@@ -104,6 +114,7 @@ struct RefPtrs {  // no arrays: a dynamically indexed member would put the struc
   uint32_t *idx, *idxT, *fin;
   uint64_t* lists;  // list (parity, big = 0 / small = 1) at lists + (2 parity + small) cap
   uint32_t cap;
+  uint32_t n;  // elements of this sort (the extent of slot, idx, fin)
   __device__ __forceinline__ uint64_t* list(int parity, int small) const {
     return lists + (size_t)(2 * parity + small) * cap;
   }
@@ -116,6 +127,7 @@ __device__ __forceinline__ void push(Sm& S, const RefPtrs& P, int nx, uint32_t o
   if (cnt < 2 || sh == 0) return;
   const int big = cnt > Sm::C::WCAP ? 0 : 1;
   const uint32_t k = atomicAdd(&S.nl[nx][big], 1u);
+  KVH_CHK(k < P.cap && off + cnt <= P.n, kChkList, k, P.cap);
   P.list(nx, big)[k] = pack(off, cnt, sh);
 }
 
@@ -147,7 +159,10 @@ __device__ __forceinline__ void wsync() {  // the same within one wave
 // reads a digit beyond it, never used: the counts are exact.)
 template <class Sm, class Fin>
 __device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t off, uint32_t sh2,
-                                       const uint8_t* dig, uint32_t* c, uint32_t* o, uint32_t nb, Fin fin) {
+                                       const uint8_t* dig, uint32_t dcap, uint32_t* c, uint32_t* o, uint32_t nb,
+                                       Fin fin) {
+  // dcap: bytes of LDS behind dig that belong to the digit array and what follows it in the same
+  // struct; the walk reads at most one digit past its node (checked build: against dcap)
   const uint32_t lane = threadIdx.x & 63;
   uint32_t base = 0;
 #pragma unroll
@@ -175,6 +190,7 @@ __device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t
       // not written while its own chains run (those fill other buckets).
       uint32_t dq = q < end ? (uint32_t)dig[q] : 0u;
       for (; q < end; q++) {
+        KVH_CHK(q + 1 < dcap, kChkDig, q + 1, dcap);
         const uint32_t dnext = dig[q + 1];  // past the region: read, never used
         uint32_t xp = q, d = dq;
         dq = dnext;
@@ -185,6 +201,7 @@ __device__ __forceinline__ void chains(Sm& S, const RefPtrs& P, int nx, uint32_t
           const uint32_t w0 = __builtin_amdgcn_readfirstlane(o[d]);  // waited for here, not at the loop head
           uint32_t dst = w0 & 0x1ffffu, nd = w0 >> 17;
           for (;;) {
+            KVH_CHK(dst + 1 < dcap, kChkDig, dst + 1, dcap);
             const uint32_t wn = o[nd];  // stale if nd == d: replaced below
             const uint32_t upd = (dst + 1) | (uint32_t)dig[dst + 1] << 17;
             o[d] = upd;
@@ -264,7 +281,11 @@ __device__ __forceinline__ void wg_step(Sm& S, const RefPtrs& P, int nx, uint64_
   const bool lf = cnt <= Sm::C::FINLDS;  // fin in LDS (u16), else in global scratch
   uint32_t* gfin = P.fin + off;
   uint16_t* lfin = S.bfin;
-  auto setfin = [&](uint32_t from, uint32_t to) { if (lf) lfin[from] = (uint16_t)to; else gfin[from] = to; };
+  KVH_CHK(off + cnt <= P.n && cnt <= Sm::C::MAXN, kChkElem, off + cnt, P.n);
+  auto setfin = [&](uint32_t from, uint32_t to) {
+    KVH_CHK(from < cnt && to < cnt, kChkFin, from, cnt);
+    if (lf) lfin[from] = (uint16_t)to; else gfin[from] = to;
+  };
   auto getfin = [&](uint32_t p) -> uint32_t { return lf ? (uint32_t)lfin[p] : gfin[p]; };
   if (sh > 1) {
     const uint32_t k = sh > 8 ? 8 : sh, sh2 = sh - k, nb = 1u << k;
@@ -283,10 +304,17 @@ __device__ __forceinline__ void wg_step(Sm& S, const RefPtrs& P, int nx, uint64_
       return;
     }
     if (tid < 64) {  // the walk specialised on where fin lives (no branch per step)
+      constexpr uint32_t dcap = sizeof(S.bdig) + sizeof(S.tail);
       if (lf)
-        chains(S, P, nx, off, sh2, S.bdig, S.bc, S.bo, nb, [&](uint32_t f, uint32_t t) { lfin[f] = (uint16_t)t; });
+        chains(S, P, nx, off, sh2, S.bdig, dcap, S.bc, S.bo, nb, [&](uint32_t f, uint32_t t) {
+          KVH_CHK(f < cnt && t < cnt, kChkFin, f, cnt);
+          lfin[f] = (uint16_t)t;
+        });
       else
-        chains(S, P, nx, off, sh2, S.bdig, S.bc, S.bo, nb, [&](uint32_t f, uint32_t t) { gfin[f] = t; });
+        chains(S, P, nx, off, sh2, S.bdig, dcap, S.bc, S.bo, nb, [&](uint32_t f, uint32_t t) {
+          KVH_CHK(f < cnt && t < cnt, kChkFin, f, cnt);
+          gfin[f] = t;
+        });
     }
   } else {  // sh == 1
     for (uint32_t p = tid; p < cnt; p += kRT) {
@@ -319,6 +347,7 @@ __device__ __forceinline__ void wave_step(Sm& S, const RefPtrs& P, int nx, uint6
   const uint32_t off = (uint32_t)(node & 0x1ffff), cnt = (uint32_t)((node >> 17) & 0x1ffff),
                  sh = (uint32_t)(node >> 34);
   const uint32_t lane = threadIdx.x & 63;
+  KVH_CHK(off + cnt <= P.n && cnt <= Sm::C::WCAP, kChkElem, off + cnt, P.n);
   if (cnt < 32) {  // a tail: sorted on less() by lane 0 (sh >= 1 here)
     if (lane < cnt) { W.ls[lane] = P.slot[off + lane]; W.li[lane] = (uint8_t)lane; }
     wave_lds_sync();
@@ -338,7 +367,10 @@ __device__ __forceinline__ void wave_step(Sm& S, const RefPtrs& P, int nx, uint6
     wsync();
     return;
   }
-  auto setfin = [&](uint32_t from, uint32_t to) { W.fin[from] = (uint16_t)to; };
+  auto setfin = [&](uint32_t from, uint32_t to) {
+    KVH_CHK(from < cnt && to < cnt, kChkFin, from, cnt);
+    W.fin[from] = (uint16_t)to;
+  };
   if (sh > 1) {
     const uint32_t k = sh > 8 ? 8 : sh, sh2 = sh - k, nb = 1u << k;
     for (uint32_t b = lane; b < 256; b += 64) W.c[b] = 0;
@@ -354,7 +386,7 @@ __device__ __forceinline__ void wave_step(Sm& S, const RefPtrs& P, int nx, uint6
       wave_lds_sync();
       return;
     }
-    chains(S, P, nx, off, sh2, W.dig, W.c, W.o, nb, setfin);
+    chains(S, P, nx, off, sh2, W.dig, (uint32_t)(sizeof(W.dig) + sizeof(W.fin)), W.c, W.o, nb, setfin);
   } else {  // sh == 1
     for (uint32_t p = lane; p < cnt; p += 64) {
       W.dig[p] = (uint8_t)(P.slot[off + p] & 1);
@@ -382,23 +414,36 @@ __global__ void __launch_bounds__(Cf::RT)
 k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ items, uint64_t ntot, uint32_t B,
           const uint64_t* __restrict__ segs, HtGeom g, uint32_t bits, uint64_t* __restrict__ h_out,
           uint64_t* __restrict__ items_out, unsigned long long* __restrict__ dup_count, uint32_t dedup,
-          uint8_t* __restrict__ scratch, uint64_t sstride) {
+          uint8_t* __restrict__ scratch, uint64_t sstride, uint64_t sbytes) {
   // workgroup b sorts batch b: elements [b * B, min(ntot, (b + 1) * B)), or with segs the
   // segment [segs[b], segs[b + 1]) of at most B elements, on its own scratch slice (one batch,
   // the kvh_ht_sort form: B = ntot, one workgroup).  dup_count[b], when given, gets the batch's
-  // duplicate count (0 without dedup); a segment longer than B (or reversed) is left unsorted and
-  // flagged with ~0.
+  // duplicate count (0 without dedup).  A segment is checked against ntot here, where the offsets
+  // are read: reversed or ending past ntot -> flagged ~0, nothing written; longer than B ->
+  // copied through in input order, unmarked, and flagged ~0.
   uint64_t b0 = (uint64_t)blockIdx.x * B, nb64 = ntot - b0 < B ? ntot - b0 : B;
   if (segs) {
     b0 = segs[blockIdx.x];
     const uint64_t e = segs[blockIdx.x + 1];
+    if (e < b0 || e > ntot) {  // workgroup-uniform
+      KVH_CHK(false, kChkSeg, e, ntot);
+      if (threadIdx.x == 0 && dup_count) dup_count[blockIdx.x] = ~0ull;
+      return;
+    }
     nb64 = e - b0;
-    if (e < b0 || nb64 > B) {  // workgroup-uniform
+    if (nb64 > B) {
+      for (uint64_t k = threadIdx.x; k < nb64; k += Cf::RT) {
+        h_out[2 * (b0 + k)] = hashes[2 * (b0 + k)];
+        h_out[2 * (b0 + k) + 1] = hashes[2 * (b0 + k) + 1];
+        if (items_out) items_out[b0 + k] = items ? items[b0 + k] : b0 + k;
+      }
       if (threadIdx.x == 0 && dup_count) dup_count[blockIdx.x] = ~0ull;
       return;
     }
   }
   const uint32_t n = (uint32_t)nb64;
+  KVH_CHK(blockIdx.x * sstride + refsort_need(n) <= sbytes, kChkScratch, blockIdx.x * sstride + refsort_need(n),
+          sbytes);
   hashes += 2 * b0;
   if (items) items += b0;
   h_out += 2 * b0;
@@ -413,6 +458,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
     uint8_t* s = scratch;
     const uint32_t cap = n / 2 + 2;
     P.cap = cap;
+    P.n = n;
     P.slot = (uint64_t*)s; s += 8 * (size_t)n;
     P.slotT = (uint64_t*)s; s += 8 * (size_t)n;
     P.lists = (uint64_t*)s; s += 4 * 8 * (size_t)cap;
@@ -421,6 +467,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
     P.fin = (uint32_t*)s;
   }
   for (uint32_t i = tid; i < n; i += kRT) {
+    KVH_CHK(b0 + i < ntot, kChkHashes, b0 + i, ntot);
     P.slot[i] = ht_mod(g, hashes[2 * (size_t)i]);  // FileHdr::ht_mod, shm_ht.h:181-184
     P.idx[i] = i;
   }
@@ -450,6 +497,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
   uint32_t local = 0;
   for (uint32_t k = tid; k < n; k += kRT) {
     const uint32_t i = P.idx[k];
+    KVH_CHK(i < n && b0 + k < ntot, kChkOut, i, n);
     uint64_t h1 = hashes[2 * (size_t)i];
     const uint64_t h2 = hashes[2 * (size_t)i + 1];
     if (dedup && k + 1 < n) {
@@ -473,10 +521,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
 namespace kvh {
 namespace rt {
 
-size_t refsort_scratch_bytes(size_t n) {
-  const size_t cap = n / 2 + 2;
-  return 16 * n + 32 * cap + 12 * n + 256;
-}
+size_t refsort_scratch_bytes(size_t n) { return refsort_need(n); }
 
 namespace {
 HtGeom ref_geom(const kvh_ht_geom_t* geom, uint32_t* bits) {
@@ -502,7 +547,7 @@ int refsort_launch(const uint64_t* hashes, const uint64_t* items, size_t n, cons
   hipLaunchKernelGGL(k_refsort<RefBig>, dim3(1), dim3(RefBig::RT), 0, st, hashes, items, (uint64_t)n, (uint32_t)n,
                      (const uint64_t*)nullptr, g, bits, h_out, items_out,
                      (unsigned long long*)(dedup ? dup_count : nullptr), dedup ? 1u : 0u, (uint8_t*)scratch,
-                     (uint64_t)0);
+                     (uint64_t)0, (uint64_t)scratch_bytes);
   return launch_done();
 }
 
@@ -519,7 +564,8 @@ size_t refsort_batched_scratch_bytes(size_t n, uint32_t batch) {
 // that seven or eight RefMany sorts per CU interleave their chain walks
 static int launch_many(const uint64_t* hashes, const uint64_t* items, uint64_t ntot, uint32_t B,
                        const uint64_t* segs, uint64_t nb, const kvh_ht_geom_t* geom, uint64_t* h_out,
-                       uint64_t* items_out, uint64_t* dup_counts, bool dedup, void* scratch, hipStream_t st) {
+                       uint64_t* items_out, uint64_t* dup_counts, bool dedup, void* scratch, size_t sbytes,
+                       hipStream_t st) {
   uint32_t bits;
   const HtGeom g = ref_geom(geom, &bits);
   int cus = 0;
@@ -529,21 +575,21 @@ static int launch_many(const uint64_t* hashes, const uint64_t* items, uint64_t n
   if (B <= kSmallMax && nb > (uint64_t)cus && form == 128)
     hipLaunchKernelGGL(k_refsort<RefTiny>, dim3((uint32_t)nb), dim3(RefTiny::RT), 0, st, hashes, items, ntot, B,
                        segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
-                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B), (uint64_t)sbytes);
   else if (B <= kSmallMax && nb > (uint64_t)cus && form == 256)
     hipLaunchKernelGGL(k_refsort<RefSmall>, dim3((uint32_t)nb), dim3(RefSmall::RT), 0, st, hashes, items, ntot, B,
                        segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
-                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B), (uint64_t)sbytes);
   else
 #endif
   if (B <= kSmallMax && nb > (uint64_t)cus)
     hipLaunchKernelGGL(k_refsort<RefMany>, dim3((uint32_t)nb), dim3(RefMany::RT), 0, st, hashes, items, ntot, B,
                        segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
-                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B), (uint64_t)sbytes);
   else
     hipLaunchKernelGGL(k_refsort<RefBig>, dim3((uint32_t)nb), dim3(RefBig::RT), 0, st, hashes, items, ntot, B,
                        segs, g, bits, h_out, items_out, (unsigned long long*)dup_counts, dedup ? 1u : 0u,
-                       (uint8_t*)scratch, (uint64_t)batch_stride(B));
+                       (uint8_t*)scratch, (uint64_t)batch_stride(B), (uint64_t)sbytes);
   return launch_done();
 }
 
@@ -555,7 +601,8 @@ int refsort_batched_launch(const uint64_t* hashes, const uint64_t* items, size_t
   if (scratch_bytes < refsort_batched_scratch_bytes(n, batch)) return set_err(KVH_EINVAL);
   const uint64_t nb = (n + batch - 1) / batch;
   if (nb > 0x7fffffffull) return set_err(KVH_EINVAL);
-  return launch_many(hashes, items, n, batch, nullptr, nb, geom, h_out, items_out, dup_counts, dedup, scratch, st);
+  return launch_many(hashes, items, n, batch, nullptr, nb, geom, h_out, items_out, dup_counts, dedup, scratch,
+                     scratch_bytes, st);
 }
 
 size_t refsort_segments_scratch_bytes(size_t nseg, uint32_t max_seg) {
@@ -563,14 +610,28 @@ size_t refsort_segments_scratch_bytes(size_t nseg, uint32_t max_seg) {
   return (nseg ? nseg : 1) * batch_stride(max_seg);
 }
 
-int refsort_segments_launch(const uint64_t* hashes, const uint64_t* items, const uint64_t* seg_offs, size_t nseg,
-                            uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out,
-                            uint64_t* dup_counts, bool dedup, void* scratch, size_t scratch_bytes, hipStream_t st) {
+int refsort_segments_launch(const uint64_t* hashes, const uint64_t* items, size_t n, const uint64_t* seg_offs,
+                            size_t nseg, uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* h_out,
+                            uint64_t* items_out, uint64_t* dup_counts, bool dedup, void* scratch, size_t scratch_bytes,
+                            hipStream_t st) {
   if (max_seg == 0 || max_seg > kRefMax || nseg > 0x7fffffffull) return set_err(KVH_EINVAL);
   if (nseg == 0) return set_err(0);
   if (!seg_offs || scratch_bytes < refsort_segments_scratch_bytes(nseg, max_seg)) return set_err(KVH_EINVAL);
-  return launch_many(hashes, items, ~0ull, max_seg, seg_offs, nseg, geom, h_out, items_out, dup_counts, dedup,
-                     scratch, st);
+  // n bounds every segment on the device (the offsets are device memory): an empty batch list (n = 0)
+  // still flags each non-empty segment instead of reading past the pairs
+  return launch_many(hashes, items, (uint64_t)n, max_seg, seg_offs, nseg, geom, h_out, items_out, dup_counts, dedup,
+                     scratch, scratch_bytes, st);
+}
+
+int chk_take_refsort(unsigned long long out[4]) {
+#if KVH_CHECKED_ON
+  if (hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chk), 32)) return hip_err(e);
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  if (hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_chk), z, 32)) return hip_err(e);
+#else
+  for (int i = 0; i < 4; i++) out[i] = 0;
+#endif
+  return 0;
 }
 
 }  // namespace rt

@@ -2279,12 +2279,13 @@ size_t kvh_ht_sort_segments_scratch_bytes(size_t nseg, uint32_t max_seg) {
   return refsort_segments_scratch_bytes(nseg, max_seg);
 }
 
-int kvh_ht_sort_segments(const uint64_t* hashes, const uint64_t* items, const uint64_t* seg_offs, size_t nseg,
-                         uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* hashes_out, uint64_t* items_out,
-                         uint64_t* dup_counts, uint32_t flags, void* scratch, size_t scratch_bytes, void* stream) {
-  if (!geom || (flags & ~(KVH_DEDUP | KVH_REF_ORDER)) || (nseg && (!hashes || !hashes_out || !scratch)))
+int kvh_ht_sort_segments(const uint64_t* hashes, const uint64_t* items, size_t n, const uint64_t* seg_offs,
+                         size_t nseg, uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* hashes_out,
+                         uint64_t* items_out, uint64_t* dup_counts, uint32_t flags, void* scratch,
+                         size_t scratch_bytes, void* stream) {
+  if (!geom || (flags & ~(KVH_DEDUP | KVH_REF_ORDER)) || (nseg && n && (!hashes || !hashes_out || !scratch)))
     return set_err(KVH_EINVAL);
-  return refsort_segments_launch(hashes, items, seg_offs, nseg, max_seg, geom, hashes_out, items_out, dup_counts,
+  return refsort_segments_launch(hashes, items, n, seg_offs, nseg, max_seg, geom, hashes_out, items_out, dup_counts,
                                  (flags & KVH_DEDUP) != 0, scratch, scratch_bytes, (hipStream_t)stream);
 }
 

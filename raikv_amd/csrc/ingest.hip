@@ -31,6 +31,10 @@ using namespace kvh::rt;
 
 namespace {
 
+KVH_CHK_DECL  // checked build: the first failed bounds check of this unit
+// check sites (kvh_debug_checks' out[1]; the sort's are 1..8)
+enum : unsigned { kChkTokSlot = 17, kChkTokChunk, kChkSpanQueue, kChkSpanIdx, kChkTokOut };
+
 constexpr int kTokBlock = 256;
 constexpr uint64_t kTokSeg = 16;                            // bytes per thread per pass
 constexpr uint64_t kTokPass = kTokBlock * kTokSeg;          // 4 KiB per pass
@@ -374,12 +378,14 @@ k_tok2(const uint8_t* __restrict__ t, TokGeo G, uint32_t max_token, uint64_t* __
         const int64_t st = sm ? p0 + 31 - __builtin_clz(sm) : ex;
         const int64_t L = p0 + (int64_t)i - st + 1;
         if (L < (int64_t)max_token) {
+          KVH_CHK(slot < 512u, kChkTokSlot, slot, 512u);
           so[wv][slot] = (uint64_t)st;
           sl[wv][slot] = (uint32_t)L;
           slot++;
         }
       }
       wave_lds_sync();
+      KVH_CHK(tot <= 512u, kChkTokSlot, tot, 512u);
       for (uint32_t j = lane; j < tot; j += 64) {
         const uint64_t k = k0 + j;
         if (k < cap) {
@@ -397,6 +403,7 @@ k_tok2(const uint8_t* __restrict__ t, TokGeo G, uint32_t max_token, uint64_t* __
   }
   if constexpr (!EMIT) {
     for (int d = 32; d >= 1; d >>= 1) total += __shfl_xor(total, d, 64);
+    KVH_CHK(w < nchunks, kChkTokChunk, w, nchunks);
     if (lane == 0) chunk_cnt[w] = total;
   }
 }
@@ -523,10 +530,11 @@ __device__ __forceinline__ void spans_long(const uint8_t* __restrict__ buf, cons
                                            const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
                                            const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
                                            uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConstL* kfull,
-                                           uint64_t s1, uint64_t s2, const LdsTab<NT>& T) {
+                                           uint64_t s1, uint64_t s2, const LdsTab<NT>& T, uint64_t nchk) {
   if (lane < cnt) {
     const uint32_t e = q[lane];
     const uint64_t j = qbase + (uint64_t)(e / CH) * step + (e % CH);
+    KVH_CHK(j < nchk, kChkSpanIdx, j, nchk);
     const uint8_t* p = buf + offs[j];
     const uint32_t D = lens[j], H = D + nul;
     const LdsK<LdsTab<NT>, uint32_t, MeowConstL> K(kfull, nullptr, H, s1, s2, T);
@@ -675,10 +683,11 @@ __device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, co
                                              const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
                                              const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
                                              uint64_t step, uint32_t CH, uint32_t nul, bool fix, const MeowConstL* kfull,
-                                             const uint32_t* __restrict__ psel, const LdsTab<NT>& T) {
+                                             const uint32_t* __restrict__ psel, const LdsTab<NT>& T, uint64_t nchk) {
   if (lane < cnt) {
     const uint32_t e = q[lane];
     const uint64_t j = qbase + (uint64_t)(e / CH) * step + (e % CH);
+    KVH_CHK(j < nchk, kChkSpanIdx, j, nchk);
     const uint32_t L = lens[j], H = L + nul;
     const MedRaw r = med_issue(buf + offs[j], L);
     store_h(out, j, meow_medium(r, L, H, kfull[H], psel, T), fix);
@@ -833,14 +842,15 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
         ql += (uint32_t)__popcll(lm);
       }
     }
+    KVH_CHK(qn + ql <= QCAP, kChkSpanQueue, qn + ql, QCAP);
     if (qn >= 64 || ql >= 64) {
       wave_lds_sync();
       while (qn >= 64) {
-        spans_medium<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CHq, nul, fix, kfull, psel, T);
+        spans_medium<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CHq, nul, fix, kfull, psel, T, n);
         qn -= 64;
       }
       while (ql >= 64) {  // its newest 64 entries: q[QCAP - ql .. QCAP - ql + 64)
-        spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, 64, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T);
+        spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, 64, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T, n);
         ql -= 64;
       }
       wave_lds_sync();
@@ -871,8 +881,8 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   }
   if (qn || ql) {
     wave_lds_sync();
-    if (qn) spans_medium<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CHq, nul, fix, kfull, psel, T);
-    if (ql) spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, ql, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T);
+    if (qn) spans_medium<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CHq, nul, fix, kfull, psel, T, n);
+    if (ql) spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, ql, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T, n);
   }
   if constexpr (Q) wt_done(tk);
 }
@@ -1155,3 +1165,18 @@ int kvh_meow128_frags(const void* buf, const uint64_t* rec_offs, size_t n, uint6
 }
 
 }  // extern "C"
+
+namespace kvh {
+namespace rt {
+int chk_take_ingest(unsigned long long out[4]) {
+#if KVH_CHECKED_ON
+  if (hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chk), 32)) return hip_err(e);
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  if (hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_chk), z, 32)) return hip_err(e);
+#else
+  for (int i = 0; i < 4; i++) out[i] = 0;
+#endif
+  return 0;
+}
+}  // namespace rt
+}  // namespace kvh

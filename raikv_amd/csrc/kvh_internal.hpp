@@ -194,7 +194,36 @@ __device__ __forceinline__ uint64_t wave_sort_window(const uint64_t* __restrict_
   return wave_sort_from<WIN, SH>(win_load<WIN>(offs, i0, k), k, hist, r_off, r_len, r_idx);
 }
 
+// Bounds-checked build (`make checked` -> tools/libkvh_checked.so, compiled
+// with -DKVH_CHECKED).  KVH_CHK(cond, site, value, limit)
+// records the first failed check of its translation unit -- (count, site,
+// value, limit) in that unit's device words g_chk[4], read back by
+// kvh_debug_checks -- and never faults; the caller clamps the access it
+// guards.  The product build compiles every check away.  A unit that checks
+// puts KVH_CHK_DECL at namespace scope once.
+#ifdef KVH_CHECKED
+#define KVH_CHK_DECL static __device__ unsigned long long g_chk[4];
+__device__ __forceinline__ void kvh_chk_fail(unsigned long long* g, unsigned long long site, unsigned long long v,
+                                             unsigned long long l) {
+  if (atomicAdd(&g[0], 1ull) == 0) { g[1] = site; g[2] = v; g[3] = l; }
+}
+#define KVH_CHK(cond, site, val, lim)                                                                       \
+  do {                                                                                                      \
+    if (!(cond)) kvh_chk_fail(g_chk, (site), (unsigned long long)(val), (unsigned long long)(lim));         \
+  } while (0)
+#define KVH_CHECKED_ON 1
+#else
+#define KVH_CHK_DECL
+#define KVH_CHK(cond, site, val, lim) \
+  do {                                \
+  } while (0)
+#define KVH_CHECKED_ON 0
+#endif
+
 namespace rt {
+// checked build: the unit's (count, site, value, limit) words, then cleared (zeros in the product build)
+int chk_take_refsort(unsigned long long out[4]);
+int chk_take_ingest(unsigned long long out[4]);
 // thread-local last error (kvh_last_error); returns e
 int set_err(int e);
 // HIP error -> KVH_EHIP_BASE - e, recorded
@@ -211,8 +240,8 @@ int stream_tickets(hipStream_t st, unsigned long long** tk);
 int stream_release(hipStream_t st);
 // kv_ht_radix_sort's exact order on the device, n <= 64K (ht_refsort.hip)
 size_t refsort_segments_scratch_bytes(size_t nseg, uint32_t max_seg);
-int refsort_segments_launch(const uint64_t* hashes, const uint64_t* items, const uint64_t* seg_offs, size_t nseg,
-                            uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out,
+int refsort_segments_launch(const uint64_t* hashes, const uint64_t* items, size_t n, const uint64_t* seg_offs,
+                            size_t nseg, uint32_t max_seg, const kvh_ht_geom_t* geom, uint64_t* h_out, uint64_t* items_out,
                             uint64_t* dup_counts, bool dedup, void* scratch, size_t scratch_bytes, hipStream_t st);
 size_t refsort_batched_scratch_bytes(size_t n, uint32_t batch);
 int refsort_batched_launch(const uint64_t* hashes, const uint64_t* items, size_t n, uint32_t batch,

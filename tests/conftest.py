@@ -17,15 +17,24 @@ def pytest_configure(config):
 # there.
 os.environ.setdefault("KVH_POISON_OUTPUTS", "1")
 
-# Test plumbing only: pageable torch copies of more than ~1 MiB (fixtures to
-# the device, results back) would make the HIP runtime page-lock the numpy
-# buffer and DMA it on an SDMA engine; below its pinned-transfer minimum it
-# copies through its own pinned staging buffer instead.  The three rare
-# illegal addresses on record were all raised by such a copy right after a
-# clean synchronize (profiles/r05/pageable_path/), so the
-# suite keeps its own copies on the staging path.  The library never hands
-# the runtime a pageable buffer for a DMA (kvh.hip: is_pinned -> bounce), and
-# the register -> DMA -> unregister -> free tests still run as before.  Set
-# GPU_PINNED_MIN_XFER_SIZE yourself (MiB; on the box 1 MiB copies still
-# staged and 2.4 MB ones were locked) to restore the runtime's default path.  Must precede HIP initialisation.
-os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", "1024")
+# Debug runs only: with KVH_LIB=tools/libkvh_checked.so
+# (`make checked`, device-side bounds checks on the exact-order sort and the
+# ingest kernels) and KVH_ASSERT_CHECKS=1, every GPU test ends by asserting
+# that no check failed.  The suite itself runs the product library and the
+# HIP runtime's default copy paths (no GPU_PINNED_MIN_XFER_SIZE override).
+import pytest  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _device_bounds_checks(request):
+    yield
+    if os.environ.get("KVH_ASSERT_CHECKS") != "1" or request.node.get_closest_marker("gpu") is None:
+        return
+    import ctypes
+    import torch
+    from raikv_amd import lib
+    torch.cuda.synchronize()
+    out = (ctypes.c_uint64 * 4)()
+    rc = lib.kvh_debug_checks(out)
+    assert rc == 1, f"KVH_ASSERT_CHECKS=1 needs the checked build (kvh_debug_checks -> {rc})"
+    assert out[0] == 0, f"device bounds check failed: count {out[0]} site {out[1]} value {out[2]} limit {out[3]}"

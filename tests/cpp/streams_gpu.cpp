@@ -12,7 +12,9 @@
 //   2. launches captured into graphs on one stream (whose ticket words
 //      already exist) and replayed on two other streams at once while direct
 //      launches run on the capture stream;
-//   3. kvh_stream_release before a stream is destroyed, and a new stream after.
+//   3. kvh_stream_release before a stream is destroyed, and a new stream after;
+//   4. more new streams than the word pool holds, during another thread's
+//      global-mode graph capture (which must stay valid).
 // The oracle (oracle/liboracle.so, test infrastructure) is the checker.
 // Runs under pytest -m gpu (tests/test_gpu_parity.py::test_streams_program).
 #include <hip/hip_runtime.h>
@@ -346,6 +348,69 @@ static long release_cycle(const Data& D) {
   return bad;
 }
 
+// 4. more streams than a device's ticket-word pool holds (1024 sets), each
+// taking words on its first call, while another thread holds a
+// hipStreamCaptureModeGlobal capture open.  No library
+// call may allocate or synchronise then (either would invalidate that
+// capture); the streams past the pool take the static chunk order.  Buffers
+// and streams are made before the capture and every result is read after it.
+static long pool_dry_under_capture(const Data& D) {
+  const Job& J = D.jobs[0];  // fixed 16-byte keys
+  const size_t n = 20011, ns = 1100, per = J.per * n;
+  std::vector<hipStream_t> ss(ns);
+  for (auto& s : ss) CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipStream_t cs;
+  CK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  uint8_t *d = nullptr, *gout = nullptr;
+  CK(hipMalloc(&d, per * ns));
+  CK(hipMalloc(&gout, per));
+  CK(hipMemset(d, 0xA5, per * ns));
+  CK(hipMemset(gout, 0xA5, per));
+  CK(hipDeviceSynchronize());
+  std::atomic<int> phase{0};
+  hipError_t end_err = hipSuccess;
+  hipGraph_t graph = nullptr;
+  std::thread capt([&] {
+    CK(hipStreamBeginCapture(cs, hipStreamCaptureModeGlobal));
+    J.launch(n, gout, cs);  // captured: the static order, no words
+    phase = 1;
+    while (phase.load() < 2) std::this_thread::yield();
+    end_err = hipStreamEndCapture(cs, &graph);
+  });
+  while (phase.load() < 1) std::this_thread::yield();
+  for (size_t i = 0; i < ns; i++) J.launch(n, d + per * i, ss[i]);  // first call on each stream
+  phase = 2;
+  capt.join();
+  long bad = 0;
+  if (end_err != hipSuccess || !graph) {
+    fprintf(stderr, "capture invalidated: %s\n", hipGetErrorString(end_err));
+    bad++;
+  } else {
+    hipGraphExec_t ex;
+    CK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ex, cs));
+    CK(hipStreamSynchronize(cs));
+    CK(hipGraphExecDestroy(ex));
+    CK(hipGraphDestroy(graph));
+  }
+  CK(hipDeviceSynchronize());
+  std::vector<uint8_t> h(per);
+  for (size_t i = 0; i <= ns; i++) {
+    CK(hipMemcpy(h.data(), i < ns ? d + per * i : gout, per, hipMemcpyDeviceToHost));
+    const long b = range_bad(h.data(), J.want.data(), per);
+    if (b) fprintf(stderr, "%s %zu: %ld bad bytes\n", i < ns ? "stream" : "graph", i, b);
+    bad += b;
+  }
+  for (auto& s : ss) {
+    KV(kvh_stream_release(s));
+    CK(hipStreamDestroy(s));
+  }
+  CK(hipStreamDestroy(cs));
+  CK(hipFree(d));
+  CK(hipFree(gout));
+  return bad;
+}
+
 int main() {
   Data D;
   make(D);
@@ -363,6 +428,9 @@ int main() {
   total += b;
   b = release_cycle(D);
   printf("kvh_stream_release / destroy / new stream: %ld bad bytes\n", b);
+  total += b;
+  b = pool_dry_under_capture(D);
+  printf("1100 new streams (past the 1024-set pool) during another thread's global-mode capture: %ld bad\n", b);
   total += b;
   printf("%s\n", total ? "FAIL" : "OK");
   return total ? 1 : 0;

@@ -150,3 +150,27 @@ def test_world_size_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=1 but --gpus 2" in r.stderr and r.stdout == ""
+
+
+# ------------------------------------------------------------ scaling anchor
+def test_anchor_efficiency_fields():
+    """an N-rank c4g line is read against the 1-GPU c4g
+    anchor each rank measured alone on its GPU: aggregate / (N x anchor),
+    and per rank its shard's kernel rate / its anchor's kernel rate."""
+    anchors = [{"hashes_per_s": 100e9, "hashes_per_s_kernel": 110e9},
+               {"hashes_per_s": 120e9, "hashes_per_s_kernel": 130e9}]
+    per_gpu = [{"rank": 0, "hashes_per_s": 99e9}, {"rank": 1, "hashes_per_s": 117e9}]
+    e = bench.anchor_efficiency(2, 198e9, per_gpu, anchors)
+    assert abs(e["efficiency_vs_anchor"] - 198e9 / (2 * 110e9)) < 1e-12
+    assert abs(e["anchor_hashes_per_s_mean"] - 110e9) < 1
+    assert [p["rank"] for p in e["per_rank"]] == [0, 1]
+    assert abs(e["per_rank"][0]["efficiency_vs_anchor"] - 0.9) < 1e-12
+    assert abs(e["per_rank"][1]["efficiency_vs_anchor"] - 0.9) < 1e-12
+
+
+def test_anchor_is_the_n_gt_1_workload():
+    """The anchor is the workload the N > 1 lines run (c4g: BASELINE configs[4],
+    1B x 32 B, one global batch), so the N = 1 line carries its 1-GPU point."""
+    name, cfg, n_global = bench.resolve_config(None, 0, 2)
+    assert name == bench.ANCHOR and cfg.get("global_batch") and n_global == bench.CONFIGS[bench.ANCHOR]["n"]
+    assert bench.resolve_config(None, 0, 1)[0] == "c1"

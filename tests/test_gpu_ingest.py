@@ -274,13 +274,16 @@ def test_tokenize_hash_large_text(kvh):
 
 def test_ctest_pipeline_on_device(kvh):
     """ctest's whole ingest on the device, as raikv's test program runs it
-    (ctest.c:73-104, :202-233) over one input block: tokenize, NUL-terminated frag hashes with the
-    table's seed (kvh_tokenize_hash), then each of ctest's batches in
-    kv_ht_radix_sort's exact order with its adjacent-duplicate marking
-    (kvh_ht_sort_segments).  Every batch equals the pinned restatement of the
-    reference sort, some also the reference compiled from its sources, and
+    (ctest.c:73-104, :195-237, :316-340): the input read in 256 KiB blocks,
+    each block tokenized on its own (its end is a separator) into
+    NUL-terminated frag hashes with the table's seed (kvh_tokenize_hash), the
+    batches cut per block (16K frags or a full 64 KiB frag buffer; count and
+    buffer restart at each block, tests/ctest_batches.py), then every batch in
+    kv_ht_radix_sort's exact order with its adjacent-duplicate marking (one
+    kvh_ht_sort_segments call).  Every batch equals the pinned restatement of
+    the reference sort, some also the reference compiled from its sources, and
     the total is ctest's dup_count."""
-    from ctest_batches import ctest_batches
+    from ctest_batches import ctest_block_batches, ctest_blocks
     from oracle_lib import load_ref_ht, orc_geom, orc_ht_radix_sort_ref, ref_ht_sort
     rng = np.random.default_rng(11)
     ms = 64 << 20
@@ -292,14 +295,16 @@ def test_ctest_pipeline_on_device(kvh):
     parts = [words[int(i)] + (b" " if j % 9 else b"\n") for j, i in enumerate(rng.integers(0, 4000, 400000))]
     for text in (G["text"], np.frombuffer(b"".join(parts), dtype=np.uint8).copy()):
         dt = torch.from_numpy(text).cuda()
-        o, l, h = kvh.tokenize_hash(dt, SEED, 256)
-        lens = host(l)
-        cuts = ctest_batches(lens)
+        hb, lb = [], []
+        for s0, e0 in ctest_blocks(text.size):  # one ctest read() block each
+            o, l, h = kvh.tokenize_hash(dt[s0:e0], SEED, 256)
+            hb.append(h)
+            lb.append(host(l))
+        h = torch.cat(hb)
+        cuts = ctest_block_batches(lb)
+        assert len(lb) > 1 and int(cuts[-1]) == h.shape[0]
         segs = dev64(cuts)
-        # attribution only (the rare illegal address): a fault in the copy is
-        # reported here, one in the sort at the next host()
-        torch.cuda.synchronize()
-        hs, oi, dc = kvh.ht_sort_segments(h.contiguous(), g, segs, max_seg=16 * 1024, dedup=True)
+        hs, oi, dc = kvh.ht_sort_segments(h, g, segs, max_seg=16 * 1024, dedup=True)
         hs, oi, dc, hh = host(hs).reshape(-1, 2), host(oi), host(dc), host(h).reshape(-1, 2)
         total = 0
         for b in range(len(cuts) - 1):

@@ -233,13 +233,46 @@ def test_segments_vs_oracle(kvh, nseg):
     oh, oi, dc = host(oh), host(oi), host(dc)
     assert dc.size == nseg and int(dc[big]) == 2 ** 64 - 1
     for b in range(nseg):
-        if b == big:
+        lo, hi = int(offs[b]), int(offs[b + 1])
+        if b == big:  # copied through in input order, unmarked
+            np.testing.assert_array_equal(oh[lo:hi], h[lo:hi])
+            np.testing.assert_array_equal(oi[lo:hi], np.arange(lo, hi, dtype=np.uint64))
+            continue
+        wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, h[lo:hi], dedup=True)
+        np.testing.assert_array_equal(oi[lo:hi], wi + np.uint64(lo), err_msg=f"segment {b}")
+        np.testing.assert_array_equal(oh[lo:hi], wh, err_msg=f"segment {b}")
+        assert int(dc[b]) == wd, b
+
+
+def test_segments_bad_offsets_are_flagged_not_followed(kvh):
+    """the offsets are device memory, so the kernel checks them
+    against n itself.  A segment that ends past n or runs backwards is
+    flagged ~0 and nothing of it is written (its range may not exist); the
+    valid segments around it are sorted as usual.  The binding rejects
+    offsets that are not an int64 device tensor."""
+    rng = np.random.default_rng(5)
+    ms = 64 << 20
+    g = kvh.HtGeom.from_map(ms, 64, 1.0, 4, 4)
+    og = orc_geom(ORC, ms, 64, 1.0, 4, 4)
+    n = 5000
+    h = rng.integers(0, 2 ** 64, size=(n, 2), dtype=np.uint64)
+    offs = np.array([0, 1000, 2500, 1500, 1 << 40, 3000, 5000, 5001], dtype=np.uint64)
+    oh, oi, dc = kvh.ht_sort_segments(dev(h), g, dev(offs), max_seg=16384, dedup=True)
+    oh, oi, dc = host(oh), host(oi), host(dc)
+    flagged = {2, 3, 4, 6}  # 2500 -> 1500 reversed, 1500 -> 2^40 past n, 2^40 -> 3000 reversed, 5000 -> 5001 past n
+    for b in range(len(offs) - 1):
+        if b in flagged:
+            assert int(dc[b]) == 2 ** 64 - 1, b
             continue
         lo, hi = int(offs[b]), int(offs[b + 1])
         wh, wi, wd = orc_ht_radix_sort_ref(ORC, og, h[lo:hi], dedup=True)
         np.testing.assert_array_equal(oi[lo:hi], wi + np.uint64(lo), err_msg=f"segment {b}")
         np.testing.assert_array_equal(oh[lo:hi], wh, err_msg=f"segment {b}")
-        assert int(dc[b]) == wd, b
+        assert int(dc[b]) == wd
+    with pytest.raises(kvh.KvhError):
+        kvh.ht_sort_segments(dev(h), g, dev(offs).to(torch.int32), max_seg=16384)
+    with pytest.raises(kvh.KvhError):
+        kvh.ht_sort_segments(dev(h), g, torch.from_numpy(offs.view(np.int64)), max_seg=16384)
 
 
 def test_segments_every_step_many_batch_form(kvh):

@@ -5,7 +5,12 @@ frag buffer fills first) in kv_ht_radix_sort's exact order with duplicate
 marking (kvh_ht_sort_segments).  Device time per stage (torch events,
 medians of 5), beside the reference on one host core: ctest's tokenize +
 frag + hash (oracle/_ref ref_ctest_ingest_bench via bench.py's leg) and
-kv_ht_radix_sort + marking on 8K batches (ref_ht_sort_bench)."""
+kv_ht_radix_sort + marking on 8K batches (ref_ht_sort_bench).
+The batch cuts restart at every 256 KiB read block as ctest's do
+(tests/ctest_batches.py); the tokens come from one pass over the whole text,
+so a token running across a block end (at most one per 4096 blocks) is kept
+whole here where ctest splits it.  The exact per-block form is
+tests/test_gpu_ingest.py::test_ctest_pipeline_on_device."""
 import json, os, sys
 import numpy as np
 import torch
@@ -13,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import raikv_amd as kvh  # noqa: E402
-from ctest_batches import ctest_batches  # noqa: E402
+from ctest_batches import CTEST_BLOCK, ctest_block_batches  # noqa: E402
 from oracle_lib import load_ref_ht  # noqa: E402  (CPU baseline only)
 
 torch.cuda.set_device(0)
@@ -27,7 +32,9 @@ geom = kvh.HtGeom.from_map(map_size=64 << 30, hash_entry_size=64, hash_value_rat
 seed = kvh.STATIC_SEED
 o, l, h = kvh.tokenize_hash(text, seed, 256)
 ntok = l.numel()
-cuts = ctest_batches(l.cpu().numpy())
+ln, blk = l.cpu().numpy(), (o // CTEST_BLOCK).cpu().numpy()
+edges = np.searchsorted(blk, np.arange(int(blk[-1]) + 2))
+cuts = ctest_block_batches([ln[edges[b]:edges[b + 1]] for b in range(len(edges) - 1)])
 dcuts = torch.from_numpy(cuts.view(np.int64)).cuda()
 h = h.contiguous()
 del o
