@@ -39,7 +39,7 @@ namespace {
 
 KVH_CHK_DECL  // checked build: the first failed bounds check of this unit
 // check sites (kvh_debug_checks' out[1])
-enum : unsigned { kChkSeg = 1, kChkScratch, kChkHashes, kChkElem, kChkList, kChkDig, kChkFin, kChkOut };
+enum : unsigned { kChkScratch = 2, kChkHashes, kChkElem, kChkList, kChkDig, kChkFin, kChkOut };
 
 constexpr uint32_t kRefMax = 65536;  // elements per call
 constexpr uint32_t kWaveCap = 2048;  // nodes up to this size: one wave each
@@ -425,8 +425,7 @@ k_refsort(const uint64_t* __restrict__ hashes, const uint64_t* __restrict__ item
   if (segs) {
     b0 = segs[blockIdx.x];
     const uint64_t e = segs[blockIdx.x + 1];
-    if (e < b0 || e > ntot) {  // workgroup-uniform
-      KVH_CHK(false, kChkSeg, e, ntot);
+    if (e < b0 || e > ntot) {  // workgroup-uniform (a caller's bad offsets: flagged, not a failed check)
       if (threadIdx.x == 0 && dup_count) dup_count[blockIdx.x] = ~0ull;
       return;
     }
