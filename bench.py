@@ -368,18 +368,20 @@ def lds_line(config_name, units, kern_ms):
 
 
 def load_traffic(config_name: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, its
+    source, and (gather kernels) the bracket [unique bytes, FETCH x2 + WRITE]
+    the uncalibrated figure lies in."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None, None
+        return None, None, None
     try:
         d = json.load(open(p))
         e = d.get(config_name)
         if e:
-            return float(e["hbm_bytes_per_launch"]), e.get("source")
+            return float(e["hbm_bytes_per_launch"]), e.get("source"), e.get("traffic_bounds")
     except Exception:
         pass
-    return None, None
+    return None, None, None
 
 
 ANCHOR = "c4g"  # BASELINE configs[4]: the workload of the N > 1 lines
@@ -717,7 +719,7 @@ def main():
     n_hash = (n_global * arity if cfg.get("global_batch") else units * world) * args.steps
     value = n_hash / wall
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    traffic, tsrc = load_traffic(args.config)
+    traffic, tsrc, tbounds = load_traffic(args.config)
     res = {
         "metric": METRIC_F1 if cfg.get("positions") else (METRIC_F4 if cfg.get("crc") else
                                                           (METRIC_F3 if cfg.get("ingest") else
@@ -743,7 +745,8 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
-                     "traffic_source": tsrc},
+                     "traffic_source": tsrc,
+                     **({"traffic_bounds": tbounds} if tbounds else {})},
         "settle": {"ms": args.settle_ms, "launches": settle_n},
         "hashes_per_s_per_gpu": n * arity / (kern_ms * 1e-3),
         "hashes_per_s_aggregate": n_hash / wall,

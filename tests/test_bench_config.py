@@ -37,3 +37,31 @@ def test_named_config_and_override():
     assert name == "c2" and cfg["n"] == n == 1000 and cfg["var"]
     name, cfg, n = bench.resolve_config("c64", 0, 1)
     assert cfg["key_len"] == 64 and n == 100_000_000
+
+
+def test_committed_traffic_is_never_below_the_algorithmic_bytes():
+    """the HBM traffic bench.py reports for a config
+    (profiles/pmc_traffic.json, from rocprofv3 FETCH_SIZE / WRITE_SIZE) is
+    at least the bytes the launch must move (the alg_bytes_per_launch of the
+    bench line profiled beside it); the gather kernels carry their bracket."""
+    import json
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t = json.load(open(os.path.join(root, "profiles", "pmc_traffic.json")))
+    checked = 0
+    for c, e in t.items():
+        m = re.match(r"(profiles/\S+)/" + re.escape(c) + r"_pmc_summary\.json", e["source"])
+        if not m:
+            continue
+        bj = os.path.join(root, m.group(1), f"{c}_bench_under_rocprof.json")
+        if not os.path.exists(bj):
+            continue
+        line = [l for l in open(bj) if l.startswith("{")][-1]
+        alg = json.loads(line)["roofline"]["alg_bytes_per_launch"]
+        assert e["hbm_bytes_per_launch"] >= alg, (c, e["hbm_bytes_per_launch"], alg)
+        if "traffic_bounds" in e:
+            lo, hi = e["traffic_bounds"]
+            assert abs(lo - alg) <= 1e-6 * alg and lo <= e["hbm_bytes_per_launch"] <= hi
+        checked += 1
+    assert checked >= 8

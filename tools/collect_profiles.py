@@ -18,19 +18,13 @@ HOT_BY_CFG = {"f1": ("k_fixed_pos",), "f1p": ("k_positions",), "f4": ("k_crc_fix
 MULTI = {"f2": (("k_bk_", "k_tw_"), "k_bk_scan") if os.environ.get("F2_ENGINE", "bucketed") == "bucketed"
          else (("k_sort", "trampoline_kernel"), "k_sort_keys"),
          "f3": (("k_tok", "k_spans"), "k_spans")}
-# configs whose hot kernel gathers 16-byte key pieces in length-sorted windows: keys per launch
-GATHER = {"c2": 100_000_000, "f4v": 100_000_000}
+# configs whose hot kernel gathers 16-byte key pieces in length-sorted windows: the unique bytes one
+# launch must move (bench.py's alg_bytes_per_launch for the seeded workload: key bytes + u64 offsets +
+# outputs), the lower end of their traffic bracket
+GATHER = {"c2": 7_116_037_957, "f4v": 5_916_037_957}
 calib = os.path.join(src, "calib", "fetch_calib.json")
-GATHER_FACTOR = 1.0
-if os.path.exists(calib):
-    for k, v in json.load(open(calib)).items():
-        if "k_gather<16>" in k:
-            GATHER_FACTOR = (4 << 30) / (v["FETCH_SIZE"] * 1024)
+if os.path.exists(calib):  # kept as a record; it does not model k_var9's loads
     shutil.copy(calib, os.path.join(dst, "fetch_calib.json"))
-elif os.path.exists(os.path.join(dst, "fetch_calib.json")):  # the round's calibration, collected earlier
-    for k, v in json.load(open(os.path.join(dst, "fetch_calib.json"))).items():
-        if "k_gather<16>" in k:
-            GATHER_FACTOR = (4 << 30) / (v["FETCH_SIZE"] * 1024)
 tpath = os.path.join(root, "profiles", "pmc_traffic.json")
 spath = os.path.join(dst, "summary.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
@@ -80,21 +74,22 @@ for c in sorted(os.listdir(src)):
     pmc = json.load(open(os.path.join(d, "pmc_summary.json")))
     for k, v in pmc.items():
         if any(h in k for h in hot_names) and "FETCH_SIZE" in v:
+            hbm = v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024
+            how = "FETCH_SIZE x2 + WRITE_SIZE, x1024"
+            extra = {}
             if c in GATHER:
-                # variable-length kernels: the u64 offsets stream coalesced (FETCH_SIZE = 1/2 of
-                # the bytes, the guide's rule), the key bytes are 16-byte gathers in sorted
-                # windows, calibrated on a known byte count by tools/fetch_calib.hip
-                # (profiles/<round>/fetch_calib.json: true/FETCH_SIZE = GATHER_FACTOR)
-                offs_b = 8 * (GATHER[c] + 1)
-                hbm = (v["FETCH_SIZE"] * 1024 - offs_b / 2) * GATHER_FACTOR + offs_b + v["WRITE_SIZE"] * 1024
-                how = (f"(FETCH_SIZE x1024 - offsets/2) x {GATHER_FACTOR:.3f} (16-B gather calibration) + "
-                       f"offsets + WRITE_SIZE x1024")
-            else:
-                hbm = v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024
-                how = "FETCH_SIZE x2 + WRITE_SIZE, x1024"
+                # 16-byte gathers in length-sorted windows: the guide's x2 is exact only for wide
+                # coalesced streaming reads (MI355X_MICROARCH.md §HBM), so the gather kernels
+                # report that raw figure with its bracket: from below the
+                # unique bytes the launch must move (no HBM read can go under them), from above
+                # the x2 figure; FETCH_SIZE x1 + WRITE_SIZE (the counter's own floor) beside it
+                how = ("FETCH_SIZE x2 + WRITE_SIZE, x1024 (uncalibrated for 16-B gathers: bracketed by "
+                       "traffic_bounds)")
+                extra = {"counter_floor_bytes": v["FETCH_SIZE"] * 1024 + v["WRITE_SIZE"] * 1024,
+                         "traffic_bounds": [GATHER[c], hbm]}
             traffic[c] = {"hbm_bytes_per_launch": hbm, "kernel": k,
                           "fetch_size_kb": v["FETCH_SIZE"], "write_size_kb": v["WRITE_SIZE"],
-                          "source": f"profiles/{rnd}/{c}_pmc_summary.json ({how})"}
+                          "source": f"profiles/{rnd}/{c}_pmc_summary.json ({how})", **extra}
             clk = None
             if hot and "GRBM_GUI_ACTIVE" in v:
                 clk = v["GRBM_GUI_ACTIVE"] / 8 / (float(hot[0]["AverageNs"]) * 1e-9) / 1e9
