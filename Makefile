@@ -81,7 +81,7 @@ $(CHK_LIB): $(CHK_OBJS) raikv_amd/csrc/kvh.map
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,--version-script=raikv_amd/csrc/kvh.map -o $@ $(CHK_OBJS)
 checked: $(CHK_LIB)
 
-oracle:
+oracle: $(KV_LIB)
 	$(MAKE) -C oracle
 
 cpptests: $(CPP_TESTS)

@@ -131,7 +131,21 @@ int kvh_meow128_var_host_multi(const void *keys, const uint64_t *offsets,
 int kvh_shard_bounds(const uint64_t *offsets, size_t n, int nshards,
                      size_t *bounds);
 /* Page-lock an existing host range (e.g. raikv's shared-memory segment,
- * include/raikv/shm_ht.h:23-29) so the pipelines above DMA it directly. */
+ * include/raikv/shm_ht.h:23-29) so the pipelines above DMA it directly.
+ * RULE (a HIP runtime defect on this ROCm stack, reproduced without this
+ * library: DESIGN.md §4.4, tools/copy_fault_stress.py,
+ * tools/heap_reuse_probe.py): register long-lived memory (the shm segment,
+ * a mapping of your own) and keep it mapped after kvh_host_unregister until
+ * the process ends.  Do NOT register and unregister transient heap
+ * (malloc / numpy) buffers in a process that also makes its own pageable
+ * hipMemcpy calls of more than ~1 MiB: once those pages come back from the
+ * heap as the buffer of such a copy, the runtime's locked-user-page copy
+ * can raise hipErrorIllegalAddress (about 1 in 1,500 such copies in the
+ * reproduction).  And do not hand the runtime a pageable copy whose range is
+ * registered only in part: it can return wrong bytes with no error.  The
+ * pipelines of this library never do either (a range that is not pinned
+ * from its first to its last byte goes through their own pinned bounce
+ * buffers). */
 int kvh_host_register(void *p, size_t bytes);
 int kvh_host_unregister(void *p);
 /* pinned (page-locked, DMA-able) host memory for kvh_meow128_fixed_host's

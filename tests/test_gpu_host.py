@@ -11,6 +11,7 @@ kvh_meow128_{fixed,var}_host_multi shard one host batch over a device list
 which runs the shards concurrently on separate pipelines of that device.
 """
 import ctypes as C
+import mmap
 
 import numpy as np
 import pytest
@@ -39,6 +40,26 @@ def dev_hash_var(kvh, keys: np.ndarray, offs: np.ndarray, seed, fixup=False):
     out = kvh.meow128_var(k, o, seed, fixup=fixup)
     torch.cuda.synchronize()
     return out.cpu().numpy().view(np.uint64)
+
+
+# Host memory these tests page-lock with kvh_host_register: fresh anonymous
+# mappings, kept mapped to the end of the process.  On this ROCm stack pages
+# that were registered and unregistered and then come back from the heap as
+# the buffer of a later pageable copy of more than ~1 MiB can make that copy
+# raise hipErrorIllegalAddress (reproduced with torch and hipHostRegister
+# alone, no code of this repository: tools/copy_fault_stress.py, DESIGN.md
+# §4.4, include/kvh.h above kvh_host_register).  Registered pages that are
+# never handed back to the allocator cannot become such a buffer; the suite's
+# own pageable copies then run on the runtime's default path.
+_LOCKED = []
+
+
+def locked_pages(nbytes: int) -> np.ndarray:
+    """A page-aligned uint8 array of nbytes on its own anonymous mapping,
+    never unmapped (the memory a caller registers: raikv's shm segment)."""
+    m = mmap.mmap(-1, max(nbytes, 1))
+    _LOCKED.append(m)
+    return np.frombuffer(m, dtype=np.uint8)[:nbytes]
 
 
 def zipf_batch(n, seed, lead=0, long_keys=()):
@@ -79,7 +100,7 @@ def test_var_host_pipeline(kvh, mib, slots):
         kvh.meow128_var_host(hk, hf, STATIC, out=ho, fixup=True)
         np.testing.assert_array_equal(ho, dev_hash_var(kvh, keys, offs, STATIC, fixup=True))
         # a caller's own buffer page-locked in place (raikv's shm segment)
-        reg = np.empty(keys.size + 4096, dtype=np.uint8)
+        reg = locked_pages(keys.size + 4096)
         view = reg[:keys.size]
         view[:] = keys
         assert kvh.lib.kvh_host_register(view.ctypes.data, view.nbytes) == 0
@@ -147,12 +168,12 @@ def test_partially_registered_buffers_take_the_bounce_path(kvh):
     page = 4096
     bufs = {}
     for name, arr in (("keys", keys), ("offs", offs)):
-        raw = np.empty(arr.nbytes + 2 * page, dtype=np.uint8)
+        raw = locked_pages(arr.nbytes + 2 * page)
         start = (-raw.ctypes.data) % page
         view = raw[start:start + arr.nbytes].view(arr.dtype)
         view[:] = arr
         bufs[name] = (raw, view)
-    out_raw = np.empty(n * 16 + 2 * page, dtype=np.uint8)
+    out_raw = locked_pages(n * 16 + 2 * page)
     ostart = (-out_raw.ctypes.data) % page
     out = out_raw[ostart:ostart + n * 16].view(np.uint64).reshape(n, 2)
     regs = [bufs["keys"][1], bufs["offs"][1], out]
@@ -183,11 +204,11 @@ def test_two_registrations_with_a_pageable_gap_bounce(kvh):
     keys, offs = zipf_batch(n, 23, lead=1)
     want = dev_hash_var(kvh, keys, offs, STATIC)
     page = 4096
-    raw = np.empty(keys.nbytes + 4 * page, dtype=np.uint8)
+    raw = locked_pages(keys.nbytes + 4 * page)
     start = (-raw.ctypes.data) % page
     kv = raw[start:start + keys.nbytes]
     kv[:] = keys
-    out_raw = np.empty(n * 16 + 4 * page, dtype=np.uint8)
+    out_raw = locked_pages(n * 16 + 4 * page)
     ostart = (-out_raw.ctypes.data) % page
     out = out_raw[ostart:ostart + n * 16].view(np.uint64).reshape(n, 2)
     regs = []
