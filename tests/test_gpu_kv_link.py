@@ -5,8 +5,9 @@ the device what the reference computes on the CPU:
 
   - ctest's ingest (ctest.c:202-233) through the reference's kv_make_key_frag /
     kv_set_key_frag_string / kv_hash_key_frag (key_ctx.cpp:1737-1783), whose
-    kv_hash_meow128 is now libkvh_kv.so's: the records and hashes equal the
-    reference's own (tests/golden/ingest.npz, made with key_hash.c);
+    kv_hash_meow128 is now libkvh_kv.so's: the records equal the reference's
+    own (tests/golden/ingest.npz, made with key_hash.c) and the hashes the
+    pinned oracle's under the table seed this run drew;
   - kv_hash_meow128 + KeyCtx::set_hash + CuckooAltHash::calc_hash for 16-byte
     keys (oracle/ref_cuckoo.cpp ref_cuckoo_bench) equal the same driver linked
     with key_hash.c (oracle/_ref/libkvref_ht.so).
@@ -17,7 +18,10 @@ import os
 import numpy as np
 import pytest
 
+from oracle_lib import load_oracle, orc_hash_spans
+
 pytestmark = pytest.mark.gpu
+ORC = load_oracle()
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -52,11 +56,16 @@ def test_reference_ctest_ingest_on_libkvh_kv(kvcore):
     seed = np.zeros(2, np.uint64)
     cnt = kvcore.ref_ctest_frags(text.ctypes.data, n, 256, frag.ctypes.data, frag.size, ro.ctypes.data,
                                  hh.ctypes.data, cap, seed.ctypes.data)
+    # the records are the reference's own (ingest.npz); the table's seed is drawn per HashTab
+    # (HashTab::alloc_map), so the hashes are checked against the pinned oracle under this run's seed
     assert cnt == len(G["rec_offs"])
-    np.testing.assert_array_equal(seed, G["seed"])
     np.testing.assert_array_equal(ro[:cnt], G["rec_offs"].astype(np.uint64))
     np.testing.assert_array_equal(frag[:G["frags"].size], G["frags"])
-    np.testing.assert_array_equal(hh[:2 * cnt].reshape(-1, 2), G["hashes"])
+    ro = ro[:cnt]
+    lens = (frag[ro.astype(np.int64)].astype(np.uint32) | (frag[ro.astype(np.int64) + 1].astype(np.uint32) << 8))
+    want = orc_hash_spans(ORC, frag, ro + np.uint64(2), lens, (int(seed[0]), int(seed[1])), nul=False, fix=True)
+    np.testing.assert_array_equal(hh[:2 * cnt].reshape(-1, 2), want)
+    assert not np.array_equal(hh[:2 * cnt].reshape(-1, 2), G["hashes"]) or np.array_equal(seed, G["seed"])
 
 
 def test_reference_cuckoo_path_on_libkvh_kv(kvcore):
