@@ -394,6 +394,16 @@ int kvh_ht_sort_segments(const uint64_t *hashes, const uint64_t *items,
  * with the tie order described above. */
 int kvh_ht_radix_sort(kvh_ht_sort_t *ar, uint32_t ar_size,
                       const kvh_ht_geom_t *geom);
+/* Batching front end of the drop-in (ctest's threads each sort a batch,
+ * test/ctest.c:89-104, :395): nbatch host arrays ars[b] of sizes[b] <=
+ * 65536 elements, each sorted in place in kv_ht_radix_sort's exact order,
+ * all in ONE device launch (one pinned H2D copy, kvh_ht_sort_segments, one
+ * D2H copy).  Synchronous, on the calling thread's hipStreamPerThread; the
+ * staging buffers persist per process.  Per batch it costs the launch /
+ * nbatch: the way a device pays for the exact order at ctest's batch sizes
+ * (DESIGN.md §3.5).  No duplicate marking (the caller's loop, as ctest's). */
+int kvh_ht_radix_sort_batch(kvh_ht_sort_t *const *ars, const uint32_t *sizes,
+                            uint32_t nbatch, const kvh_ht_geom_t *geom);
 
 /* ---------------------------------------------------------------------
  * Key ingest: the key formats raikv produces, hashed on

@@ -136,6 +136,7 @@ def _load():
         "kvh_ht_sort_segments_scratch_bytes": (SZ, [SZ, U32]),
         "kvh_ht_sort_segments": (I, [P, P, SZ, P, SZ, U32, P, P, P, P, U32, P, SZ, P]),
         "kvh_ht_radix_sort": (I, [P, U32, P]),
+        "kvh_ht_radix_sort_batch": (I, [P, P, U32, P]),
         "kvh_last_error": (I, []),
         "kvh_strerror": (C.c_char_p, [I]),
         "kvh_version": (C.c_char_p, []),

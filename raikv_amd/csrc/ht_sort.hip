@@ -2289,6 +2289,99 @@ int kvh_ht_sort_segments(const uint64_t* hashes, const uint64_t* items, size_t n
                                  (flags & KVH_DEDUP) != 0, scratch, scratch_bytes, (hipStream_t)stream);
 }
 
+// Many kv_ht_radix_sort calls in one launch from host arrays: the batching front end a
+// raikv process with several ctest threads would use.  The batches are packed into one pinned staging
+// buffer, moved in one H2D copy, sorted by one kvh_ht_sort_segments launch (one workgroup per batch, each
+// in the reference's exact element order) and moved back in one D2H copy; each array is then rewritten in
+// place.  Staging and device buffers persist per process (grown on demand, under a lock).
+namespace {
+struct BatchStage {
+  std::mutex mu;
+  uint8_t *host = nullptr, *dev = nullptr;
+  size_t hcap = 0, dcap = 0;
+  int device = -1;
+};
+BatchStage g_bstage;
+}  // namespace
+
+int kvh_ht_radix_sort_batch(kvh_ht_sort_t* const* ars, const uint32_t* sizes, uint32_t nbatch,
+                            const kvh_ht_geom_t* geom) {
+  if (!geom || (nbatch && (!ars || !sizes))) return set_err(KVH_EINVAL);
+  size_t n = 0;
+  uint32_t maxb = 1;
+  for (uint32_t b = 0; b < nbatch; b++) {
+    if (sizes[b] > 65536 || (sizes[b] && !ars[b])) return set_err(KVH_EINVAL);
+    n += sizes[b];
+    maxb = std::max(maxb, sizes[b]);
+  }
+  if (n == 0) return set_err(0);
+  // one layout for host staging and device: pairs, items, segment offsets (the host copy's region),
+  // then on the device only the outputs and the sort's scratch
+  const size_t off_h = 0, off_i = al256(16 * n), off_g = off_i + al256(8 * n), in_bytes = off_g + al256(8 * (nbatch + 1));
+  const size_t sb = kvh_ht_sort_segments_scratch_bytes(nbatch, maxb);
+  if (sb == 0) return set_err(KVH_EINVAL);
+  const size_t off_ho = in_bytes, off_io = off_ho + al256(16 * n), off_s = off_io + al256(8 * n), dev_bytes = off_s + sb;
+  const size_t out_bytes = off_s - off_ho;  // hashes_out + items_out, contiguous
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_err(e);
+  std::lock_guard<std::mutex> g(g_bstage.mu);
+  if (g_bstage.device != dev) {  // buffers belong to one device
+    if (g_bstage.host) (void)hipHostFree(g_bstage.host);
+    if (g_bstage.dev) (void)hipFree(g_bstage.dev);
+    g_bstage.host = g_bstage.dev = nullptr;
+    g_bstage.hcap = g_bstage.dcap = 0;
+    g_bstage.device = dev;
+  }
+  const size_t hneed = std::max(in_bytes, out_bytes);
+  if (g_bstage.hcap < hneed) {
+    if (g_bstage.host) (void)hipHostFree(g_bstage.host);
+    g_bstage.host = nullptr;
+    g_bstage.hcap = 0;
+    if ((e = hipHostMalloc((void**)&g_bstage.host, hneed, hipHostMallocDefault)) != hipSuccess) return hip_err(e);
+    g_bstage.hcap = hneed;
+  }
+  if (g_bstage.dcap < dev_bytes) {
+    if (g_bstage.dev) (void)hipFree(g_bstage.dev);
+    g_bstage.dev = nullptr;
+    g_bstage.dcap = 0;
+    if ((e = hipMalloc((void**)&g_bstage.dev, dev_bytes)) != hipSuccess) return hip_err(e);
+    g_bstage.dcap = dev_bytes;
+  }
+  uint8_t *hs = g_bstage.host, *d = g_bstage.dev;
+  uint64_t *hv = (uint64_t*)(hs + off_h), *iv = (uint64_t*)(hs + off_i), *sg = (uint64_t*)(hs + off_g);
+  size_t k = 0;
+  for (uint32_t b = 0; b < nbatch; b++) {
+    sg[b] = k;
+    for (uint32_t i = 0; i < sizes[b]; i++, k++) {
+      hv[2 * k] = ars[b][i].key;
+      hv[2 * k + 1] = ars[b][i].key2;
+      iv[k] = (uint64_t)(uintptr_t)ars[b][i].item;
+    }
+  }
+  sg[nbatch] = k;
+  hipStream_t st = hipStreamPerThread;
+  if ((e = hipMemcpyAsync(d, hs, in_bytes, hipMemcpyHostToDevice, st)) != hipSuccess) return hip_err(e);
+  int rc = refsort_segments_launch((const uint64_t*)(d + off_h), (const uint64_t*)(d + off_i), n,
+                                   (const uint64_t*)(d + off_g), nbatch, maxb, geom, (uint64_t*)(d + off_ho),
+                                   (uint64_t*)(d + off_io), nullptr, false, d + off_s, sb, st);
+  if (rc) {
+    (void)hipStreamSynchronize(st);
+    return rc;
+  }
+  if ((e = hipMemcpyAsync(hs, d + off_ho, out_bytes, hipMemcpyDeviceToHost, st)) != hipSuccess) return hip_err(e);
+  if ((e = hipStreamSynchronize(st)) != hipSuccess) return hip_err(e);
+  const uint64_t *ho = (const uint64_t*)hs, *io = (const uint64_t*)(hs + (off_io - off_ho));
+  k = 0;
+  for (uint32_t b = 0; b < nbatch; b++)
+    for (uint32_t i = 0; i < sizes[b]; i++, k++) {
+      ars[b][i].key = ho[2 * k];
+      ars[b][i].key2 = ho[2 * k + 1];
+      ars[b][i].item = (void*)(uintptr_t)io[k];
+    }
+  return set_err(0);
+}
+
 int kvh_ht_radix_sort(kvh_ht_sort_t* ar, uint32_t ar_size, const kvh_ht_geom_t* geom) {
   if (!geom) return set_err(KVH_EINVAL);
   if (ar_size <= 1) return set_err(0);

@@ -109,6 +109,47 @@ def test_radix_sort_drop_in_is_the_reference_order(kvh, f):
     np.testing.assert_array_equal(keys, h[f["out_items"].astype(np.int64)])
 
 
+def test_radix_sort_batch_front_end(kvh):
+    """kvh_ht_radix_sort_batch: many host kv_ht_sort_t
+    arrays -- ctest's batch shapes (empty, 1, 2, 31, 32, a full 16K, ~8K
+    ones) and the reference's own fixtures -- sorted in place in ONE launch,
+    each in kv_ht_radix_sort's exact order (the pinned restatement, and the
+    fixtures' own element order word for word), items carried; again with a
+    larger second call (the staging buffers grow)."""
+    rng = np.random.default_rng(8)
+    f = FIX[0]
+    g = kvh.HtGeom.from_map(f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    og = orc_geom(ORC, f["map_size"], f["entry_size"], f["ratio"], f["buckets"], f["arity"])
+    for sizes in ([0, 1, 2, 31, 32, 16384] + [int(x) for x in rng.integers(6000, 10000, 10)],
+                  [int(x) for x in rng.integers(1, 16385, 48)]):
+        hs = [rng.integers(0, 2 ** 64, size=(k, 2), dtype=np.uint64) for k in sizes]
+        for h in hs[6:9]:
+            if len(h) > 100:
+                h[rng.integers(0, len(h), len(h) // 30)] = h[rng.integers(0, len(h), len(h) // 30)]
+        hs.append(f["hashes"])  # the fixture, with its own expected order
+        arrs, views = [], []
+        for b, h in enumerate(hs):
+            ar = (SortT * max(len(h), 1))()
+            v = np.frombuffer(ar, dtype=np.uint64).reshape(-1, 3)[:len(h)]
+            v[:, :2] = h
+            v[:, 2] = (np.uint64(b) << np.uint64(32)) + np.arange(len(h), dtype=np.uint64)
+            arrs.append(ar)
+            views.append(v)
+        ptrs = (C.c_void_p * len(arrs))(*[C.addressof(a) for a in arrs])
+        szs = (C.c_uint32 * len(arrs))(*[len(h) for h in hs])
+        assert kvh.lib.kvh_ht_radix_sort_batch(ptrs, szs, len(arrs), C.byref(g)) == 0
+        for b, (h, v) in enumerate(zip(hs, views)):
+            items = v[:, 2] - (np.uint64(b) << np.uint64(32))
+            if b == len(hs) - 1:
+                np.testing.assert_array_equal(items, f["out_items"])
+            wh, wi, _ = orc_ht_radix_sort_ref(ORC, og, h)
+            np.testing.assert_array_equal(items, wi, err_msg=f"batch {b} of {len(hs)}")
+            np.testing.assert_array_equal(v[:, :2], wh, err_msg=f"batch {b}")
+    assert kvh.lib.kvh_ht_radix_sort_batch(None, None, 0, C.byref(g)) == 0
+    bad = (C.c_uint32 * 1)(65537)
+    assert kvh.lib.kvh_ht_radix_sort_batch(ptrs, bad, 1, C.byref(g)) == -22
+
+
 def test_radix_sort_drop_in_above_64k(kvh):
     """Above 64K elements the drop-in takes the engine's total order (same
     slot order; ties by (h1 << 1, h1, h2))."""

@@ -70,3 +70,45 @@ for nb in (1, 64, 1024):
                               for _ in range(10)]))
         res["reference_cpu_G_pairs_s_1core"] = 16384 / t1 / 1e9
     print(json.dumps(res), flush=True)
+
+# The batching front end of the drop-in (kvh_ht_radix_sort_batch, VERDICT r5
+# item 8): nbatch host kv_ht_sort_t arrays of ctest's batch shape (~8K frags:
+# its 64 KiB frag buffer fills first; and full 16K ones) in one call, wall
+# clock per call including the pinned H2D / D2H copies and the host packing,
+# against the reference's kv_ht_radix_sort on one host core per batch
+import ctypes as C  # noqa: E402
+import time  # noqa: E402
+
+
+class SortT(C.Structure):  # kv_ht_sort_t (radix_sort.h:8-11)
+    _fields_ = [("key", C.c_uint64), ("key2", C.c_uint64), ("item", C.c_void_p)]
+
+
+for bsz in (8192, 16384):
+    hb = rng.integers(0, 2 ** 64, size=(bsz, 2), dtype=np.uint64)
+    d = np.zeros(1, np.uint64)
+    t1 = float(np.median([ref.ref_ht_sort_bench(geom.ht_size, geom.ht_mod_mask, geom.ht_mod_fraction,
+                                                geom.ht_mod_shift, hb.ctypes.data, bsz, d.ctypes.data)
+                          for _ in range(20)])) if ref is not None else None
+    for nb in (1, 8, 24, 64, 256):
+        arrs = []
+        for b in range(nb):
+            ar = (SortT * bsz)()
+            v = np.frombuffer(ar, dtype=np.uint64).reshape(-1, 3)
+            v[:, :2] = rng.integers(0, 2 ** 64, size=(bsz, 2), dtype=np.uint64)
+            v[:, 2] = np.arange(bsz, dtype=np.uint64)
+            arrs.append(ar)
+        ptrs = (C.c_void_p * nb)(*[C.addressof(a) for a in arrs])
+        szs = (C.c_uint32 * nb)(*([bsz] * nb))
+        for _ in range(3):
+            assert kvh.lib.kvh_ht_radix_sort_batch(ptrs, szs, nb, C.byref(geom)) == 0
+        ts = []
+        for _ in range(10):
+            t = time.perf_counter()
+            assert kvh.lib.kvh_ht_radix_sort_batch(ptrs, szs, nb, C.byref(geom)) == 0
+            ts.append(time.perf_counter() - t)
+        ms = float(np.median(ts)) * 1e3
+        res = {"radix_sort_batch": nb, "batch": bsz, "ms_per_call": ms, "ms_per_batch": ms / nb}
+        if t1 is not None:
+            res["reference_cpu_ms_per_batch_1core"] = t1 * 1e3
+        print(json.dumps(res), flush=True)

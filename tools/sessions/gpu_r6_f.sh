@@ -18,3 +18,5 @@ for f in ("bench_c1", "bench_gpus2"):
     d = json.loads(open(f"gpurun_out/r6f/{f}.json").read().strip().splitlines()[-1])
     print(f, d["value"], d["ms_per_step"], d["roofline"]["frac"], json.dumps(d.get("scaling_anchor"))[:400], d.get("efficiency_vs_anchor"))
 PY
+timeout -k 10 300 python -u tools/refsort_time.py > $O/refsort_time.jsonl 2> $O/refsort_time.err || { echo "refsort rc=$?"; tail -5 $O/refsort_time.err; exit 1; }
+grep radix_sort_batch $O/refsort_time.jsonl
