@@ -11,7 +11,7 @@ mkdir -p $OUT
 for c in $CFGS; do
   mkdir -p $OUT/$c
   # the driver's protocol (W = 5, K = 20, after the settle phase); no e2e / copy-probe legs
-  B="python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-copy-peak"
+  B="python3 bench.py --config $c --steps 20 --warmup 5 --no-cpu-baseline --no-e2e --no-copy-peak --no-anchor"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$c/trace -o run -- $B > $OUT/$c/bench.json 2> $OUT/$c/trace.err || exit 1
   R="python3 tools/run_kernel.py --config $c --reps 5"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- $R > $OUT/$c/fetch.log 2>&1 || exit 1
