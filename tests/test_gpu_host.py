@@ -97,6 +97,7 @@ def test_var_host_pipeline(kvh, mib, slots):
         hf = kvh.host_empty(offs.shape, np.uint64)
         hf[:] = offs
         ho = kvh.host_empty((n, 2), np.uint64)
+        _LOCKED.extend((hk, hf, ho))  # pinned pages are never handed back during the session either
         kvh.meow128_var_host(hk, hf, STATIC, out=ho, fixup=True)
         np.testing.assert_array_equal(ho, dev_hash_var(kvh, keys, offs, STATIC, fixup=True))
         # a caller's own buffer page-locked in place (raikv's shm segment)
@@ -251,6 +252,7 @@ def test_one_chunk_batches_at_raikv_sizes(kvh, n, tiny):
         hk = kvh.host_empty(kb.shape, np.uint8)
         hk[:] = kb
         ho = kvh.host_empty((n, 2), np.uint64)
+        _LOCKED.extend((hk, ho))
         kvh.meow128_fixed_host(hk, 16, STATIC, out=ho)
         np.testing.assert_array_equal(ho, want)
         keys, offs = zipf_batch(n, 100 + n, lead=2)

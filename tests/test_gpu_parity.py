@@ -22,6 +22,10 @@ VEC = json.load(open(os.path.join(GOLDEN, "reference_vectors.json")))
 STATIC = (0xA8E0BCC94D1855F5, 0xAD3BEC1E8DE4A1A3)
 
 
+# pinned host buffers of these tests, kept to the end of the process
+_PINNED = []
+
+
 @pytest.fixture(scope="module")
 def kvh():
     if not torch.cuda.is_available():
@@ -346,6 +350,7 @@ def test_host_pipeline_pinned_and_pageable(kvh):
     hk = kvh.host_empty((n * L,), np.uint8)
     hk[:] = kb
     ho = kvh.host_empty((n, 2), np.uint64)
+    _PINNED.extend((hk, ho))  # never handed back during the session
     for mib, slots in ((1, 2), (4, 4), (64, 16)):
         pm, ps = kvh.lib.kvh_set_tuning(15, mib), kvh.lib.kvh_set_tuning(16, slots)
         try:

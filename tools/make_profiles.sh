@@ -17,7 +17,11 @@ for c in $CFGS; do
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/$c/fetch -o run -- $R > $OUT/$c/fetch.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/$c/write -o run -- $R > $OUT/$c/write.log 2>&1 || exit 1
   timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU --output-format csv -d $OUT/$c/sq -o run -- $R > $OUT/$c/sq.log 2>&1 || exit 1
-  python3 tools/pmc_summary.py $OUT/$c/fetch $OUT/$c/write $OUT/$c/sq > $OUT/$c/pmc_summary.json || exit 1
+  # request-size counters (round 6): DRAM read bytes = 32 x TCC_EA0_RDREQ_DRAM_32B_sum (64-byte requests
+  # counted twice, 128-byte four times), so gathers need no calibration; writes by request size
+  timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --output-format csv -d $OUT/$c/rdreq -o run -- $R > $OUT/$c/rdreq.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum --output-format csv -d $OUT/$c/wrreq -o run -- $R > $OUT/$c/wrreq.log 2>&1 || exit 1
+  python3 tools/pmc_summary.py $OUT/$c/fetch $OUT/$c/write $OUT/$c/sq $OUT/$c/rdreq $OUT/$c/wrreq > $OUT/$c/pmc_summary.json || exit 1
 done
 if [ -x tools/fetch_calib ]; then
   mkdir -p $OUT/calib
