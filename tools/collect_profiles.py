@@ -29,6 +29,17 @@ tpath = os.path.join(root, "profiles", "pmc_traffic.json")
 spath = os.path.join(dst, "summary.json")
 traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # merge: other configs keep their entries
 summary = json.load(open(spath)) if os.path.exists(spath) else {}
+def req_bytes(v):
+    """HBM bytes of one dispatch from the request-size counters (round 6, tools/make_profiles.sh): reads =
+    32 x TCC_EA0_RDREQ_DRAM_32B_sum (DRAM-bound reads in 32-byte units: a 64-byte request counts 2, a
+    128-byte one 4), writes = 64 x WRREQ_64B + 32 x the other write requests.  None without them."""
+    if "TCC_EA0_RDREQ_DRAM_32B_sum" not in v or "TCC_EA0_WRREQ_sum" not in v:
+        return None
+    rd = 32 * v["TCC_EA0_RDREQ_DRAM_32B_sum"]
+    wr = 64 * v["TCC_EA0_WRREQ_64B_sum"] + 32 * (v["TCC_EA0_WRREQ_sum"] - v["TCC_EA0_WRREQ_64B_sum"])
+    return rd, wr
+
+
 def timed_avg(d, names, steps):
     """Mean duration of the LAST `steps` dispatches of the hot kernel(s) in
     the traced bench run: bench.py's timed region (the settle phase and the
@@ -59,11 +70,18 @@ for c in sorted(os.listdir(src)):
         pmc = json.load(open(os.path.join(d, "pmc_summary.json")))
         reps = max(v["_dispatches"] for k, v in pmc.items() if marker in k)
         calls = max(int(r["Calls"]) for r in stats if marker in r["Name"])
-        hbm = sum((v["FETCH_SIZE"] * 2 + v["WRITE_SIZE"]) * 1024 * v["_dispatches"] / reps
-                  for k, v in pmc.items() if any(h in k for h in names) and "FETCH_SIZE" in v)
-        traffic[c] = {"hbm_bytes_per_launch": hbm, "kernel": "+".join(names),
-                      "source": f"profiles/{rnd}/{c}_pmc_summary.json (sum over the call's kernels: "
-                                f"(FETCH_SIZE x2 + WRITE_SIZE) x1024 x dispatches / {reps} calls)"}
+        mine = [(k, v) for k, v in pmc.items() if any(h in k for h in names) and "FETCH_SIZE" in v]
+        fx2 = sum((v["FETCH_SIZE"] * 2 + v["WRITE_SIZE"]) * 1024 * v["_dispatches"] / reps for k, v in mine)
+        rq = [req_bytes(v) for k, v in mine]
+        if mine and all(r is not None for r in rq):
+            hbm = sum((r[0] + r[1]) * v["_dispatches"] / reps for r, (k, v) in zip(rq, mine))
+            how = (f"sum over the call's kernels: (32 x TCC_EA0_RDREQ_DRAM_32B_sum + write requests by size) x "
+                   f"dispatches / {reps} calls")
+        else:
+            hbm, how = fx2, (f"sum over the call's kernels: (FETCH_SIZE x2 + WRITE_SIZE) x1024 x dispatches / "
+                             f"{reps} calls")
+        traffic[c] = {"hbm_bytes_per_launch": hbm, "kernel": "+".join(names), "fetch_x2_bytes": fx2,
+                      "source": f"profiles/{rnd}/{c}_pmc_summary.json ({how})"}
         tot = sum(float(r["TotalDurationNs"]) for r in stats if any(h in r["Name"] for h in names))
         summary[c] = {"kernel": "+".join(names), "avg_ns": tot / calls, "calls": calls, "hbm_bytes_per_launch": hbm,
                       "clock_GHz_est": None, "lds_util": None,
@@ -77,7 +95,13 @@ for c in sorted(os.listdir(src)):
             hbm = v["FETCH_SIZE"] * 1024 * 2 + v["WRITE_SIZE"] * 1024
             how = "FETCH_SIZE x2 + WRITE_SIZE, x1024"
             extra = {}
-            if c in GATHER:
+            rq = req_bytes(v)
+            if rq is not None:  # exact for every access width: the gathers need no bracket
+                extra = {"fetch_x2_bytes": hbm, "read_bytes": rq[0], "write_bytes": rq[1],
+                         "write_size_bytes": v["WRITE_SIZE"] * 1024}
+                hbm = rq[0] + rq[1]
+                how = "32 x TCC_EA0_RDREQ_DRAM_32B_sum + 64 x WRREQ_64B + 32 x other WRREQ"
+            elif c in GATHER:
                 # 16-byte gathers in length-sorted windows: the guide's x2 is exact only for wide
                 # coalesced streaming reads (MI355X_MICROARCH.md §HBM), so the gather kernels
                 # report that raw figure with its bracket: from below the
