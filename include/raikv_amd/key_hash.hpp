@@ -199,6 +199,13 @@ inline void ht_sort(const uint64_t* hashes, const uint64_t* items, size_t n, con
         "kvh::ht_sort");
 }
 
+// f2 at ctest's call shape (ctest.c:89-104, :395): several threads' kv_ht_sort_t batches (<= 64K
+// elements each) sorted in place in kv_ht_radix_sort's exact order, all in one launch.
+inline void ht_radix_sort_batch(kvh_ht_sort_t* const* ars, const uint32_t* sizes, uint32_t nbatch,
+                                const kvh_ht_geom_t& g) {
+  check(kvh_ht_radix_sort_batch(ars, sizes, nbatch, &g), "kvh::ht_radix_sort_batch");
+}
+
 // f3: ctest's ingest loop (tokenize + kv_hash_key_frag of "token\0") in one
 // asynchronous call; *count (device) receives the kept token count.
 inline void ingest_text(const void* text, size_t nbytes, const HashSeed& hs, uint64_t* tok_offs, uint32_t* tok_lens,

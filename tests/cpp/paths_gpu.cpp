@@ -112,6 +112,25 @@ int main() {
   uint64_t want = 0;
   for (size_t i = 0; i + 1 < n; i++) want += pairs[i] == pairs[i + 1];
   CHECK(dups == want, "duplicates %llu, want %llu", (unsigned long long)dups, (unsigned long long)want);
+  {  // the exact-order drop-in: three batches in one call == each batch through kvh_ht_radix_sort
+    const uint32_t sz[3] = {10000, 5000, 3};
+    std::vector<std::vector<kvh_ht_sort_t>> one(3), many(3);
+    size_t o = 0;
+    for (int b = 0; b < 3; b++) {
+      for (uint32_t i = 0; i < sz[b]; i++, o++)
+        one[b].push_back({hh[2 * o], hh[2 * o + 1], (void*)(uintptr_t)(o + 1)});
+      many[b] = one[b];
+      CHECK(kvh_ht_radix_sort(one[b].data(), sz[b], &g) == 0, "kvh_ht_radix_sort");
+    }
+    kvh_ht_sort_t* ptrs[3] = {many[0].data(), many[1].data(), many[2].data()};
+    kvh::ht_radix_sort_batch(ptrs, sz, 3, g);
+    bool same = true;
+    for (int b = 0; b < 3; b++)
+      for (uint32_t i = 0; i < sz[b]; i++)
+        same &= one[b][i].key == many[b][i].key && one[b][i].key2 == many[b][i].key2 &&
+                one[b][i].item == many[b][i].item;
+    CHECK(same, "ht_radix_sort_batch differs from kvh_ht_radix_sort per batch");
+  }
 
   // f3: one-call ingest == tokenize + span hash
   std::string text;
