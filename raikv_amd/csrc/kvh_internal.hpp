@@ -42,6 +42,44 @@ __device__ __forceinline__ void load_fixed(const uint8_t* __restrict__ p, Blk* D
   }
 }
 
+// 64-byte keys at 16-byte aligned bases, by lane pairs:
+// in a group of 64 keys, lanes 2i and 2i+1 own keys i and 32+i.  Loading
+// key k in lane k reads a 16-byte piece of each of 64 keys per instruction,
+// 64 B apart: 32 cache lines a quarter used each, and the kernel ran 15 %
+// slower than with the pair form (tools/load_ab.py).  Here each instruction
+// reads 32 contiguous bytes of each of 32 keys (16 lines, half each): the
+// even lane loads pieces 0, 2 of key i and 1, 3 of key 32+i, the odd lane
+// pieces 1, 3 of key i and 0, 2 of key 32+i, and each lane passes the two it
+// loaded for its partner across the pair with one DPP move per dword.
+// `last` clamps past-the-end keys to key n-1 (a benign duplicate, as in
+// load_fixed's callers).
+__device__ __forceinline__ uint32_t pair64_key(uint32_t lane) { return (lane & 1) ? 32 + (lane >> 1) : lane >> 1; }
+__device__ __forceinline__ void load_pair64(const uint8_t* __restrict__ keys, uint64_t g, uint64_t last,
+                                            uint32_t lane, Blk* D) {
+  const uint64_t i = lane >> 1;
+  const bool odd = (lane & 1) != 0;
+  const uint64_t klo = g + i < last ? g + i : last, khi = g + 32 + i < last ? g + 32 + i : last;
+  const uint32_t o = odd ? 16u : 0u, e = 16u - o;
+  const uint8_t* src[4] = {keys + klo * 64 + o, keys + klo * 64 + 32 + o, keys + khi * 64 + e,
+                           keys + khi * 64 + 32 + e};
+  Blk R[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const v4u v = __builtin_nontemporal_load((const v4u*)src[c]);
+    R[c].w[0] = v.x; R[c].w[1] = v.y; R[c].w[2] = v.z; R[c].w[3] = v.w;
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    // sent: the even lane's R2/R3 (key 32+i), the odd lane's R0/R1 (key i);
+    // quad_perm [1,0,3,2] swaps the lanes of each pair
+    const uint32_t X = odd ? R[0].w[w] : R[2].w[w], Y = odd ? R[1].w[w] : R[3].w[w];
+    D[0].w[w] = odd ? R[2].w[w] : R[0].w[w];
+    D[1].w[w] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)X, 0xB1, 0xF, 0xF, false);
+    D[2].w[w] = odd ? R[3].w[w] : R[1].w[w];
+    D[3].w[w] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Y, 0xB1, 0xF, 0xF, false);
+  }
+}
+
 template <bool NTM = false>
 __device__ __forceinline__ void store_h(uint64_t* __restrict__ out, uint64_t idx, Blk h, bool fix) {
   if (fix) h = fixup(h);

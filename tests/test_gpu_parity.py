@@ -201,12 +201,13 @@ def test_all_lengths_0_300_all_paths(kvh):
 def test_fixed_every_length_batched(kvh):
     """Every length 1..70 as a batch of a few thousand keys (the runtime-length
     kernel for 1..63 outside the multiples of 8, its byte-exact last chunk, the
-    specialised kernels, k_generic past 63), at an aligned and an odd base,
-    against the oracle."""
+    specialised kernels, k_generic past 63), at a 16-byte aligned, an 8-byte
+    aligned (the per-key loads where 64-byte keys otherwise go by lane pairs)
+    and an odd base, against the oracle."""
     rng = np.random.default_rng(70)
     for L in range(1, 71):
         n = 2000 + 37 * L
-        for shift in (0, 3):
+        for shift in (0, 8, 3):
             raw = rng.integers(0, 256, n * L + shift, dtype=np.uint8)
             t = dev(raw)
             got = u64(kvh.meow128_fixed(t[shift:], L, STATIC, n=n))

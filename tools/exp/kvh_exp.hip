@@ -75,10 +75,61 @@ k_fixed_x(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2
         for (int c = 0; c < NC; c++)
 #pragma unroll
           for (int w = 0; w < 4; w++) D[u][c].w[w] = (uint32_t)j * 2654435761u + (uint32_t)(4 * c + w);
+      } else if constexpr (MODE == 4) {
+        // the same 64L bytes of the group, read as NC fully coalesced 1 KiB
+        // runs (lane l takes 16 bytes at 1024c + 16l): the load pattern a
+        // lane transpose would allow, with the keys scrambled
+        static_assert(L % 16 == 0, "MODE 4: whole 16-byte pieces");
+        const uint64_t cb = (b + 64 * u) * (uint64_t)L, tot = n * (uint64_t)L;
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          uint64_t off = cb + 1024 * (uint64_t)c + 16 * lane;
+          off = off + 16 <= tot ? off : tot - 16;
+          const v4u v = __builtin_nontemporal_load((const v4u*)(keys + off));
+          D[u][c].w[0] = v.x; D[u][c].w[1] = v.y; D[u][c].w[2] = v.z; D[u][c].w[3] = v.w;
+        }
+      } else if constexpr (MODE == 6 || MODE == 8) {
+        // 64-byte keys, lanes in pairs (2i, 2i+1) owning keys i and 32 + i
+        // of the group: each load instruction reads 32 bytes of each of 32
+        // keys (16 lines, half of each), and the pair swaps the two pieces
+        // each lane loaded for the other (two DPP moves per dword: lane
+        // parity picks which registers are sent; MODE 8 skips the exchange,
+        // the load pattern alone, keys scrambled)
+        static_assert(L == 64, "MODE 6/8: 64-byte keys");
+        const uint64_t g = b + 64 * u, i = lane >> 1;
+        const bool odd = (lane & 1) != 0;
+        const uint64_t klo = g + i < last ? g + i : last, khi = g + 32 + i < last ? g + 32 + i : last;
+        const uint32_t o = odd ? 16u : 0u, e = odd ? 0u : 16u;
+        const uint8_t* src[4] = {keys + klo * 64 + o, keys + klo * 64 + 32 + o, keys + khi * 64 + e,
+                                 keys + khi * 64 + 32 + e};
+        Blk R[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const v4u v = __builtin_nontemporal_load((const v4u*)src[c]);
+          R[c].w[0] = v.x; R[c].w[1] = v.y; R[c].w[2] = v.z; R[c].w[3] = v.w;
+        }
+        if constexpr (MODE == 8) {
+#pragma unroll
+          for (int c = 0; c < 4; c++) D[u][c] = R[c];
+        } else {
+#pragma unroll
+          for (int w = 0; w < 4; w++) {
+            const uint32_t X = odd ? R[0].w[w] : R[2].w[w], Y = odd ? R[1].w[w] : R[3].w[w];
+            D[u][0].w[w] = odd ? R[2].w[w] : R[0].w[w];
+            D[u][1].w[w] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)X, 0xB1, 0xF, 0xF, false);
+            D[u][2].w[w] = odd ? R[3].w[w] : R[1].w[w];
+            D[u][3].w[w] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Y, 0xB1, 0xF, 0xF, false);
+          }
+        }
       } else {
         load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
       }
     }
+  };
+  // the key a lane hashes: lane l, except under MODE 6/8 (lane pairs own i and 32 + i)
+  auto key_of = [&](uint64_t b, int u) -> uint64_t {
+    if constexpr (MODE == 6 || MODE == 8) return b + 64 * u + ((lane & 1) ? 32 + (lane >> 1) : (lane >> 1));
+    else return b + 64 * u + lane;
   };
   // PF: the next chunk's loads are issued before this chunk's rounds, so
   // each wave keeps its HBM reads in flight across its whole compute phase
@@ -105,7 +156,7 @@ k_fixed_x(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint64_t j = b + 64 * u + lane;
+      const uint64_t j = key_of(b, u);
       if constexpr (MODE == 3) acc = bxor(acc, h[u]);
       else store_h<true>(out, j < last ? j : last, h[u], fix);
     }
@@ -2703,9 +2754,38 @@ int exp_fixed_L(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint6
   return kNotMine;
 }
 
+// the load-pattern ablation at 32 and 64 B (round 6, knob 5 = 4..8): the
+// product's (NT, U) in k_fixed_x's static order, with the keys' 16-byte
+// pieces loaded per key (5, the product's pattern: a 16-byte piece of each of
+// 64 keys per instruction, 2L-byte lane stride), as coalesced 1 KiB runs (4,
+// keys scrambled), or (64 B) 32 bytes of each of 32 keys per instruction with
+// a lane-pair exchange (6; 8 without the exchange, keys scrambled)
+template <int L, int U>
+int exp_fixed_load_ab(const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,
+                      hipStream_t st, int cus) {
+  if (((uintptr_t)keys & 15) != 0) return set_err(KVH_EINVAL);
+  switch (knob(g_tune_ablate)) {
+    case 1: return launch_k<L, 4, U, 1>(keys, n, s1, s2, out, flags, st, cus);
+    case 2: return launch_k<L, 4, U, 2>(keys, n, s1, s2, out, flags, st, cus);
+    case 3: return launch_k<L, 4, U, 3>(keys, n, s1, s2, out, flags, st, cus);
+    case 4: return launch_k<L, 4, U, 4>(keys, n, s1, s2, out, flags, st, cus);
+    case 5: return launch_k<L, 4, U, 0>(keys, n, s1, s2, out, flags, st, cus);
+    case 6: if constexpr (L == 64) return launch_k<L, 4, U, 6>(keys, n, s1, s2, out, flags, st, cus); break;
+    case 8: if constexpr (L == 64) return launch_k<L, 4, U, 8>(keys, n, s1, s2, out, flags, st, cus); break;
+    default: break;
+  }
+  return set_err(KVH_EINVAL);
+}
+
 bool exp_fixed(int L, const uint8_t* keys, uint64_t n, uint64_t s1, uint64_t s2, uint64_t* out, uint32_t flags,
                hipStream_t st, int cus, int tnt, int tkpl, int* rc) {
   int r = kNotMine;
+  if (knob(g_tune_ablate) && (L == 64 || ((L == 32 || L == 48) && knob(g_tune_ablate) >= 4))) {
+    *rc = L == 64   ? exp_fixed_load_ab<64, 1>(keys, n, s1, s2, out, flags, st, cus)
+          : L == 48 ? exp_fixed_load_ab<48, 3>(keys, n, s1, s2, out, flags, st, cus)
+                    : exp_fixed_load_ab<32, 4>(keys, n, s1, s2, out, flags, st, cus);
+    return true;
+  }
   if (L == 16) r = exp_fixed_L<16>(keys, n, s1, s2, out, flags, st, cus, tnt, tkpl);
   if (L == 32) r = exp_fixed_L<32>(keys, n, s1, s2, out, flags, st, cus, tnt, tkpl);
   if (r == kNotMine) return false;
@@ -2833,7 +2913,7 @@ bool exp_var_knob(int v) { return (v >= 2 && v <= 50) || (v >= 61 && v <= 70); }
 int exp_set_tuning(int k, int value) {
   auto set = [](Knob& g, int v) { return g.exchange(v, std::memory_order_relaxed); };
   switch (k) {
-    case 5: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_ablate, value);
+    case 5: if (value < 0 || value > 8) return KVH_EINVAL; return set(g_tune_ablate, value);
     case 6: if (value != 0 && value != 2 && value != 3 && value != 4 && value != 6) return KVH_EINVAL;
             return set(g_tune_dma, value);
     case 9: if (value < 0 || value > 3) return KVH_EINVAL; return set(g_tune_var_mode, value);
