@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <mutex>
 #include <vector>
+#include <type_traits>
 #include "kvh_internal.hpp"
 #include "tickets.hpp"
 #include "../../include/kvh.h"
@@ -66,13 +67,31 @@ constexpr int kWords = 4 * 8192;  // 4 tables x 256 entries x 32 copies
 // R = 16 copies (64 KiB, lanes 16 apart share a bank: 2-way), all four
 // slots in one 256-byte row per value:
 //   v << 8 | s << 6 | c << 2
+// eight words per thread per batch, every load before the first write (as
+// fill_tables, meow_dev.hpp)
 template <int R = 32>
 __device__ __forceinline__ void fill_crc(uint32_t* lds) {
   constexpr uint32_t words = R == 32 ? (uint32_t)kWords : (uint32_t)kWords / 2;
-  for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
-    const uint32_t s = R == 32 ? ((((i >> 14) & 1u) << 1) | ((i >> 5) & 1u)) : ((i >> 4) & 3u);
-    const uint32_t v = (i >> 6) & 255u;
-    lds[i] = c_crc.t[3 - s][v];
+  constexpr int B = 8;
+  const uint32_t bd = blockDim.x;
+  auto batch = [&](uint32_t i0, auto guarded) {
+    uint32_t x[B];
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const uint32_t i0k = i0 + (uint32_t)k * bd, i = (guarded && i0k >= words) ? 0u : i0k;
+      const uint32_t s = R == 32 ? ((((i >> 14) & 1u) << 1) | ((i >> 5) & 1u)) : ((i >> 4) & 3u);
+      x[k] = c_crc.t[3 - s][(i >> 6) & 255u];
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const uint32_t i = i0 + (uint32_t)k * bd;
+      if (!guarded || i < words) lds[i] = x[k];
+    }
+  };
+  if (words % (B * bd) == 0) {  // workgroup-uniform: whole batches
+    for (uint32_t i0 = threadIdx.x; i0 < words; i0 += B * bd) batch(i0, std::false_type{});
+  } else {
+    for (uint32_t i0 = threadIdx.x; i0 < words; i0 += B * bd) batch(i0, std::true_type{});
   }
 }
 

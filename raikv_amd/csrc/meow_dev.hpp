@@ -20,6 +20,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "aes_tables.hpp"
 
 namespace kvh {
@@ -112,12 +113,32 @@ struct LdsTab {
 // fill the replicated tables; dword index i = addr >> 2 decodes to
 // copy = i & 31, table = ((i>>14)&1)*2 + ((i>>5)&1), x = (i>>6) & 255
 // (NT = 5: copy = i & 15, table = (i>>4) & 3, x = (i>>6) & 255)
+// Eight table words per thread per batch, every load of a batch issued
+// before its first write: a word-at-a-time loop waits one full memory round
+// trip per word (32 in a row for a 1024-thread workgroup filling 128 KiB).
 template <int NT>
 __device__ __forceinline__ void fill_tables(uint32_t* lds) {
-  for (uint32_t i = threadIdx.x; i < (uint32_t)LdsTab<NT>::kWords; i += blockDim.x) {
-    const uint32_t t = NT == 5 ? (i >> 4) & 3u : (((i >> 14) & 1u) << 1) | ((i >> 5) & 1u);
-    const uint32_t x = (i >> 6) & 255u;
-    lds[i] = rotl32(c_td0.v[x], 8 * (int)t);
+  constexpr uint32_t W = (uint32_t)LdsTab<NT>::kWords;
+  constexpr int B = 8;
+  const uint32_t bd = blockDim.x;
+  auto batch = [&](uint32_t i0, auto guarded) {
+    uint32_t v[B];
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const uint32_t i = i0 + (uint32_t)k * bd;
+      v[k] = c_td0.v[(((guarded && i >= W) ? 0u : i) >> 6) & 255u];
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+      const uint32_t i = i0 + (uint32_t)k * bd;
+      const uint32_t t = NT == 5 ? (i >> 4) & 3u : (((i >> 14) & 1u) << 1) | ((i >> 5) & 1u);
+      if (!guarded || i < W) lds[i] = rotl32(v[k], 8 * (int)t);
+    }
+  };
+  if (W % (B * bd) == 0) {  // workgroup-uniform: whole batches (1024 and 512 threads)
+    for (uint32_t i0 = threadIdx.x; i0 < W; i0 += B * bd) batch(i0, std::false_type{});
+  } else {
+    for (uint32_t i0 = threadIdx.x; i0 < W; i0 += B * bd) batch(i0, std::true_type{});
   }
 }
 
