@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Keys per lane at 64 B under the lane-pair loads (round 6; experiments
-build, knobs 0 = 4 tables and 3 = keys per lane): interleaved rounds in one
+"""Tables (Td0..Td3 or Td0/Td1, knob 0) and keys per lane (knob 3) at 64 B
+under the lane-pair loads (round 6; experiments build): interleaved rounds in one
 process, HIP-event medians, every variant's output equal to the default's."""
 import os as _os
 _os.environ.setdefault("KVH_LIB", _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "libkvh_exp.so"))
@@ -15,18 +15,18 @@ L, n = 64, 100_000_000
 keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda")
 out = torch.empty((n, 2), dtype=torch.int64, device="cuda")
 ref = kvh.meow128_fixed(keys, L, kvh.STATIC_SEED).cpu()
-kpls = (0, 1, 2, 3, 4)  # 0 = the default (1)
+# (tables, keys per lane); (0, 0) = the default
+kpls = [(0, 0)] + [(nt, k) for nt in (4, 2) for k in (1, 2, 3, 4)]
 same = {}
-kvh.lib.kvh_set_tuning(0, 4)
 for k in kpls:
-    kvh.lib.kvh_set_tuning(3, k)
+    kvh.lib.kvh_set_tuning(0, k[0]); kvh.lib.kvh_set_tuning(3, k[1])
     same[k] = bool(torch.equal(kvh.meow128_fixed(keys, L, kvh.STATIC_SEED).cpu(), ref))
 del ref
 res = {k: [] for k in kpls}
 st = torch.cuda.current_stream()
 for r in range(6):
     for k in kpls:
-        kvh.lib.kvh_set_tuning(3, k)
+        kvh.lib.kvh_set_tuning(0, k[0]); kvh.lib.kvh_set_tuning(3, k[1])
         kvh.meow128_fixed(keys, L, kvh.STATIC_SEED, out=out)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
         for a, b in ev:
@@ -36,5 +36,6 @@ for r in range(6):
 kvh.lib.kvh_set_tuning(3, 0); kvh.lib.kvh_set_tuning(0, 0)
 for k in kpls:
     t = float(np.median(res[k]))
-    print(json.dumps({"L": L, "n": n, "keys_per_lane": k or "default", "median_ms": round(t, 4),
+    print(json.dumps({"L": L, "n": n, "tables": k[0] or "default", "keys_per_lane": k[1] or "default",
+                      "median_ms": round(t, 4),
                       "Gkeys_s": round(n / t / 1e6, 2), "equals_default": same[k]}), flush=True)
