@@ -35,9 +35,10 @@ namespace {
 // prefetch tops out near 5.1 TB/s (tools/mem_probe.hip).
 // Indices past the end are clamped to n-1: those lanes recompute key n-1 and
 // store the identical hash to out[n-1] (benign duplicate), which keeps the
-// chunk body one basic block.  64-byte keys at 16-byte aligned bases go by
-// lane pairs instead (load_pair64: lanes 2i, 2i+1 own keys i, 32+i of each
-// 64-key group; each load instruction reads 32 contiguous bytes per key).
+// chunk body one basic block.  64-byte keys at 16-byte aligned bases and
+// 56-byte keys go by lane pairs instead (load_pair64 / load_pair56: lanes 2i,
+// 2i+1 own keys i, 32+i of each 64-key group; each load instruction of the
+// first two reads 32 contiguous bytes per key).
 template <int L, int NT, bool A16, int U>
 __global__ void __launch_bounds__(kBlock)
 k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
@@ -53,14 +54,15 @@ k_fixed(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s2,
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t step = (((uint64_t)gridDim.x * blockDim.x) >> 6) * 64 * U;
   const uint64_t last = n - 1;
-  constexpr bool PAIR = A16 && L == 64;  // 64-byte keys by lane pairs (load_pair64)
+  constexpr bool PAIR = (A16 && L == 64) || L == 56;  // lane pairs (load_pair64 / load_pair56)
   const uint64_t kl = PAIR ? pair64_key((uint32_t)lane) : lane;
   for (uint64_t b = wave * 64 * U; b < n; b += step) {  // wave-uniform trip count
     Blk D[U][NC];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint64_t j = b + 64 * u + lane;
-      if constexpr (PAIR) load_pair64(keys, b + 64 * u, last, (uint32_t)lane, D[u]);
+      if constexpr (L == 56) load_pair56(keys, b + 64 * u, last, (uint32_t)lane, D[u]);
+      else if constexpr (PAIR) load_pair64(keys, b + 64 * u, last, (uint32_t)lane, D[u]);
       else load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
     }
     Blk h[U];
@@ -162,7 +164,7 @@ k_fixed_qw(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s
   const bool fix = (flags & KVH_FIXUP) != 0;
   const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6;
   const uint64_t last = n - 1;
-  constexpr bool PAIR = A16 && L == 64;  // 64-byte keys by lane pairs (load_pair64)
+  constexpr bool PAIR = (A16 && L == 64) || L == 56;  // lane pairs (load_pair64 / load_pair56)
   const uint32_t kl = PAIR ? pair64_key(lane) : lane;
   for (;;) {
     const uint64_t b = wt_next(W, tk, wpb) * (64 * U);
@@ -171,7 +173,8 @@ k_fixed_qw(const uint8_t* __restrict__ keys, uint64_t n, uint64_t s1, uint64_t s
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint64_t j = b + 64 * u + lane;
-      if constexpr (PAIR) load_pair64(keys, b + 64 * u, last, lane, D[u]);
+      if constexpr (L == 56) load_pair56(keys, b + 64 * u, last, lane, D[u]);
+      else if constexpr (PAIR) load_pair64(keys, b + 64 * u, last, lane, D[u]);
       else load_fixed<L, A16, true>(keys + (j < last ? j : last) * L, D[u]);
     }
     Blk h[U];
@@ -469,13 +472,13 @@ int launch_fixed_rt(const uint8_t* keys, uint64_t n, uint32_t L, uint64_t s1, ui
 // 24 and 32 B (32 B: 2.6 % over 2), 3 at 40 / 48 B (7 / 4 % over the round-3
 // defaults), 1 at 56 / 64 B (4 / 8 %).  The other (NT, U) instances are the
 // sweep's losers and compile only into the experiments build, where knobs 0
-// and 3 select them (a pair with no instance runs the default).  64 B: 3 keys
-// per lane since the lane-pair loads (round 6: 1.62 vs 1.69 ms at 1,
-// profiles/r06/c64_pair/kpl.jsonl).
+// and 3 select them (a pair with no instance runs the default).  56 and
+// 64 B since the lane-pair loads (round 6, profiles/r06/c64_pair/): 64 B 3
+// keys per lane (1.62 vs 1.69 ms at 1), 56 B 2 (1.585 vs 1.613; 3 spills).
 template <int L>
 struct FixedDefault {
   static constexpr int NT = 4;
-  static constexpr int U = (L == 40 || L == 48 || L == 64) ? 3 : (L == 56 ? 1 : 4);
+  static constexpr int U = (L == 40 || L == 48 || L == 64) ? 3 : (L == 56 ? 2 : 4);
 };
 
 template <int L>

@@ -80,6 +80,36 @@ __device__ __forceinline__ void load_pair64(const uint8_t* __restrict__ keys, ui
   }
 }
 
+// 56-byte keys (8-byte aligned) by the same lane pairs: pieces 0-2 are 16
+// bytes, piece 3 the last 8.  The even lane loads A.p0 and the odd lane A.p1
+// in one instruction (32 contiguous bytes of key A = i), then B.p1 / B.p0
+// (key B = 32+i), then each its own key's p2 (16 B) and p3 (8 B); the one
+// piece each lane lacks (A.p1 on the even lane, B.p1 on the odd one) crosses
+// the pair by DPP.  Per-key loads would read 8 bytes of each of 64 keys per
+// instruction, 56 B apart: 28 lines for 512 bytes.
+__device__ __forceinline__ void load_pair56(const uint8_t* __restrict__ keys, uint64_t g, uint64_t last,
+                                            uint32_t lane, Blk* D) {
+  const uint64_t i = lane >> 1;
+  const bool odd = (lane & 1) != 0;
+  const uint64_t ka = g + i < last ? g + i : last, kb = g + 32 + i < last ? g + 32 + i : last;
+  const uint8_t* pa = keys + ka * 56;
+  const uint8_t* pb = keys + kb * 56;
+  const uint8_t* own = odd ? pb : pa;
+  const v4u r0 = __builtin_nontemporal_load((const v4u*)(pa + (odd ? 16 : 0)));
+  const v4u r1 = __builtin_nontemporal_load((const v4u*)(pb + (odd ? 0 : 16)));
+  const v4u r2 = __builtin_nontemporal_load((const v4u*)(own + 32));
+  const v2u r3 = __builtin_nontemporal_load((const v2u*)(own + 48));
+  const uint32_t R0[4] = {r0.x, r0.y, r0.z, r0.w}, R1[4] = {r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    const uint32_t X = odd ? R0[w] : R1[w];  // sent: the partner's p1
+    D[0].w[w] = odd ? R1[w] : R0[w];
+    D[1].w[w] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)X, 0xB1, 0xF, 0xF, false);
+  }
+  D[2].w[0] = r2.x; D[2].w[1] = r2.y; D[2].w[2] = r2.z; D[2].w[3] = r2.w;
+  D[3].w[0] = r3.x; D[3].w[1] = r3.y; D[3].w[2] = 0; D[3].w[3] = 0;
+}
+
 template <bool NTM = false>
 __device__ __forceinline__ void store_h(uint64_t* __restrict__ out, uint64_t idx, Blk h, bool fix) {
   if (fix) h = fixup(h);

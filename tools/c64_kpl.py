@@ -11,7 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import raikv_amd as kvh  # noqa: E402
 
 torch.cuda.set_device(0)
-L, n = 64, 100_000_000
+L = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+n = 100_000_000
 keys = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda")
 out = torch.empty((n, 2), dtype=torch.int64, device="cuda")
 ref = kvh.meow128_fixed(keys, L, kvh.STATIC_SEED).cpu()
