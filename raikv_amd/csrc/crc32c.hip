@@ -474,6 +474,153 @@ k_crc_var_sorted(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
   if constexpr (Q) wt_done(tk);
 }
 
+#ifdef KVH_EXPERIMENTS  // lost its A/B (round 6): experiments build only
+// kv_crc_c of one key whose bytes sit in an LDS stage at byte `off`: the
+// bytes up to the next dword boundary as a short step, then one aligned
+// ds_read_b32 and one slice-by-4 step per 4 bytes, then the tail.
+template <int R>
+__device__ __forceinline__ uint32_t crc_stage(const uint8_t* st, uint32_t off, uint32_t len, uint32_t r,
+                                              const CrcLdsT<R>& T) {
+  const uint32_t* w32 = (const uint32_t*)st;
+  uint32_t p = off, left = len;
+  const uint32_t h = p & 3u;
+  if (h != 0 && left != 0) {
+    const uint32_t nb = 4u - h < left ? 4u - h : left;  // 1..3
+    r = T.tail(r, (w32[p >> 2] >> (8 * h)) & ((1u << (8 * nb)) - 1u), nb);
+    p += nb;
+    left -= nb;
+  }
+  for (; left >= 4; left -= 4, p += 4) r = T.word(r, w32[p >> 2]);
+  if (left) r = T.tail(r, w32[p >> 2] & ((1u << (8 * left)) - 1u), left);
+  return r;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Variable length, windows STAGED IN LDS (round 6, knob 14 = 7; lost its A/B,
+// experiments build only: DESIGN.md §3.7).  The sorted
+// kernel above gathers each key from global memory in length order: a load
+// instruction touches up to 64 lines of its ~12 KiB window, and lines shared
+// by keys of two length classes are fetched again once the XCD's L2 dropped
+// them (8.3 GB requested for 5.9 GB of unique bytes).  Here each wave cuts its
+// keys into windows of at most 256 keys whose bytes fit SB bytes of LDS,
+// reads the window's bytes once as coalesced 16-byte groups of the 16-byte
+// aligned span (a group that holds one byte of the window lies in that byte's
+// page, so nothing past the caller's buffer can fault), sorts the window by
+// exact length, and steps each key's CRC from the stage.  Keys too long for a
+// stage run one per lane from global memory (crc_key_pf), up to 64 at a time.
+// A wave takes SEG consecutive keys per ticket; windows never cross a segment.
+template <int NW, int SB, bool Q>
+__global__ void __launch_bounds__(NW * 64)
+k_crc_var_stg(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ offs, uint64_t n,
+              const uint32_t* seeds, uint32_t seed, uint32_t* out,
+              unsigned long long* __restrict__ tk = nullptr) {  // seeds may alias out
+  constexpr uint32_t SEG = 1024, WIN = 256, M = WIN / 64, NG = SB / 1024;
+  static_assert(SB % 1024 == 0 && SB <= 65535, "stage size");
+  struct Wave {
+    uint8_t stage[SB];
+    uint32_t hist[WIN];  // the counting sort's buckets, then the CRC staging area
+    uint32_t roff[WIN];
+    uint16_t rlen[WIN], ridx[WIN];
+  };
+  struct Smem {
+    uint32_t tab[kWords / 2];  // 16 copies (64 KiB)
+    Wave w[NW];
+    WaveTickets W;
+  };
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  fill_crc<16>(sm.tab);
+  __syncthreads();
+  if constexpr (Q) wt_init(sm.W, tk);
+  const CrcLdsT<16> T(sm.tab);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  Wave& V = sm.w[wv];
+  const uint64_t kend = offs[n];
+  const uint64_t nseg = (n + SEG - 1) / SEG;
+  const uint64_t kb0 = (uint64_t)(uintptr_t)keys;
+  for (uint64_t sg = Q ? wt_next(sm.W, tk, NW) : (uint64_t)blockIdx.x * NW + wv; sg < nseg;
+       sg = Q ? wt_next(sm.W, tk, NW) : sg + (uint64_t)gridDim.x * NW) {
+    uint64_t i = sg * SEG;
+    const uint64_t iend = n - i < SEG ? n : i + SEG;
+    while (i < iend) {  // wave-uniform
+      const uint32_t cap = (uint32_t)(iend - i < WIN ? iend - i : WIN);
+      const WinOffs<WIN> W = win_load<WIN>(offs, i, cap);
+      const uint64_t base = (kb0 + W.ws) & ~15ull;  // the stage's first byte (absolute)
+      uint32_t k = 0;
+#pragma unroll
+      for (uint32_t m = 0; m < M; m++) {
+        const uint32_t j = lane + 64 * m;
+        const bool fit = j < cap && ((kb0 + W.e[m] + 15) & ~15ull) - base <= (uint64_t)SB;
+        k += (uint32_t)__popcll(__ballot(fit));  // a prefix: the ends never decrease
+      }
+      if (k == 0) {
+        // key i alone overflows a stage: the run of such keys (up to 64), one per lane from global memory
+        const bool big = lane < cap && ((kb0 + W.e[0] + 15) & ~15ull) - ((kb0 + W.a[0]) & ~15ull) > (uint64_t)SB;
+        const uint64_t nb = __ballot(!big);
+        const uint32_t kb = nb ? (uint32_t)__builtin_ctzll(nb) : (cap < 64 ? cap : 64u);
+        if (lane < kb) {
+          const uint64_t a = W.a[0];
+          out[i + lane] = crc_key_pf(keys + a, W.e[0] - a, seeds ? seeds[i + lane] : seed, T);
+        }
+        i += kb;
+        continue;
+      }
+      // the window's bytes, [base, end of key k-1 rounded up to 16), as coalesced 16-byte groups
+      uint64_t ek = 0;
+#pragma unroll
+      for (uint32_t m = 0; m < M; m++) {
+        const uint64_t v = readlane64(W.e[m], (k - 1) & 63);
+        if (((k - 1) >> 6) == m) ek = v;
+      }
+      const uint32_t G = (uint32_t)((((kb0 + ek + 15) & ~15ull) - base) >> 4);
+      v4u g[NG];
+#pragma unroll
+      for (uint32_t q = 0; q < NG; q++) {
+        const uint32_t x = lane + 64 * q, xc = x < G ? x : G - 1;
+        g[q] = __builtin_nontemporal_load((const v4u*)(uintptr_t)(base + 16ull * xc));
+      }
+      const uint32_t mis = (uint32_t)((kb0 + W.ws) - base);
+      wave_sort_from<WIN>(W, k, V.hist, V.roff, V.rlen, V.ridx);
+#pragma unroll
+      for (uint32_t q = 0; q < NG; q++) {
+        const uint32_t x = lane + 64 * q;
+        if (x < G) *(v4u*)(V.stage + 16 * x) = g[q];
+      }
+      wave_lds_sync();
+      uint32_t crc[M], ix[M];
+#pragma unroll
+      for (uint32_t c = 0; c < M; c++) {
+        const uint32_t pos = 64 * c + lane;
+        ix[c] = 0xffffffffu;
+        if (64 * c < k && pos < k) {
+          const uint32_t j = V.ridx[pos];
+          crc[c] = crc_stage(V.stage, V.roff[pos] + mis, V.rlen[pos], seeds ? seeds[i + j] : seed, T);
+          ix[c] = j;
+        }
+      }
+      wave_lds_sync();  // the records are read; the hist slice becomes the staging area
+#pragma unroll
+      for (uint32_t c = 0; c < M; c++)
+        if (ix[c] != 0xffffffffu) V.hist[ix[c]] = crc[c];
+      wave_lds_sync();
+#pragma unroll
+      for (uint32_t c = 0; c < M; c++) {
+        const uint32_t j = 64 * c + lane;
+        if (j < k) __builtin_nontemporal_store(V.hist[j], out + i + j);
+      }
+      wave_lds_sync();  // stage, records and staging read before the next window's
+      i += k;
+    }
+  }
+  if constexpr (Q) wt_done(tk);
+  (void)kend;
+}
+#endif  // KVH_EXPERIMENTS
+
 }  // namespace
 namespace kvh { namespace rt { std::atomic<int> g_tune_crc_var{6}; } }
 namespace {
@@ -588,6 +735,19 @@ int kvh_crc_c_var(const void* keys, const uint64_t* offsets, size_t n, const uin
   int cus = 0, rc = device_cus(&cus);
   if (rc) return rc;
   const int v = g_tune_crc_var.load(std::memory_order_relaxed);
+#ifdef KVH_EXPERIMENTS
+  if (v == 7) {  // windows staged in LDS, segments in address order unless knob 24 = 1 (or captured)
+    unsigned long long* tk = nullptr;
+    if (knob(g_tune_order) != 1)
+      if ((rc = stream_tickets((hipStream_t)stream, &tk))) return rc;
+    if (tk)
+      hipLaunchKernelGGL((k_crc_var_stg<8, 8192, true>), dim3(cus), dim3(512), 0, (hipStream_t)stream,
+                         (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, tk);
+    else
+      hipLaunchKernelGGL((k_crc_var_stg<8, 8192, false>), dim3(cus), dim3(512), 0, (hipStream_t)stream,
+                         (const uint8_t*)keys, offsets, (uint64_t)n, seeds, seed, out, nullptr);
+  } else
+#endif
   if (v == 6) {  // windows in address order unless knob 24 = 1 (or a captured launch)
     unsigned long long* tk = nullptr;
     if (knob(g_tune_order) != 1)

@@ -1188,7 +1188,7 @@ int kvh_set_tuning(int k, int value) {
               return KVH_EINVAL;
             return set(g_tune_var, value);
     case 8: return set(g_tune_ms_lanes, value ? 1 : 0);
-    case 14: if (value != 0 && value != 6 && !(kExperiments && value > 0 && value < 6)) return KVH_EINVAL;
+    case 14: if (value != 0 && value != 6 && !(kExperiments && value > 0 && value <= 7)) return KVH_EINVAL;
              return set(g_tune_crc_var, value);
     case 15: if (value < 1 || value > 1024) return KVH_EINVAL; return set(g_tune_pipe_mib, value);
     case 16: if (value < 2 || value > 16) return KVH_EINVAL; return set(g_tune_pipe_slots, value);
