@@ -1777,7 +1777,8 @@ k_tw_start2(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ start
   if (d2 < nb2) start[(d1 << B2) | d2] = start1[d1] + wo + inc - v;
 }
 
-// MODE selects how a tile's records are read; the library launches MODE 3.
+// MODE selects how a tile's records are read; the library launches MODE 7
+// (MODE 3 with the digit recomputed from h1 instead of loaded from bA).
 // tools/scatter2_real.hip ran every mode on the real
 // pass-2 inputs (profiles/r04/s1/s2real*.json): with plain 24-byte record
 // loads (MODE 0, the round-3 kernel) the stride-24 load instructions pull
@@ -1795,7 +1796,7 @@ __global__ void __launch_bounds__(kTwT)
 k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, const uint32_t* __restrict__ tbs,
               const uint32_t* __restrict__ cnt1, const uint32_t* __restrict__ start1, uint32_t nb1, uint32_t B2,
               const uint32_t* __restrict__ H2, const uint32_t* __restrict__ start, R24* __restrict__ rec,
-              R24* __restrict__ dummy) {
+              R24* __restrict__ dummy, HtGeom g, uint32_t sb, uint32_t B) {
   __shared__ TwSh<ND> S;
   const uint32_t tid = threadIdx.x, nb2 = 1u << B2, j = xcd_tile(blockIdx.x, gridDim.x);
   uint32_t d1, p0, p1;
@@ -1831,7 +1832,7 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
       } else if constexpr (MODE == 2) {
         r[k].h1 = p; r[k].h2 = ~(uint64_t)p; r[k].item = p;
         dg[k] = (p * 2654435761u >> 9) & (nb2 - 1);
-      } else if constexpr (MODE == 3) {
+      } else if constexpr (MODE == 3 || MODE == 7) {
         // (loaded below, outside the branch)
       } else {
         r[k] = recA[p];
@@ -1839,7 +1840,7 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
       }
     }
   }
-  if constexpr (MODE == 3) {  // every load of the tile in flight together: clamped, not branched around
+  if constexpr (MODE == 3 || MODE == 7) {  // every load of the tile in flight together: clamped, not branched around
     uint32_t bv[kTwPer];
 #pragma unroll
     for (int k = 0; k < kTwPer; k++) {
@@ -1848,10 +1849,14 @@ k_tw_scatter2(const R24* __restrict__ recA, const uint16_t* __restrict__ bA, con
       r[k].h1 = __builtin_nontemporal_load(q);
       r[k].h2 = __builtin_nontemporal_load(q + 1);
       r[k].item = __builtin_nontemporal_load(q + 2);
-      bv[k] = __builtin_nontemporal_load(bA + pc);
+      if constexpr (MODE == 3) bv[k] = __builtin_nontemporal_load(bA + pc);
     }
+    // MODE 7 (the library's, round 6): the low digit recomputed from h1
+    // (ht_mod is a multiply and a shift) instead of read from bA: 2 B less
+    // per record, 3.80 -> 3.75 ms for f2 (profiles/r06/f2_ab/)
 #pragma unroll
-    for (int k = 0; k < kTwPer; k++) dg[k] = v[k] ? bv[k] & (nb2 - 1) : 0u;
+    for (int k = 0; k < kTwPer; k++)
+      dg[k] = v[k] ? (MODE == 7 ? bk_of(sort_key64(g, sb, r[k].h1), B) : bv[k]) & (nb2 - 1) : 0u;
   }
   if (tid < nb2) S.gofs[tid] = start[(d1 << B2) | tid] + H2[(uint64_t)j * nb2 + tid];
   tw_rank<ND>(dg, v, S, pos);
@@ -2055,14 +2060,17 @@ int sort_impl(const uint64_t* hashes, const uint64_t* items, size_t n, const kvh
       hipLaunchKernelGGL(k_tw_start2, dim3(nb1), dim3(256), 0, st, (const uint32_t*)cnt, (const uint32_t*)start1,
                          nb1, B2, start);
       if ((rc = launch_done())) return rc;
-      if (d8)
-        hipLaunchKernelGGL((k_tw_scatter2<3, kTwD8>), dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA,
-                           (const uint16_t*)bA, (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1,
-                           nb1, B2, (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
-      else
-        hipLaunchKernelGGL((k_tw_scatter2<3, kTwD>), dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA,
-                           (const uint16_t*)bA, (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1,
-                           nb1, B2, (const uint32_t*)H2, (const uint32_t*)start, recB, (R24*)nullptr);
+#define KVH_TWS2(M, NDv)                                                                                             \
+  hipLaunchKernelGGL((k_tw_scatter2<M, NDv>), dim3(ntB), dim3(kTwT), 0, st, (const R24*)recA, (const uint16_t*)bA,     \
+                     (const uint32_t*)tbs, (const uint32_t*)cnt1, (const uint32_t*)start1, nb1, B2, (const uint32_t*)H2,  \
+                     (const uint32_t*)start, recB, (R24*)nullptr, g, sb, B)
+#ifdef KVH_EXPERIMENTS
+      if (b3 == 17) {  // A/B: the round-5 pass 2, low digit loaded from bA
+        if (d8) KVH_TWS2(3, kTwD8); else KVH_TWS2(3, kTwD);
+      } else
+#endif
+      if (d8) KVH_TWS2(7, kTwD8); else KVH_TWS2(7, kTwD);
+#undef KVH_TWS2
       if ((rc = launch_done())) return rc;
       if (small_b && half) {  // half-size buckets: two 512-thread workgroups per CU
         const uint32_t hg = std::min<uint32_t>(nb, 2u * (uint32_t)cus);

@@ -1198,7 +1198,7 @@ int kvh_set_tuning(int k, int value) {
     case 20: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_engine, value);
     case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
     case 22: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_sort_cap, value);
-    case 23: if (value != 0 && value != 3 && !(kExperiments && (value == 1 || value == 2 || (value >= 5 && value <= 15)))) return KVH_EINVAL;
+    case 23: if (value != 0 && value != 3 && !(kExperiments && (value == 1 || value == 2 || (value >= 5 && value <= 15) || value == 17))) return KVH_EINVAL;
              return set(g_tune_sort_b3, value);
     case 24: if (value < 0 || value > (kExperiments ? 5 : 2)) return KVH_EINVAL; return set(g_tune_order, value);
     case 25: if (value != 0 && value != 10 && value != 11 && value != 12) return KVH_EINVAL; return set(g_tune_sort_hd, value);

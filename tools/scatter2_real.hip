@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(want, recB, 24 * n, hipMemcpyDeviceToDevice));
   auto launch = [&](int m) {
 #define S2(M) hipLaunchKernelGGL(k_tw_scatter2<M>, dim3(ntB), dim3(kTwT), 0, 0, recA, bA, tbs, cnt1, start1, nb1, B2, \
-                                 H2, start, recB, dummy)
+                                 H2, start, recB, dummy, HtGeom{}, 0u, 0u)
     switch (m) { case 0: S2(0); break; case 1: S2(1); break; case 2: S2(2); break; case 3: S2(3); break;
                  case 4: S2(4); break; case 5: S2(5); break; default: S2(6); break; }
 #undef S2

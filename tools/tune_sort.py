@@ -31,14 +31,14 @@ for r in range(3):
         srt.sort(h, items, dedup=True, out=ho, items_out=io)
         torch.cuda.synchronize()
         if ref is None: ref = (ho.clone(), io.clone(), int(srt.dups.item()))
-        elif not (KNOB == 23 and bits >= 7 and bits != 11):  # knob 23 = 7-10, 12-15: phase ablations, outputs not sorted
+        elif not (KNOB == 23 and (7 <= bits <= 10 or 12 <= bits <= 15)):  # knob 23 = 7-10, 12-15: phase ablations, outputs not sorted
             assert torch.equal(ho, ref[0]) and torch.equal(io, ref[1]) and int(srt.dups.item()) == ref[2], bits
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
         for a, b in ev:
             a.record(st); srt.sort(h, items, dedup=True, out=ho, items_out=io); b.record(st)
         torch.cuda.synchronize()
         res.setdefault(bits, []).extend(a.elapsed_time(b) for a, b in ev)
-kvh.lib.kvh_set_tuning(KNOB, 0 if KNOB == 20 else 16)
+kvh.lib.kvh_set_tuning(KNOB, {20: 0, 23: 3}.get(KNOB, 16))
 for bits, t in res.items():
     ms = float(np.median(t))
     print(json.dumps({"knob": KNOB, "value": bits, "median_ms": ms, "Gkeys_s": n / ms / 1e6, "dups": ref[2]}))
