@@ -4,14 +4,15 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c3|c4|c4g|c64|...]
 
 A "step" is one pass of the hot path (one kvh_meow128_* launch) over one
-batch of synthetic keys already resident in HBM.  Default workload at N=1 is
-BASELINE.json configs[1] (C1: 100M fixed 16-byte keys); at N>1 it is
-configs[4] as stated (c4g: ONE global batch of 1B 32-byte keys, rank r
-hashing index range shard_range(1B, r, N), "scaling": "strong"; per-GPU and
-aggregate rates in the line).  Keys are independent: there is no data-path
-collective; a CPU gloo group only carries the barrier and the max-over-ranks
-time.  The other configs ("c1".."c4", "c64", the §8 f rows) keep a fixed
-per-GPU batch ("scaling": "weak").
+batch of synthetic keys already resident in HBM.  Default workload at every
+N is BASELINE.json configs[1] (C1: 100M fixed 16-byte keys) per GPU: at N>1
+each rank hashes its own 100M-key shard of an N x 100M batch ("scaling":
+"weak"), so the driver's per-N values compare one workload.  Keys are
+independent: there is no data-path collective; a CPU gloo group only carries
+the barrier and the max-over-ranks time.  BASELINE configs[4] as stated (c4g:
+ONE global batch of 1B 32-byte keys, rank r hashing index range
+shard_range(1B, r, N), "scaling": "strong") runs with --config c4g and reads
+against its 1-GPU anchor, which the default N=1 line carries.
 
 The JSON line carries
   roofline     : algorithmic bytes/launch / avg kernel time (HIP events on
@@ -384,7 +385,7 @@ def load_traffic(config_name: str):
     return None, None, None
 
 
-ANCHOR = "c4g"  # BASELINE configs[4]: the workload of the N > 1 lines
+ANCHOR = "c4g"  # BASELINE configs[4] as stated: the workload of `--config c4g` at N > 1
 
 
 def measure_anchor(kvh, seed, steps: int = 10, settle_ms: float = 300.0) -> dict:
@@ -493,12 +494,13 @@ def launch_ranks(world: int, argv, exe=None, port=None, poll_s: float = 0.2) -> 
 
 
 def resolve_config(name, rank: int, world: int, keys_override: int = 0):
-    """The workload of this rank: c1 at N = 1 and c4g (BASELINE configs[4]:
-    one global 1B x 32 B batch, strong scaling) at N > 1 unless named; a
-    global batch's rank r hashes index range shard_range(n, r, N).  Returns
-    (name, cfg with this rank's n, the global key count)."""
+    """The workload of this rank: c1 per GPU at every N (weak scaling: the
+    driver's per-N values then compare one workload) unless named; a global
+    batch (c4g, BASELINE configs[4] as stated) has rank r hash index range
+    shard_range(n, r, N).  Returns (name, cfg with this rank's n, the global
+    key count)."""
     if name is None:
-        name = "c1" if world == 1 else "c4g"
+        name = "c1"
     cfg = dict(CONFIGS[name])
     if keys_override:
         cfg["n"] = keys_override
@@ -518,7 +520,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
-                    help="default: c1 at N=1, c4g (BASELINE configs[4], strong scaling) at N>1")
+                    help="default: c1 per GPU at every N (weak scaling); c4g = BASELINE configs[4] as stated "
+                         "(one global 1B x 32 B batch, strong scaling)")
     ap.add_argument("--keys", type=int, default=0, help="override keys per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1,7 +1,8 @@
 """CPU: bench.py's workload selection (the driver runs `bench.py --gpus N`
-with no --config): c1 (BASELINE configs[1]) at N = 1; at N > 1 c4g, the
-north star's C4 as stated -- one global batch of 1B 32-byte keys whose index
-ranges the ranks share exactly (strong scaling)."""
+with no --config): c1 (BASELINE configs[1]) per GPU at every N (weak
+scaling); `--config c4g` is the north star's C4 as stated -- one global batch
+of 1B 32-byte keys whose index ranges the ranks share exactly (strong
+scaling)."""
 import os
 import sys
 
@@ -15,11 +16,20 @@ def test_default_is_c1_at_one_gpu():
     assert not cfg.get("global_batch")
 
 
-def test_default_is_one_global_batch_at_n_gpus():
+def test_default_is_c1_per_gpu_at_n_gpus():
+    """Weak scaling: every rank its own 100M x 16 B shard, the N = 1 workload."""
+    for world in (2, 4, 8):
+        for r in range(world):
+            name, cfg, n = bench.resolve_config(None, r, world)
+            assert name == "c1" and cfg["n"] == n == 100_000_000 and cfg["key_len"] == 16
+            assert not cfg.get("global_batch")
+
+
+def test_c4g_is_one_global_batch_at_n_gpus():
     for world in (2, 4, 8, 3):
         shards = []
         for r in range(world):
-            name, cfg, n = bench.resolve_config(None, r, world)
+            name, cfg, n = bench.resolve_config("c4g", r, world)
             assert name == "c4g" and n == 1_000_000_000 and cfg["key_len"] == 32 and cfg["global_batch"]
             lo, hi = cfg["shard"]
             assert hi - lo == cfg["n"]

@@ -168,9 +168,10 @@ def test_anchor_efficiency_fields():
     assert abs(e["per_rank"][1]["efficiency_vs_anchor"] - 0.9) < 1e-12
 
 
-def test_anchor_is_the_n_gt_1_workload():
-    """The anchor is the workload the N > 1 lines run (c4g: BASELINE configs[4],
-    1B x 32 B, one global batch), so the N = 1 line carries its 1-GPU point."""
-    name, cfg, n_global = bench.resolve_config(None, 0, 2)
-    assert name == bench.ANCHOR and cfg.get("global_batch") and n_global == bench.CONFIGS[bench.ANCHOR]["n"]
-    assert bench.resolve_config(None, 0, 1)[0] == "c1"
+def test_anchor_is_the_c4g_workload():
+    """The anchor is the workload `--config c4g` runs at N > 1 (BASELINE
+    configs[4], 1B x 32 B, one global batch), so the N = 1 line carries its
+    1-GPU point; the default N > 1 lines are c1 per GPU (weak scaling)."""
+    name, cfg, n_global = bench.resolve_config(bench.ANCHOR, 0, 2)
+    assert cfg.get("global_batch") and n_global == bench.CONFIGS[bench.ANCHOR]["n"]
+    assert bench.resolve_config(None, 0, 1)[0] == "c1" and bench.resolve_config(None, 0, 2)[0] == "c1"
