@@ -578,6 +578,11 @@ struct ShortRaw {
 // offsets too)
 __device__ v4u g_no_span[1];
 
+// SB (experiments A/B): 0 B = the block of the last byte (== A unless the
+// span crosses a 16-byte boundary); 1 B loaded only by the lanes whose span
+// crosses (the others copy A).  (Always loading the next block reads past
+// the buffer's last byte: not an option.)
+template <int SB = 0>
 __device__ __forceinline__ ShortRaw short_issue(const uint8_t* __restrict__ p, uint32_t D, bool load) {
   ShortRaw r;
   const uint8_t* q = load ? p : (const uint8_t*)g_no_span;
@@ -587,7 +592,12 @@ __device__ __forceinline__ ShortRaw short_issue(const uint8_t* __restrict__ p, u
   r.D = load ? D : 0u;
   // pointer arithmetic (not integer masks) keeps these global loads
   r.A = *(const v4u*)(q - a);
-  r.B = *(const v4u*)(q + e - ((a + e) & 15u));
+  if constexpr (SB == 1) {
+    r.B = r.A;
+    if (a + e >= 16u) r.B = *(const v4u*)(q - a + 16);  // the last byte's block: in bounds
+  } else {
+    r.B = *(const v4u*)(q + e - ((a + e) & 15u));
+  }
   return r;
 }
 
@@ -696,7 +706,7 @@ __device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, co
 
 // Q: chunks in address order through wave tickets (tickets.hpp; n < 2^32 - 1,
 // the queues then hold span indices themselves)
-template <int NT, int NH, int PD = 2, bool Q = false>
+template <int NT, int NH, int PD = 2, bool Q = false, int SB = 0>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
@@ -777,7 +787,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
       mo[d][h] = __builtin_nontemporal_load(offs + jd);  // read once: streaming
       mD[d][h] = __builtin_nontemporal_load(lens + jd);
     }
-    tr[0][h] = short_issue(buf + o0, D0, b0 + 64 * h + lane < n && D0 && is_short(D0));
+    tr[0][h] = short_issue<SB>(buf + o0, D0, b0 + 64 * h + lane < n && D0 && is_short(D0));
     tr[0][h].D = D0;  // the length rides with the blocks (0-byte spans load nothing)
   }
   uint32_t it = 0;
@@ -795,7 +805,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
 #pragma unroll
     for (int h = 0; h < NH; h++) {  // text of the next chunk
       const uint32_t D1 = mD[un][h];
-      tr[x ^ 1][h] = short_issue(buf + mo[un][h], D1, bn + 64 * h + lane < n && D1 && is_short(D1));
+      tr[x ^ 1][h] = short_issue<SB>(buf + mo[un][h], D1, bn + 64 * h + lane < n && D1 && is_short(D1));
       tr[x ^ 1][h].D = D1;
     }
     bool valid[NH], shrt[NH];
@@ -992,6 +1002,13 @@ int launch_spans(const void* buf, const uint64_t* offs, const uint32_t* lens, ui
   unsigned long long* tk = nullptr;
   if (knob(g_tune_order) != 1 && n < 0xffffffffull)
     if (int rc = stream_tickets(st, &tk)) return rc;
+#ifdef KVH_EXPERIMENTS
+  const int sk = g_tune_spans.load(std::memory_order_relaxed);
+  if (tk && sk == 3)  // A/B: the second text block loaded only where the span crosses
+    hipLaunchKernelGGL((k_spans<4, 2, 2, true, 1>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens,
+                       n, seed1, seed2, out, flags, dcount, tk);
+  else
+#endif
   if (tk) {  // (no words for a captured launch: the static order)
     hipLaunchKernelGGL((k_spans<4, 2, 2, true>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens, n,
                        seed1, seed2, out, flags, dcount, tk);
@@ -1140,7 +1157,7 @@ int kvh_meow128_spans(const void* buf, const uint64_t* offs, const uint32_t* len
   if (rc) return rc;
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n + 1023) / 1024, (uint64_t)cus));
   const int sk = g_tune_spans.load(std::memory_order_relaxed);
-  if (sk == 2)
+  if (sk >= 2)
     return launch_spans(buf, offs, lens, n, seed1, seed2, out, flags, nullptr, grid, (hipStream_t)stream);
   else if (sk == 1)
     hipLaunchKernelGGL((k_spans<4, 1>), dim3(grid), dim3(1024), 0, (hipStream_t)stream, (const uint8_t*)buf, offs,
