@@ -580,7 +580,8 @@ __device__ v4u g_no_span[1];
 
 // SB (experiments A/B): 0 B = the block of the last byte (== A unless the
 // span crosses a 16-byte boundary); 1 B loaded only by the lanes whose span
-// crosses (the others copy A).  (Always loading the next block reads past
+// crosses (the others copy A); traffic ablations, hashes wrong: 2 the A
+// block only, 3 no text loads.  (Always loading the next block reads past
 // the buffer's last byte: not an option.)
 template <int SB = 0>
 __device__ __forceinline__ ShortRaw short_issue(const uint8_t* __restrict__ p, uint32_t D, bool load) {
@@ -591,10 +592,17 @@ __device__ __forceinline__ ShortRaw short_issue(const uint8_t* __restrict__ p, u
   r.s = a;
   r.D = load ? D : 0u;
   // pointer arithmetic (not integer masks) keeps these global loads
+  if constexpr (SB == 3) {  // traffic ablation (hashes wrong): no text loads at all
+    r.A = v4u{a, e, 0u, 0u};
+    r.B = r.A;
+    return r;
+  }
   r.A = *(const v4u*)(q - a);
   if constexpr (SB == 1) {
     r.B = r.A;
     if (a + e >= 16u) r.B = *(const v4u*)(q - a + 16);  // the last byte's block: in bounds
+  } else if constexpr (SB == 2) {  // traffic ablation (hashes wrong): the A block only
+    r.B = r.A;
   } else {
     r.B = *(const v4u*)(q + e - ((a + e) & 15u));
   }
@@ -1006,6 +1014,12 @@ int launch_spans(const void* buf, const uint64_t* offs, const uint32_t* lens, ui
   const int sk = g_tune_spans.load(std::memory_order_relaxed);
   if (tk && sk == 3)  // A/B: the second text block loaded only where the span crosses
     hipLaunchKernelGGL((k_spans<4, 2, 2, true, 1>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens,
+                       n, seed1, seed2, out, flags, dcount, tk);
+  else if (tk && sk == 4)  // traffic ablation (hashes wrong): the A block only
+    hipLaunchKernelGGL((k_spans<4, 2, 2, true, 2>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens,
+                       n, seed1, seed2, out, flags, dcount, tk);
+  else if (tk && sk == 5)  // traffic ablation (hashes wrong): no text loads on the short path
+    hipLaunchKernelGGL((k_spans<4, 2, 2, true, 3>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens,
                        n, seed1, seed2, out, flags, dcount, tk);
   else
 #endif

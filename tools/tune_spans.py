@@ -4,7 +4,9 @@ f3 text (1 GiB, ~25 % separators, ~200M tokens), outputs asserted equal:
 2 the product (wave tickets, two spans per lane, the short-key path and
 medium/long queues), 1 the static-order form, 0 lane per span; with the
 experiments build (KVH_LIB=tools/libkvh_exp.so) 3 = 2 with the short path's
-second text block loaded only where the span crosses a 16-byte boundary.
+second text block loaded only where the span crosses a 16-byte boundary;
+4 / 5 traffic ablations (outputs not hashes): the first text block only / no
+text loads on the short path.
 
     python tools/tune_spans.py [arms, default 2,3] [--once]
 
@@ -34,7 +36,7 @@ for rnd in range(1 if once else 3):
         kvh.meow128_spans(text, offs, lens, kvh.STATIC_SEED, out=out)
         torch.cuda.synchronize()
         if ref is None: ref = out.clone()
-        else: assert torch.equal(ref, out), v
+        elif v < 4: assert torch.equal(ref, out), v  # 4, 5: traffic ablations (not hashes)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
         for a, b in ev:
             a.record(st); kvh.meow128_spans(text, offs, lens, kvh.STATIC_SEED, out=out); b.record(st)
