@@ -525,7 +525,22 @@ k_keysrc(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, con
 }
 
 // hash the queued spans q[0 .. cnt) (cnt <= 64), lane per entry, runtime length
-template <int NT>
+// STASH: the span's (offset, length) was parked in its own output slot
+// out[j] when it was queued (k_spans' short-hash store, by this wave); read
+// it there (one slot) instead of offs[j] and lens[j] (two scattered lines).
+// The pop waits for the wave's stores (vmcnt(0)) and reads through L2.
+template <bool STASH>
+__device__ __forceinline__ void span_at(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
+                                        const uint64_t* out, uint64_t j, uint64_t* off, uint32_t* len) {
+  if constexpr (STASH) {  // agent-scope atomic loads: served by L2, never by a stale L1 line
+    *off = __hip_atomic_load(out + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *len = (uint32_t)__hip_atomic_load(out + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *off = offs[j];
+    *len = lens[j];
+  }
+}
+template <int NT, bool STASH = false>
 __device__ __forceinline__ void spans_long(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
                                            const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
                                            const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
@@ -535,8 +550,11 @@ __device__ __forceinline__ void spans_long(const uint8_t* __restrict__ buf, cons
     const uint32_t e = q[lane];
     const uint64_t j = qbase + (uint64_t)(e / CH) * step + (e % CH);
     KVH_CHK(j < nchk, kChkSpanIdx, j, nchk);
-    const uint8_t* p = buf + offs[j];
-    const uint32_t D = lens[j], H = D + nul;
+    uint64_t o;
+    uint32_t D;
+    span_at<STASH>(offs, lens, out, j, &o, &D);
+    const uint8_t* p = buf + o;
+    const uint32_t H = D + nul;
     const LdsK<LdsTab<NT>, uint32_t, MeowConstL> K(kfull, nullptr, H, s1, s2, T);
     const MaskLd ld{p + D};
     store_h(out, j, meow_rt<LdsTab<NT>, LdsK<LdsTab<NT>, uint32_t, MeowConstL>, MaskLd>(p, H, K, T, ld), fix);
@@ -696,7 +714,7 @@ __device__ __forceinline__ Blk meow_medium(const MedRaw& r, uint32_t L, uint32_t
 }
 
 // hash the queued medium spans q[0 .. cnt) (cnt <= 64), lane per entry
-template <int NT>
+template <int NT, bool STASH = false>
 __device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs,
                                              const uint32_t* __restrict__ lens, uint64_t* __restrict__ out,
                                              const uint32_t* q, uint32_t cnt, uint32_t lane, uint64_t qbase,
@@ -706,15 +724,18 @@ __device__ __forceinline__ void spans_medium(const uint8_t* __restrict__ buf, co
     const uint32_t e = q[lane];
     const uint64_t j = qbase + (uint64_t)(e / CH) * step + (e % CH);
     KVH_CHK(j < nchk, kChkSpanIdx, j, nchk);
-    const uint32_t L = lens[j], H = L + nul;
-    const MedRaw r = med_issue(buf + offs[j], L);
+    uint64_t o;
+    uint32_t L;
+    span_at<STASH>(offs, lens, out, j, &o, &L);
+    const uint32_t H = L + nul;
+    const MedRaw r = med_issue(buf + o, L);
     store_h(out, j, meow_medium(r, L, H, kfull[H], psel, T), fix);
   }
 }
 
 // Q: chunks in address order through wave tickets (tickets.hpp; n < 2^32 - 1,
 // the queues then hold span indices themselves)
-template <int NT, int NH, int PD = 2, bool Q = false, int SB = 0>
+template <int NT, int NH, int PD = 2, bool Q = false, int SB = 0, bool STASH = false>
 __global__ void __launch_bounds__(1024)
 k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
         uint64_t n, uint64_t s1, uint64_t s2, uint64_t* __restrict__ out, uint32_t flags,
@@ -774,6 +795,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   uint64_t mo[PD][NH];
   uint32_t mD[PD][NH];
   ShortRaw tr[2][NH];
+  uint64_t to[2][NH];  // STASH: the text offsets behind tr (dead code otherwise)
   // Q: cb[u] = base of the chunk whose offsets sit in slot u
   uint64_t cb[PD];
   if constexpr (Q) {
@@ -797,6 +819,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
     }
     tr[0][h] = short_issue<SB>(buf + o0, D0, b0 + 64 * h + lane < n && D0 && is_short(D0));
     tr[0][h].D = D0;  // the length rides with the blocks (0-byte spans load nothing)
+    to[0][h] = o0;
   }
   uint32_t it = 0;
   auto body = [&](uint64_t b, auto uc) {
@@ -815,6 +838,7 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
       const uint32_t D1 = mD[un][h];
       tr[x ^ 1][h] = short_issue<SB>(buf + mo[un][h], D1, bn + 64 * h + lane < n && D1 && is_short(D1));
       tr[x ^ 1][h].D = D1;
+      to[x ^ 1][h] = mo[un][h];
     }
     bool valid[NH], shrt[NH];
     Blk hh[NH];
@@ -839,9 +863,26 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
         const Blk S2 = aesdec(bxor(c.TG2, S3), M, T);
         hh[h] = aesdec(bxor(c.TCS0a, S2), M, T);
       }
+      if constexpr (!STASH) {
+#pragma unroll
+        for (int h = 0; h < NH; h++)
+          if (valid[h] && shrt[h]) store_h<true>(out, b + 64 * h + lane, hh[h], fix);  // streaming
+      }
+    }
+    if constexpr (STASH) {  // short lanes their hash, the queued ones their (offset, length): whole lines
 #pragma unroll
       for (int h = 0; h < NH; h++)
-        if (valid[h] && shrt[h]) store_h<true>(out, b + 64 * h + lane, hh[h], fix);  // streaming
+        if (valid[h]) {
+          v4u v;
+          if (shrt[h]) {
+            const Blk hx = fix ? fixup(hh[h]) : hh[h];
+            v.x = hx.w[0]; v.y = hx.w[1]; v.z = hx.w[2]; v.w = hx.w[3];
+          } else {
+            const uint64_t o = to[x][h];
+            v.x = (uint32_t)o; v.y = (uint32_t)(o >> 32); v.z = tr[x][h].D; v.w = 0u;
+          }
+          *(v4u*)(out + 2 * (b + 64 * h + lane)) = v;
+        }
     }
 #pragma unroll
     for (int h = 0; h < NH; h++) {
@@ -863,12 +904,17 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
     KVH_CHK(qn + ql <= QCAP, kChkSpanQueue, qn + ql, QCAP);
     if (qn >= 64 || ql >= 64) {
       wave_lds_sync();
+      if constexpr (STASH) {  // this wave's stash stores before its reads of them
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stash stores have reached L2
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
       while (qn >= 64) {
-        spans_medium<NT>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CHq, nul, fix, kfull, psel, T, n);
+        spans_medium<NT, STASH>(buf, offs, lens, out, q + qn - 64, 64, lane, qbase, step, CHq, nul, fix, kfull, psel, T, n);
         qn -= 64;
       }
       while (ql >= 64) {  // its newest 64 entries: q[QCAP - ql .. QCAP - ql + 64)
-        spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, 64, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T, n);
+        spans_long<NT, STASH>(buf, offs, lens, out, q + QCAP - ql, 64, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T, n);
         ql -= 64;
       }
       wave_lds_sync();
@@ -899,8 +945,13 @@ k_spans(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ offs, cons
   }
   if (qn || ql) {
     wave_lds_sync();
-    if (qn) spans_medium<NT>(buf, offs, lens, out, q, qn, lane, qbase, step, CHq, nul, fix, kfull, psel, T, n);
-    if (ql) spans_long<NT>(buf, offs, lens, out, q + QCAP - ql, ql, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T, n);
+    if constexpr (STASH) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the stash stores have reached L2
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    if (qn) spans_medium<NT, STASH>(buf, offs, lens, out, q, qn, lane, qbase, step, CHq, nul, fix, kfull, psel, T, n);
+    if (ql) spans_long<NT, STASH>(buf, offs, lens, out, q + QCAP - ql, ql, lane, qbase, step, CHq, nul, fix, kfull, s1, s2, T, n);
   }
   if constexpr (Q) wt_done(tk);
 }
@@ -1015,6 +1066,9 @@ int launch_spans(const void* buf, const uint64_t* offs, const uint32_t* lens, ui
   if (tk && sk == 3)  // A/B: the second text block loaded only where the span crosses
     hipLaunchKernelGGL((k_spans<4, 2, 2, true, 1>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens,
                        n, seed1, seed2, out, flags, dcount, tk);
+  else if (tk && sk == 6)  // A/B: queued spans' (offset, length) parked in their output slots
+    hipLaunchKernelGGL((k_spans<4, 2, 2, true, 0, true>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs,
+                       lens, n, seed1, seed2, out, flags, dcount, tk);
   else if (tk && sk == 4)  // traffic ablation (hashes wrong): the A block only
     hipLaunchKernelGGL((k_spans<4, 2, 2, true, 2>), dim3(grid), dim3(1024), 0, st, (const uint8_t*)buf, offs, lens,
                        n, seed1, seed2, out, flags, dcount, tk);

@@ -1193,7 +1193,7 @@ int kvh_set_tuning(int k, int value) {
     case 15: if (value < 1 || value > 1024) return KVH_EINVAL; return set(g_tune_pipe_mib, value);
     case 16: if (value < 2 || value > 16) return KVH_EINVAL; return set(g_tune_pipe_slots, value);
     case 17: if (value < 0 || value > 64) return KVH_EINVAL; return set(g_tune_sort_bits, value);
-    case 18: if (value < 0 || value > (kExperiments ? 5 : 2)) return KVH_EINVAL; return set(g_tune_spans, value);
+    case 18: if (value < 0 || value > (kExperiments ? 6 : 2)) return KVH_EINVAL; return set(g_tune_spans, value);
     case 19: if (value < 0 || value > 1) return KVH_EINVAL; return set(g_tune_tok, value);
     case 20: if (value < 0 || value > 2) return KVH_EINVAL; return set(g_tune_sort_engine, value);
     case 21: if (value < 0 || value > (1 << 20)) return KVH_EINVAL; return set(g_tune_tiny, value);
