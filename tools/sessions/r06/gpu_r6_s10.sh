@@ -21,4 +21,4 @@ for a in (2, 4, 5):
         agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     print(a, {k: round(sum(v) / len(v) * (32 if "32B" in k else 1) / 1e9, 3) for k, v in agg.items()}, len(rows))
 PY
-bash tools/sessions/gpu_r6_s9.sh || exit 1
+bash tools/sessions/r06/gpu_r6_s9.sh || exit 1

@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_sort.py tests/test_gpu_inge
 tail -1 $O/sort_tests.txt
 timeout -k 10 600 python -u bench.py --config f2 --steps 20 --warmup 5 > $O/bench_f2.json 2> $O/bench_f2.err || { echo "bench rc=$?"; tail -20 $O/bench_f2.err; exit 1; }
 python3 -c "import json; d=json.loads(open('$O/bench_f2.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['parity']['mismatches'], d['parity']['full_compare'])"
-bash tools/sessions/gpu_r6_g2.sh $O/g2 "f2" || { echo "profiles rc=$?"; exit 1; }
+bash tools/sessions/r06/gpu_r6_g2.sh $O/g2 "f2" || { echo "profiles rc=$?"; exit 1; }

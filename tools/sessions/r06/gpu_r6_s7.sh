@@ -8,4 +8,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 $O/gpu_tests.txt
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { echo "smoke rc=$?"; tail -5 $O/smoke.txt; exit 1; }
 tail -1 $O/smoke.txt
-bash tools/sessions/gpu_r6_g1.sh $O/final || exit 1
+bash tools/sessions/r06/gpu_r6_g1.sh $O/final || exit 1
